@@ -1,0 +1,159 @@
+"""North-star benchmark: MulticlassAccuracy metric-updates/sec on MI355X (BASELINE.json).
+
+Config (BASELINE.json "metric"): MulticlassAccuracy, bs=8192 per GPU, num_classes=1000,
+fp32 logits (the dtype of the reference measurement), synthetic data.  One step = one
+``metric.update(logits, target)`` on a fresh batch.  Weak scaling: every rank updates its own
+metric on its own batches; the timed region ends with ONE ``sync_and_compute`` (RCCL
+all-reduce of the metric state) so the reported number includes the distributed merge.
+
+Data: a pool of 8 distinct [8192, 1000] fp32 batches per GPU (262 MB, larger than the
+256 MiB Infinity Cache), rotated every step, so updates stream from HBM.
+
+Usage::
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...     (driver launches N > 1 this way)
+
+Rank 0 prints ONE JSON line.
+"""
+
+import argparse
+import json
+import os
+import time
+
+import torch
+import torch.distributed as dist
+
+BATCH = 8192
+NUM_CLASSES = 1000
+POOL = 8
+BASELINE_UPDATES_PER_S = 351.0  # reference MulticlassAccuracy.update bs=8192, C=1000
+
+
+def _reference_eager_rate(x_pool, y_pool, iters: int) -> float:
+    """The reference's update op chain (accuracy.py:250-278 + class :111-132) as eager ATen
+    on the same GPU, for context: argmax -> eq -> long -> sum, torch.tensor(N), two adds."""
+    dev = x_pool[0].device
+    num_correct = torch.tensor(0.0, device=dev)
+    num_total = torch.tensor(0.0, device=dev)
+
+    @torch.inference_mode()
+    def step(x, y):
+        nonlocal num_correct, num_total
+        x = x.to(dev)
+        y = y.to(dev)
+        pred = torch.argmax(x, dim=1)
+        mask = (pred == y).long()
+        c = mask.sum()
+        t = torch.tensor(y.shape[0])
+        num_correct += c
+        num_total += t
+
+    for i in range(20):
+        step(x_pool[i % POOL], y_pool[i % POOL])
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(iters):
+        step(x_pool[i % POOL], y_pool[i % POOL])
+    torch.cuda.synchronize()
+    return iters / (time.perf_counter() - t0)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20000)
+    ap.add_argument("--warmup", type=int, default=1000)
+    ap.add_argument("--no-reference", action="store_true", help="skip the eager-ATen context run")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    from torcheval_amd.metrics import MulticlassAccuracy
+    from torcheval_amd.metrics.toolkit import sync_and_compute
+    from torcheval_amd.parallel import init_from_env
+
+    dev = init_from_env(device_type="cuda") if world > 1 else torch.device("cuda", local_rank)
+    torch.cuda.set_device(dev)
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    x_pool = [torch.randn(BATCH, NUM_CLASSES, device=dev, generator=g) for _ in range(POOL)]
+    y_pool = [torch.randint(0, NUM_CLASSES, (BATCH,), device=dev, generator=g) for _ in range(POOL)]
+
+    metric = MulticlassAccuracy(device=dev)
+    for i in range(args.warmup):
+        metric.update(x_pool[i % POOL], y_pool[i % POOL])
+    if world > 1:
+        sync_and_compute(metric)
+    metric.reset()
+
+    def barrier():
+        if world > 1:
+            dist.barrier(device_ids=[dev.index])
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        metric.update(x_pool[i % POOL], y_pool[i % POOL])
+    acc = sync_and_compute(metric) if world > 1 else metric.compute()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    # correctness guard: the synced count must equal world * steps * batch
+    total = float(metric.num_total) if world == 1 else None
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    else:
+        assert total == args.steps * BATCH, (total, args.steps * BATCH)
+    acc_v = float(acc)
+    assert 0.0 <= acc_v <= 0.01, acc_v  # random logits: ~1/1000
+
+    ref_rate = None
+    if rank == 0 and not args.no_reference:
+        ref_rate = _reference_eager_rate(x_pool, y_pool, 2000)
+
+    if rank == 0:
+        updates_per_s = world * args.steps / elapsed
+        out = {
+            "metric": "metric-updates/sec (whole node) MulticlassAccuracy bs=8192 at 1/2/4/8 MI355X",
+            "value": round(updates_per_s, 2),
+            "unit": "updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 6),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(updates_per_s / BASELINE_UPDATES_PER_S, 2),
+            "dtype": "fp32",
+            "data": "synthetic (8-batch pool of randn logits / randint targets per GPU)",
+            "config": {
+                "model": "MulticlassAccuracy",
+                "global_batch": BATCH * world,
+                "seq_len": None,
+                "num_classes": NUM_CLASSES,
+                "batch_per_gpu": BATCH,
+                "average": "micro",
+                "parallelism": f"dp{world}",
+            },
+            "samples_per_s": round(updates_per_s * BATCH, 1),
+            "hbm_GBps_per_gpu": round(updates_per_s / world * BATCH * NUM_CLASSES * 4 / 1e9, 1),
+            "reference_eager_same_gpu_updates_per_s": None if ref_rate is None else round(ref_rate, 1),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,34 @@
+"""Distributed layer: one process per MI355X, RCCL (backend "nccl") over xGMI.
+
+* ``distributed`` — process-group helpers (PGWrapper, init_from_env, transport device).
+* ``collectives`` — bucketed all-reduce and packed all-gather-v of metric states.
+* ``state_sync`` — typed metric-state sync engine used by ``metrics.toolkit``.
+"""
+
+from torcheval_amd.parallel.collectives import (
+    all_gather_tensors,
+    allreduce_coalesced,
+    allreduce_coalesced_async,
+    packed_all_gather,
+)
+from torcheval_amd.parallel.distributed import (
+    get_local_rank,
+    get_rank,
+    get_world_size,
+    init_from_env,
+    PGWrapper,
+    transport_device,
+)
+
+__all__ = [
+    "PGWrapper",
+    "all_gather_tensors",
+    "allreduce_coalesced",
+    "allreduce_coalesced_async",
+    "get_local_rank",
+    "get_rank",
+    "get_world_size",
+    "init_from_env",
+    "packed_all_gather",
+    "transport_device",
+]

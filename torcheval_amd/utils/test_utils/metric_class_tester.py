@@ -1,0 +1,235 @@
+"""Generic conformance suite for class metrics.
+
+Behavioural parity with torcheval/utils/test_utils/metric_class_tester.py:52-383: for each
+device it checks (1) state registry, pickling, hashing and the state_dict round trip,
+(2) chained ``update().compute()`` and idempotent compute, (3) ``merge_state`` semantics
+(merge with fresh metrics, before/after updates, N-way merge equals the expected result,
+inputs of the merge untouched, metric still usable, cross-device merge) and, on CPU,
+(4) ``sync_and_compute`` across real processes over gloo.
+
+Differences: step (4) runs on a persistent worker pool (``dist_pool``) instead of a fresh
+elastic launch per test, and ``test_devices`` defaults to CPU plus the ROCm device when one
+is present (the GPU pass exercises the HIP kernels against the same expected values).
+"""
+
+import pickle
+import unittest
+from copy import deepcopy
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence, Set
+
+import torch
+
+from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.toolkit import clone_metric, sync_and_compute
+from torcheval_amd.utils.device import copy_data_to_device
+from torcheval_amd.utils.test_utils.dist_pool import run_distributed
+
+BATCH_SIZE = 16
+IMG_CHANNELS = 3
+IMG_WIDTH = 32
+IMG_HEIGHT = 32
+NUM_TOTAL_UPDATES = 8
+NUM_PROCESSES = 4
+
+
+@dataclass
+class _MetricClassTestCaseSpecs:
+    metric: Metric
+    state_names: Set[str]
+    update_kwargs: Dict[str, Any]
+    compute_result: Any
+    merge_and_compute_result: Any
+    num_total_updates: int = NUM_TOTAL_UPDATES
+    num_processes: int = NUM_PROCESSES
+    atol: float = 1e-8
+    rtol: float = 1e-5
+    min_updates_before_compute: int = 0
+    device: str = "cpu"
+
+
+def _kwargs_at(update_kwargs: Dict[str, Any], i: int) -> Dict[str, Any]:
+    return {k: v[i] for k, v in update_kwargs.items()}
+
+
+class MetricClassTester(unittest.TestCase):
+    def setUp(self) -> None:
+        self._test_case_spec: Optional[_MetricClassTestCaseSpecs] = None
+
+    def run_class_implementation_tests(
+        self,
+        metric: Metric,
+        state_names: Set[str],
+        update_kwargs: Dict[str, Any],
+        compute_result: Any,
+        merge_and_compute_result: Any = None,
+        num_total_updates: int = NUM_TOTAL_UPDATES,
+        num_processes: int = NUM_PROCESSES,
+        test_merge_with_one_update: bool = True,
+        min_updates_before_compute: int = 0,
+        atol: float = 1e-8,
+        rtol: float = 1e-5,
+        test_devices: Optional[List[str]] = None,
+    ) -> None:
+        """Run the full conformance suite (see module docstring)."""
+        self.assertTrue(update_kwargs)
+        self.assertTrue(state_names)
+        self.assertTrue(
+            all(len(v) == num_total_updates for v in update_kwargs.values()),
+            "The outer size of each update argument should be equal to number of updates",
+        )
+        self.assertGreater(num_total_updates, 1)
+        self.assertGreater(num_processes, 1)
+        self.assertEqual(num_total_updates % num_processes, 0)
+        if merge_and_compute_result is None:
+            merge_and_compute_result = compute_result
+        base = _MetricClassTestCaseSpecs(
+            metric,
+            state_names,
+            update_kwargs,
+            compute_result,
+            merge_and_compute_result,
+            num_total_updates,
+            num_processes,
+            atol,
+            rtol,
+            min_updates_before_compute,
+        )
+        if test_devices is None:
+            test_devices = ["cpu", "cuda"] if torch.cuda.is_available() else ["cpu"]
+        for device in test_devices:
+            spec = deepcopy(base)
+            spec.device = device
+            spec = copy_data_to_device(spec, torch.device(device))
+            self._test_case_spec = spec
+            self._test_init()
+            self._test_update_and_compute()
+            self._test_merge_state(test_merge_with_one_update)
+            if device == "cpu":
+                self._test_sync_and_compute()
+
+    # ------------------------------------------------------------------ phases
+    def _test_metric_pickable_hashable(self, metric: Metric) -> None:
+        loaded = pickle.loads(pickle.dumps(metric))
+        self.assert_state_unchanged(self._test_case_spec.state_names, loaded, metric)
+        self.assertTrue(hash(metric))
+
+    def _test_state_dict_load_state_dict(self, metric: Metric) -> None:
+        fresh = deepcopy(metric).reset()
+        fresh.load_state_dict(metric.state_dict())
+        self.assert_state_unchanged(self._test_case_spec.state_names, fresh, metric)
+
+    def _test_init(self) -> None:
+        spec = self._test_case_spec
+        self.assertEqual(set(spec.metric._state_name_to_default.keys()), spec.state_names)
+        self._test_metric_pickable_hashable(spec.metric)
+        self._test_state_dict_load_state_dict(spec.metric)
+
+    def _test_update_and_compute(self) -> None:
+        spec = self._test_case_spec
+        metric = deepcopy(spec.metric)
+        result = None
+        for i in range(spec.num_total_updates):
+            kwargs = _kwargs_at(spec.update_kwargs, i)
+            if i >= spec.min_updates_before_compute:
+                result = metric.update(**kwargs).compute()
+            else:
+                metric.update(**kwargs)
+        final = metric.compute()
+        assert_result_close(final, spec.compute_result, atol=spec.atol, rtol=spec.rtol)
+        assert_result_close(final, result)  # compute is idempotent
+        self._test_metric_pickable_hashable(metric)
+        self._test_state_dict_load_state_dict(metric)
+
+    def _test_merge_state(self, test_merge_with_one_update: bool) -> None:
+        spec = self._test_case_spec
+        nproc, ntotal = spec.num_processes, spec.num_total_updates
+        metrics: List[Metric] = [deepcopy(spec.metric) for _ in range(nproc)]
+        first = _kwargs_at(spec.update_kwargs, 0)
+
+        if test_merge_with_one_update:
+            expected = deepcopy(metrics[0]).update(**first).compute()
+            # merge an empty metric, then update
+            m0, m1 = deepcopy(metrics[0]), deepcopy(metrics[1])
+            m0.merge_state([m1])
+            assert_result_close(expected, m0.update(**first).compute())
+            # update, then merge an empty metric
+            m0, m1 = deepcopy(metrics[0]), deepcopy(metrics[1])
+            m0.update(**first)
+            m0.merge_state([m1])
+            assert_result_close(expected, m0.compute())
+            # merge an updated metric into an empty one
+            m0, m1 = deepcopy(metrics[0]), deepcopy(metrics[1])
+            m1.update(**first)
+            m0.merge_state([m1])
+            assert_result_close(expected, m0.compute())
+
+        per = ntotal // nproc
+        for i in range(nproc):
+            for j in range(per):
+                metrics[i].update(**_kwargs_at(spec.update_kwargs, i * per + j))
+                if j >= spec.min_updates_before_compute:
+                    metrics[i].compute()
+        unmerged = [deepcopy(m) for m in metrics]
+        final = metrics[0].merge_state(metrics[1:]).compute()
+        assert_result_close(final, spec.merge_and_compute_result, atol=spec.atol, rtol=spec.rtol)
+        for i in range(1, nproc):  # merge inputs unchanged
+            self.assert_state_unchanged(spec.state_names, unmerged[i], metrics[i])
+        torch.testing.assert_close(final, metrics[0].compute(), equal_nan=True)
+        self._test_metric_pickable_hashable(metrics[0])
+        self._test_state_dict_load_state_dict(metrics[0])
+        metrics[0].update(**first).compute()  # still usable after merge
+
+        if torch.cuda.is_available():  # merge across devices
+            copies = [deepcopy(m) for m in metrics]
+            past = spec.device
+            self.assertEqual(copies[0]._device.type, past)
+            copies[0].to("cuda").merge_state(copies[1:])
+            for i in range(1, nproc):
+                self.assert_state_unchanged(spec.state_names, copies[i], metrics[i])
+                self.assertEqual(copies[i]._device.type, past)
+            self.assertEqual(copies[0]._device.type, "cuda")
+
+    def _test_sync_and_compute(self) -> None:
+        spec = self._test_case_spec
+        results = run_distributed(_per_rank_sync_and_compute, spec.num_processes, spec)
+        assert_result_close(
+            results[0], spec.merge_and_compute_result, atol=spec.atol, rtol=spec.rtol
+        )
+        for r in results[1:]:  # identical on every rank
+            assert_result_close(r, results[0])
+
+    def assert_state_unchanged(self, state_names: Set[str], metric1: Metric, metric2: Metric) -> None:
+        for state in state_names:
+            assert_result_close(getattr(metric1, state), getattr(metric2, state))
+
+
+def _per_rank_sync_and_compute(rank: int, world_size: int, spec: _MetricClassTestCaseSpecs) -> Any:
+    metric = clone_metric(spec.metric)
+    per = spec.num_total_updates // world_size
+    for i in range(per):
+        metric.update(**_kwargs_at(spec.update_kwargs, rank * per + i))
+        if i >= spec.min_updates_before_compute:
+            metric.compute()
+    return sync_and_compute(metric)
+
+
+def assert_result_close(result: Any, expected_result: Any, atol: float = 1e-8, rtol: float = 1e-5) -> None:
+    tc = unittest.TestCase()
+    tc.assertEqual(type(result), type(expected_result))
+    if isinstance(result, torch.Tensor):
+        torch.testing.assert_close(result, expected_result, atol=atol, rtol=rtol, equal_nan=True)
+    elif isinstance(result, dict):
+        tc.assertEqual(set(result.keys()), set(expected_result.keys()))
+        for k in result:
+            assert_result_close(result[k], expected_result[k], atol, rtol)
+    elif isinstance(result, Sequence) and not isinstance(result, str):
+        tc.assertEqual(len(result), len(expected_result))
+        for a, b in zip(result, expected_result):
+            assert_result_close(a, b, atol, rtol)
+    elif isinstance(result, bool) or isinstance(result, int):
+        tc.assertEqual(result, expected_result)
+    elif isinstance(result, float):
+        torch.testing.assert_close(result, expected_result, atol=atol, rtol=rtol, equal_nan=True)
+    else:
+        raise ValueError("Compute result comparision is not supported.")
