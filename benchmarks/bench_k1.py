@@ -10,7 +10,11 @@ Reports (bs=8192, C=1000, fp32 unless --dtype):
 
 import argparse
 import json
+import os
+import sys
 import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 
@@ -71,6 +75,9 @@ def main():
         m.update(xs[k], ys[k])
 
     res["python_update_us"] = timeit(upd, 5000)
+    xt, yt = xs[0][:64].contiguous(), ys[0][:64].contiguous()
+    mt = MulticlassAccuracy(device=dev)
+    res["host_only_update_us"] = timeit(lambda: mt.update(xt, yt), 5000)
     out = torch.zeros(2, device=dev)
 
     def raw():

@@ -6,6 +6,9 @@
 // not assume, so no kernel ever runs with a mismatched grid.
 #include <torch/extension.h>
 
+#include <mutex>
+#include <unordered_map>
+
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
@@ -51,6 +54,24 @@ float* f32_out(const optional<Tensor>& t, const Tensor& ref, int64_t numel, cons
   TORCH_CHECK(x.numel() == numel, "torcheval_amd._C: ", name, " must have ", numel,
               " elements, got ", x.numel());
   return x.data_ptr<float>();
+}
+
+// Per-(device, stream) workspace for tea_fold.h: zeroed once, self-cleaning after every
+// launch, so all kernels on one stream can share it (stream order serialises them).
+// Allocate (warm up) before any HIP-graph capture that uses it.
+unsigned long long* fold_workspace(const Tensor& like, hipStream_t stream) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, Tensor> cache;
+  const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
+                       reinterpret_cast<uint64_t>(stream);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it == cache.end()) {
+    Tensor ws = at::zeros({16 * tea::kFoldCells},
+                          at::TensorOptions().dtype(at::kLong).device(like.device()));
+    it = cache.emplace(key, ws).first;
+  }
+  return reinterpret_cast<unsigned long long*>(it->second.data_ptr<int64_t>());
 }
 
 void check_launch(int rc, const char* what) {
@@ -109,7 +130,9 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
     a.check_target = 1;
   }
   a.max_blocks = static_cast<int>(max_blocks);
-  const int rc = tea::launch_cls_counts(a, stream_for(input));
+  const hipStream_t stream = stream_for(input);
+  if (a.micro_correct) a.fold_ws = fold_workspace(input, stream);
+  const int rc = tea::launch_cls_counts(a, stream);
   TORCH_CHECK(rc != -1, "cls_counts: unsupported input dtype ", input.scalar_type());
   check_launch(rc, "cls_counts");
 }

@@ -29,6 +29,7 @@ struct ClsCountsArgs {
   float* confusion = nullptr;    // [num_classes, num_classes] (target, pred)
   int* err = nullptr;            // error bits (1: bad target, 2: bad prediction)
   int check_target = 0;          // flag bad targets even without histograms
+  unsigned long long* fold_ws = nullptr;  // tea_fold.h cells (per-stream, self-cleaning)
   int max_blocks = 0;
 };
 int launch_cls_counts(const ClsCountsArgs& a, hipStream_t stream);

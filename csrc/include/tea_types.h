@@ -18,4 +18,7 @@ enum class DType : int {
   i16 = 9,
 };
 
+// fold workspace size in u64 cells (tea_fold.h: 64 shards x 64-B stride, 16 value slots)
+constexpr int kFoldCells = 64 * 8;
+
 }  // namespace tea

@@ -8,19 +8,23 @@
 // with ONE streaming pass over the [N, C] score matrix that writes straight into the metric
 // state tensors (no temporaries, no host syncs).
 //
-// Layout / mapping (gfx950):
-//  * one wave64 per row, grid-stride over rows; a row is read with 16-B loads per lane
-//    (float4 for f32, 8 x 16-bit for bf16/f16), four loads in flight per lane before the
-//    compare chain, so a 256-thread block keeps 16 KB of HBM reads outstanding.
-//  * argmax reduces (value, index) across the wave with xor-shuffles, torch.argmax tie/NaN
-//    semantics (first index, NaN is max).  top-k (k > 1) uses rank-of-target = #(x > x_t).
-//  * micro counts: per-block LDS reduction -> ONE float atomic per block.  Per-class
-//    histograms / confusion matrix: one lane per row issues the scatter atomics (targets are
-//    spread over C addresses, so contention is low).
+// Design (gfx950, measured with csrc/bench/k1_variants.hip at N=8192, C=1000, fp32):
+//  * "wide" kernel (C > 32): one wave64 per row.  Every lane issues ALL its 16-B loads of the
+//    row chunk (4 x float4 = 1024 f32 columns, or 4 x 8 x bf16 = 2048 columns) before any
+//    compare, and the grid is sized so every wave owns ~one row (2048 blocks x 4 waves for
+//    N=8192): the whole 32.8 MB read is in flight at once -> 4.5 TB/s.
+//  * two-phase argmax per lane: v_maximum3_f32 (NaN-propagating max) over the lane's values,
+//    then the first column equal to that max; the cross-lane step is a max-reduce followed by
+//    a min-reduce of candidate indices.  ~2.5 VALU per element instead of the ~12 of a
+//    (value, index) compare chain (10.5 -> 7.3 us).  Rows containing NaN take a wave-uniform
+//    slow path with exact torch.argmax semantics (NaN is the max, first index wins).
+//  * micro counts are folded with tea_fold.h (sharded 64-bit {arrivals, count} cells): one
+//    same-address float atomic per block costs +23 us at 2048 blocks, the fold +0.5 us.
+//  * "narrow" kernel (C <= 32): one thread per row, LDS-privatised class histograms.
 //  * invalid targets / predictions never fault: they are skipped and flagged in ``err``
-//    (bit 0: target out of range, bit 1: predicted label out of range); the Python layer
-//    checks the flag where the reference would have raised.
+//    (bit 0: target out of range, bit 1: predicted label out of range).
 #include "tea_common.h"
+#include "tea_fold.h"
 #include "tea_kernels.h"
 
 namespace tea {
@@ -29,39 +33,30 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
-constexpr int kUnroll = 4;
+constexpr int kChunkLoads = 4;  // 16-B loads per lane per row chunk
+constexpr int kNarrowMaxC = 32;
 
-template <int KIND, int VEC>
-struct RowLoader;
+__device__ __forceinline__ float fmaximum(float a, float b) {
+  return __builtin_elementwise_maximum(a, b);
+}
 
-// f32
-template <>
-struct RowLoader<0, 4> {
-  static __device__ __forceinline__ void load(const void* row, int col, float (&v)[4]) {
-    const float4 x = *reinterpret_cast<const float4*>(static_cast<const float*>(row) + col);
-    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
-  }
-  static __device__ __forceinline__ float one(const void* row, int64_t col) {
-    return static_cast<const float*>(row)[col];
-  }
-};
-template <>
-struct RowLoader<0, 1> {
-  static __device__ __forceinline__ void load(const void* row, int col, float (&v)[1]) {
-    v[0] = static_cast<const float*>(row)[col];
-  }
-  static __device__ __forceinline__ float one(const void* row, int64_t col) {
-    return static_cast<const float*>(row)[col];
-  }
-};
-// bf16 (KIND 1) / f16 (KIND 2)
 template <int KIND>
 __device__ __forceinline__ float h16(uint16_t b) {
   return KIND == 1 ? bf16_to_f32(b) : f16_to_f32(b);
 }
-template <int KIND>
-struct RowLoader16x8 {
-  static __device__ __forceinline__ void load(const void* row, int col, float (&v)[8]) {
+
+// KIND 0: f32 (VEC 4 or 1); KIND 1: bf16, KIND 2: f16 (VEC 8 or 1)
+template <int KIND, int VEC>
+__device__ __forceinline__ void load_vec(const void* row, int col, float (&v)[VEC]) {
+  if constexpr (KIND == 0 && VEC == 4) {
+    const float4 x = *reinterpret_cast<const float4*>(static_cast<const float*>(row) + col);
+    v[0] = x.x;
+    v[1] = x.y;
+    v[2] = x.z;
+    v[3] = x.w;
+  } else if constexpr (KIND == 0) {
+    v[0] = static_cast<const float*>(row)[col];
+  } else if constexpr (VEC == 8) {
     const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(row) + col);
     const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -69,185 +64,274 @@ struct RowLoader16x8 {
       v[2 * e] = h16<KIND>(static_cast<uint16_t>(w[e] & 0xffffu));
       v[2 * e + 1] = h16<KIND>(static_cast<uint16_t>(w[e] >> 16));
     }
-  }
-  static __device__ __forceinline__ float one(const void* row, int64_t col) {
-    return h16<KIND>(static_cast<const uint16_t*>(row)[col]);
-  }
-};
-template <>
-struct RowLoader<1, 8> : RowLoader16x8<1> {};
-template <>
-struct RowLoader<2, 8> : RowLoader16x8<2> {};
-template <int KIND>
-struct RowLoader16x1 {
-  static __device__ __forceinline__ void load(const void* row, int col, float (&v)[1]) {
+  } else {
     v[0] = h16<KIND>(static_cast<const uint16_t*>(row)[col]);
   }
-  static __device__ __forceinline__ float one(const void* row, int64_t col) {
-    return h16<KIND>(static_cast<const uint16_t*>(row)[col]);
-  }
-};
-template <>
-struct RowLoader<1, 1> : RowLoader16x1<1> {};
-template <>
-struct RowLoader<2, 1> : RowLoader16x1<2> {};
+}
+
+template <int KIND>
+__device__ __forceinline__ float load_one(const void* row, int64_t col) {
+  if constexpr (KIND == 0) return static_cast<const float*>(row)[col];
+  return h16<KIND>(static_cast<const uint16_t*>(row)[col]);
+}
 
 __device__ __forceinline__ int64_t load_target(const void* tgt, DType dt, int64_t i) {
   return dt == DType::i64 ? static_cast<const int64_t*>(tgt)[i] : load_as_i64(tgt, dt, i);
 }
 
-// Per-row bookkeeping shared by the score and label kernels (executed by one lane).
-__device__ __forceinline__ void row_epilogue(const ClsCountsArgs& a, int64_t t, int64_t pred,
-                                             bool correct) {
-  const int64_t C = a.num_classes;
+// Per-row bookkeeping (one lane / thread per row).  Histogram atomics go to ``hist`` which
+// is either global memory or an LDS privatisation (narrow kernel).
+struct Hist {
+  float* cls_correct;
+  float* cls_label;
+  float* cls_pred;
+  float* confusion;
+};
+
+__device__ __forceinline__ void row_hist(const Hist& h, int64_t C, int64_t t, int64_t pred,
+                                         bool correct, int* err, int check_target) {
   const bool t_ok = t >= 0 && t < C;
   const bool p_ok = pred >= 0 && pred < C;
-  if (a.err) {
-    if (!t_ok && (a.cls_label || a.cls_correct || a.confusion || a.check_target)) atomicOr(a.err, 1);
-    if (!p_ok && (a.cls_pred || a.confusion)) atomicOr(a.err, 2);
+  if (err) {
+    if (!t_ok && (h.cls_label || h.cls_correct || h.confusion || check_target)) atomicOr(err, 1);
+    if (!p_ok && (h.cls_pred || h.confusion)) atomicOr(err, 2);
   }
   if (t_ok) {
-    if (a.cls_correct && correct) atomicAdd(a.cls_correct + t, 1.f);
-    if (a.cls_label) atomicAdd(a.cls_label + t, 1.f);
+    if (h.cls_correct && correct) atomicAdd(h.cls_correct + t, 1.f);
+    if (h.cls_label) atomicAdd(h.cls_label + t, 1.f);
   }
-  if (p_ok && a.cls_pred) atomicAdd(a.cls_pred + pred, 1.f);
-  if (t_ok && p_ok && a.confusion) atomicAdd(a.confusion + t * C + pred, 1.f);
+  if (p_ok && h.cls_pred) atomicAdd(h.cls_pred + pred, 1.f);
+  if (t_ok && p_ok && h.confusion) atomicAdd(h.confusion + t * C + pred, 1.f);
 }
 
-__device__ __forceinline__ void block_flush_micro(const ClsCountsArgs& a, int correct_lane0) {
-  __shared__ int lds[kWavesPerBlock];
-  if (lane_id() == 0) lds[threadIdx.x >> 6] = correct_lane0;
+// Block epilogue for the micro counters: LDS reduce, then the sharded fold.
+__device__ __forceinline__ void block_micro(const ClsCountsArgs& a, uint32_t my_correct) {
+  __shared__ uint32_t lds[kWavesPerBlock];
+  const uint32_t w = static_cast<uint32_t>(wave_sum(static_cast<int>(my_correct)));
+  if (lane_id() == 0) lds[threadIdx.x >> 6] = w;
   __syncthreads();
   if (threadIdx.x == 0) {
-    int s = 0;
+    uint32_t s = 0;
 #pragma unroll
-    for (int w = 0; w < kWavesPerBlock; ++w) s += lds[w];
-    if (a.micro_correct && s) atomicAdd(a.micro_correct, static_cast<float>(s));
+    for (int k = 0; k < kWavesPerBlock; ++k) s += lds[k];
+    if (a.micro_correct) {
+      if (a.fold_ws) {
+        fold_count(a.fold_ws, s, a.micro_correct);
+      } else if (s) {
+        atomicAdd(a.micro_correct, static_cast<float>(s));
+      }
+    }
     if (a.micro_total && blockIdx.x == 0) atomicAdd(a.micro_total, static_cast<float>(a.n));
   }
 }
 
+// Exact torch.argmax over one row (slow path, NaN-aware compare chain).
+template <int KIND>
+__device__ __noinline__ int row_argmax_exact(const void* rp, int C, int lane) {
+  float bv = -__builtin_huge_valf();
+  int bi = 0x7fffffff;
+  for (int col = lane; col < C; col += kWave) {
+    const float v = load_one<KIND>(rp, col);
+    if (argmax_better(v, col, bv, bi)) {
+      bv = v;
+      bi = col;
+    }
+  }
+  wave_argmax(bv, bi);
+  return bi;
+}
+
 template <int KIND, int VEC, bool TOPK>
-__global__ __launch_bounds__(kBlock) void cls_scores_kernel(ClsCountsArgs a) {
-  using L = RowLoader<KIND, VEC>;
+__global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
   const int lane = lane_id();
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  const int elsize = KIND == 0 ? 4 : 2;
+  constexpr int ELSIZE = KIND == 0 ? 4 : 2;
+  constexpr int STEP = kWave * VEC;             // columns per wave-load
+  constexpr int CHUNK = STEP * kChunkLoads;     // columns per chunk
   const int C = static_cast<int>(a.c);
-  int correct_acc = 0;
+  const Hist h{a.cls_correct, a.cls_label, a.cls_pred, a.confusion};
+  uint32_t correct_acc = 0;
 
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id(); row < a.n;
        row += nwaves) {
-    const void* rp = static_cast<const char*>(a.input) + row * a.row_stride * elsize;
+    const void* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELSIZE;
     const int64_t t = load_target(a.target, a.tg_dt, row);
     bool correct;
     int64_t pred = -1;
     if constexpr (!TOPK) {
       float bv = -__builtin_huge_valf();
       int bi = 0x7fffffff;
-      constexpr int STEP = kWave * VEC;
-      for (int base = 0; base < C; base += STEP * kUnroll) {
-        float v[kUnroll][VEC];
-        bool ok[kUnroll];
+      bool saw_nan = false;
+      for (int base = 0; base < C; base += CHUNK) {
+        float v[kChunkLoads][VEC];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kChunkLoads; ++u) {
           const int col = base + u * STEP + lane * VEC;
-          ok[u] = col < C;
-          if (ok[u]) L::load(rp, col, v[u]);
-        }
+          if (col < C) {
+            load_vec<KIND, VEC>(rp, col, v[u]);
+          } else {
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          if (ok[u]) {
-            const int col = base + u * STEP + lane * VEC;
-#pragma unroll
-            for (int e = 0; e < VEC; ++e)
-              if (argmax_better(v[u][e], col + e, bv, bi)) {
-                bv = v[u][e];
-                bi = col + e;
-              }
+            for (int e = 0; e < VEC; ++e) v[u][e] = -__builtin_huge_valf();
           }
         }
+        // phase 1: NaN-propagating lane max; phase 2: first column holding it
+        float m = v[0][0];
+#pragma unroll
+        for (int u = 0; u < kChunkLoads; ++u)
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) m = fmaximum(m, v[u][e]);
+        int idx = 0x7fffffff;
+#pragma unroll
+        for (int u = kChunkLoads - 1; u >= 0; --u)
+#pragma unroll
+          for (int e = VEC - 1; e >= 0; --e)
+            idx = (v[u][e] == m) ? (base + u * STEP + lane * VEC + e) : idx;
+        saw_nan |= (m != m);
+        // columns of this chunk are all larger than earlier chunks': strict > keeps the first
+        if (m > bv || bi == 0x7fffffff) {
+          bv = m;
+          bi = idx;
+        }
       }
-      wave_argmax(bv, bi);
-      pred = bi;
+      // cross-lane: max value, then smallest index among the lanes holding it
+      float wm = bv;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wm = fmaximum(wm, __shfl_xor(wm, o, kWave));
+      int widx = (bv == wm) ? bi : 0x7fffffff;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) widx = min(widx, __shfl_xor(widx, o, kWave));
+      if (__builtin_expect(__any(saw_nan), 0)) widx = row_argmax_exact<KIND>(rp, C, lane);
+      pred = widx;
       correct = pred == t;
     } else {
       const bool t_ok = t >= 0 && t < C;
-      const float xt = t_ok ? L::one(rp, t) : __builtin_nanf("");
+      const float xt = t_ok ? load_one<KIND>(rp, t) : __builtin_nanf("");
       int cnt = 0;
-      constexpr int STEP = kWave * VEC;
-      for (int base = 0; base < C; base += STEP * kUnroll) {
-        float v[kUnroll][VEC];
-        bool ok[kUnroll];
+      for (int base = 0; base < C; base += CHUNK) {
+        float v[kChunkLoads][VEC];
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
+        for (int u = 0; u < kChunkLoads; ++u) {
           const int col = base + u * STEP + lane * VEC;
-          ok[u] = col < C;
-          if (ok[u]) L::load(rp, col, v[u]);
+          if (col < C) {
+            load_vec<KIND, VEC>(rp, col, v[u]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) v[u][e] = -__builtin_huge_valf();
+          }
         }
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u)
-          if (ok[u]) {
+        for (int u = 0; u < kChunkLoads; ++u)
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) cnt += v[u][e] > xt;
-          }
+          for (int e = 0; e < VEC; ++e) cnt += v[u][e] > xt;
       }
       cnt = wave_sum(cnt);
       correct = t_ok && cnt < a.k;
     }
     if (lane == 0) {
       correct_acc += correct;
-      row_epilogue(a, t, pred, correct);
+      row_hist(h, a.num_classes, t, pred, correct, a.err, a.check_target);
     }
   }
-  block_flush_micro(a, correct_acc);
+  block_micro(a, correct_acc);
+}
+
+// Narrow rows (C <= 32): one thread per row, class histograms privatised in LDS.
+template <int KIND, bool TOPK>
+__global__ __launch_bounds__(kBlock) void cls_narrow_kernel(ClsCountsArgs a) {
+  constexpr int ELSIZE = KIND == 0 ? 4 : 2;
+  __shared__ float s_correct[kNarrowMaxC], s_label[kNarrowMaxC], s_pred[kNarrowMaxC];
+  __shared__ float s_conf[kNarrowMaxC * kNarrowMaxC];
+  const int C = static_cast<int>(a.c);
+  for (int i = threadIdx.x; i < C * C; i += kBlock) s_conf[i] = 0.f;
+  if (threadIdx.x < kNarrowMaxC) {
+    s_correct[threadIdx.x] = 0.f;
+    s_label[threadIdx.x] = 0.f;
+    s_pred[threadIdx.x] = 0.f;
+  }
+  __syncthreads();
+  const Hist lh{a.cls_correct ? s_correct : nullptr, a.cls_label ? s_label : nullptr,
+                a.cls_pred ? s_pred : nullptr, a.confusion ? s_conf : nullptr};
+  uint32_t correct_acc = 0;
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; row < a.n;
+       row += stride) {
+    const void* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELSIZE;
+    const int64_t t = load_target(a.target, a.tg_dt, row);
+    bool correct;
+    int64_t pred = -1;
+    if constexpr (!TOPK) {
+      float bv = -__builtin_huge_valf();
+      int bi = 0x7fffffff;
+      for (int c = 0; c < C; ++c) {
+        const float v = load_one<KIND>(rp, c);
+        if (argmax_better(v, c, bv, bi)) {
+          bv = v;
+          bi = c;
+        }
+      }
+      pred = bi;
+      correct = pred == t;
+    } else {
+      const bool t_ok = t >= 0 && t < C;
+      const float xt = t_ok ? load_one<KIND>(rp, t) : __builtin_nanf("");
+      int cnt = 0;
+      for (int c = 0; c < C; ++c) cnt += load_one<KIND>(rp, c) > xt;
+      correct = t_ok && cnt < a.k;
+    }
+    correct_acc += correct;
+    row_hist(lh, C, t, pred, correct, a.err, a.check_target);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += kBlock) {
+    if (a.cls_correct && s_correct[i] != 0.f) atomicAdd(a.cls_correct + i, s_correct[i]);
+    if (a.cls_label && s_label[i] != 0.f) atomicAdd(a.cls_label + i, s_label[i]);
+    if (a.cls_pred && s_pred[i] != 0.f) atomicAdd(a.cls_pred + i, s_pred[i]);
+  }
+  if (a.confusion)
+    for (int i = threadIdx.x; i < C * C; i += kBlock)
+      if (s_conf[i] != 0.f) atomicAdd(a.confusion + i, s_conf[i]);
+  block_micro(a, correct_acc);
 }
 
 // 1-D integer label predictions: elementwise compare + histograms.
 __global__ __launch_bounds__(kBlock) void cls_labels_kernel(ClsCountsArgs a) {
-  int correct_acc = 0;
+  const Hist h{a.cls_correct, a.cls_label, a.cls_pred, a.confusion};
+  uint32_t correct_acc = 0;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
     const int64_t p = load_as_i64(a.input, a.in_dt, i);
     const int64_t t = load_target(a.target, a.tg_dt, i);
     const bool correct = p == t;
     correct_acc += correct;
-    row_epilogue(a, t, p, correct);
+    row_hist(h, a.num_classes, t, p, correct, a.err, a.check_target);
   }
-  correct_acc = wave_sum(correct_acc);
-  block_flush_micro(a, correct_acc);
+  block_micro(a, correct_acc);
 }
 
 // Binary: thresholded scores vs targets -> [tp, fp, tn, fn] (+ optional weights).
 __global__ __launch_bounds__(kBlock) void binary_counts_kernel(BinaryCountsArgs a) {
-  float tp = 0.f, fp = 0.f, tn = 0.f, fn = 0.f;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
     const float x = load_as_f32(a.input, a.in_dt, i);
     const double t = load_as_f64(a.target, a.tg_dt, i);
-    const int pred = (x < a.threshold) ? 0 : 1;
     const float w = a.weight ? load_as_f32(a.weight, a.w_dt, i) : 1.f;
-    if (pred == 1) {
-      if (t == 1.0) tp += w;
-      else if (t == 0.0) fp += w;
-      else fp += a.strict_binary ? 0.f : w;
+    const bool pos = !(x < a.threshold);
+    const bool t1 = t == 1.0, t0 = t == 0.0;
+    const float other = a.strict_binary ? 0.f : w;
+    if (pos) {
+      acc[0] += t1 ? w : 0.f;
+      acc[1] += t0 ? w : (t1 ? 0.f : other);
     } else {
-      if (t == 0.0) tn += w;
-      else if (t == 1.0) fn += w;
-      else fn += a.strict_binary ? 0.f : w;
+      acc[2] += t0 ? w : 0.f;
+      acc[3] += t1 ? w : (t0 ? 0.f : other);
     }
   }
-  tp = wave_sum(tp);
-  fp = wave_sum(fp);
-  tn = wave_sum(tn);
-  fn = wave_sum(fn);
   __shared__ float lds[4][kWavesPerBlock];
-  if (lane_id() == 0) {
-    const int w = threadIdx.x >> 6;
-    lds[0][w] = tp;
-    lds[1][w] = fp;
-    lds[2][w] = tn;
-    lds[3][w] = fn;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float s = wave_sum(acc[j]);
+    if (lane_id() == 0) lds[j][threadIdx.x >> 6] = s;
   }
   __syncthreads();
   if (threadIdx.x < 4) {
@@ -261,43 +345,47 @@ __global__ __launch_bounds__(kBlock) void binary_counts_kernel(BinaryCountsArgs 
 }
 
 template <int KIND, int VEC>
-void launch_scores(const ClsCountsArgs& a, int grid, hipStream_t s) {
+void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
   if (a.k > 1)
-    hipLaunchKernelGGL((cls_scores_kernel<KIND, VEC, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, true>), dim3(grid), dim3(kBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((cls_scores_kernel<KIND, VEC, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, false>), dim3(grid), dim3(kBlock), 0, s, a);
+}
+
+template <int KIND>
+void launch_narrow(const ClsCountsArgs& a, int grid, hipStream_t s) {
+  if (a.k > 1)
+    hipLaunchKernelGGL((cls_narrow_kernel<KIND, true>), dim3(grid), dim3(kBlock), 0, s, a);
+  else
+    hipLaunchKernelGGL((cls_narrow_kernel<KIND, false>), dim3(grid), dim3(kBlock), 0, s, a);
 }
 
 }  // namespace
 
 int launch_cls_counts(const ClsCountsArgs& a, hipStream_t stream) {
-  if (a.n <= 0) {
-    return 0;
-  }
-  const int cap = a.max_blocks > 0 ? a.max_blocks : 1024;
+  if (a.n <= 0) return 0;
   if (a.c > 0) {
-    const int grid = stream_grid(a.n, kWavesPerBlock, cap);
     const uintptr_t base = reinterpret_cast<uintptr_t>(a.input);
-    switch (a.in_dt) {
-      case DType::f32: {
-        const bool vec = (a.c % 4 == 0) && (a.row_stride % 4 == 0) && (base % 16 == 0);
-        vec ? launch_scores<0, 4>(a, grid, stream) : launch_scores<0, 1>(a, grid, stream);
-        break;
-      }
-      case DType::bf16: {
-        const bool vec = (a.c % 8 == 0) && (a.row_stride % 8 == 0) && (base % 16 == 0);
-        vec ? launch_scores<1, 8>(a, grid, stream) : launch_scores<1, 1>(a, grid, stream);
-        break;
-      }
-      case DType::f16: {
-        const bool vec = (a.c % 8 == 0) && (a.row_stride % 8 == 0) && (base % 16 == 0);
-        vec ? launch_scores<2, 8>(a, grid, stream) : launch_scores<2, 1>(a, grid, stream);
-        break;
-      }
-      default:
-        return -1;  // caller falls back / converts
+    const int kind = a.in_dt == DType::f32 ? 0 : a.in_dt == DType::bf16 ? 1 : a.in_dt == DType::f16 ? 2 : -1;
+    if (kind < 0) return -1;
+    if (a.c <= kNarrowMaxC) {
+      const int cap = a.max_blocks > 0 ? a.max_blocks : 512;
+      const int grid = stream_grid(a.n, kBlock, cap);
+      if (kind == 0) launch_narrow<0>(a, grid, stream);
+      else if (kind == 1) launch_narrow<1>(a, grid, stream);
+      else launch_narrow<2>(a, grid, stream);
+    } else {
+      // one wave per row up to 8 waves/SIMD residency (2048 blocks of 4 waves)
+      const int cap = a.max_blocks > 0 ? a.max_blocks : 2048;
+      const int grid = stream_grid(a.n, kWavesPerBlock, cap);
+      const int vw = kind == 0 ? 4 : 8;
+      const bool vec = (a.c % vw == 0) && (a.row_stride % vw == 0) && (base % 16 == 0);
+      if (kind == 0) vec ? launch_wide<0, 4>(a, grid, stream) : launch_wide<0, 1>(a, grid, stream);
+      else if (kind == 1) vec ? launch_wide<1, 8>(a, grid, stream) : launch_wide<1, 1>(a, grid, stream);
+      else vec ? launch_wide<2, 8>(a, grid, stream) : launch_wide<2, 1>(a, grid, stream);
     }
   } else {
+    const int cap = a.max_blocks > 0 ? a.max_blocks : 1024;
     const int grid = stream_grid(a.n, kBlock, cap);
     hipLaunchKernelGGL(cls_labels_kernel, dim3(grid), dim3(kBlock), 0, stream, a);
   }
@@ -306,7 +394,7 @@ int launch_cls_counts(const ClsCountsArgs& a, hipStream_t stream) {
 
 int launch_binary_counts(const BinaryCountsArgs& a, hipStream_t stream) {
   if (a.n <= 0) return 0;
-  const int cap = a.max_blocks > 0 ? a.max_blocks : 1024;
+  const int cap = a.max_blocks > 0 ? a.max_blocks : 256;
   const int grid = stream_grid(a.n, kBlock * 4, cap);
   hipLaunchKernelGGL(binary_counts_kernel, dim3(grid), dim3(kBlock), 0, stream, a);
   return static_cast<int>(hipGetLastError());

@@ -118,3 +118,20 @@ def test_binary_counts(tdtype):
     ref = torch.stack([(w * (p & tb)).sum(), (w * (p & ~tb)).sum(), (w * (~p & ~tb)).sum(),
                        (w * (~p & tb)).sum(), torch.tensor(100003.0)])
     torch.testing.assert_close(buf.cpu(), ref, rtol=1e-5, atol=1e-2)
+
+
+@pytest.mark.parametrize("n,c", [(8192, 1000), (100000, 64), (3, 1000), (70000, 33), (5000, 10)])
+def test_micro_fold_accumulates_exactly(n, c):
+    # many back-to-back launches sharing the per-stream fold workspace must count exactly
+    g = torch.Generator().manual_seed(n + c)
+    x = torch.randn(n, c, generator=g)
+    y = torch.randint(0, c, (n,), generator=g)
+    x[:, 0] = torch.where(torch.rand(n, generator=g) < 0.3, 100.0, x[:, 0])  # many correct rows
+    exp = (x.argmax(1) == y).sum().item()
+    out = torch.zeros(2, device=DEV)
+    xd, yd = x.to(DEV), y.to(DEV)
+    for _ in range(25):
+        cls_counts(xd, yd, num_classes=c, micro_correct=out[0:1], micro_total=out[1:2])
+    torch.cuda.synchronize()
+    assert out[0].item() == 25 * exp
+    assert out[1].item() == 25 * n
