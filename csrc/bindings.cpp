@@ -83,7 +83,9 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
                 const optional<Tensor>& micro_correct, const optional<Tensor>& micro_total,
                 const optional<Tensor>& cls_correct, const optional<Tensor>& cls_label,
                 const optional<Tensor>& cls_pred, const optional<Tensor>& confusion,
-                const optional<Tensor>& err, int64_t max_blocks) {
+                const optional<Tensor>& err, int64_t max_blocks,
+                const optional<Tensor>& micro_incorrect, const optional<Tensor>& micro_total2,
+                const optional<Tensor>& cls_fp) {
   check_gpu(input, "input");
   check_gpu(target, "target");
   TORCH_CHECK(target.dim() == 1, "cls_counts: target must be 1-D");
@@ -119,9 +121,13 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
   a.cls_label = f32_out(cls_label, input, C, "cls_label");
   a.cls_pred = f32_out(cls_pred, input, C, "cls_pred");
   a.confusion = f32_out(confusion, input, C * C, "confusion");
-  TORCH_CHECK(!(k > 1 && (a.cls_pred || a.confusion)),
+  a.micro_incorrect = f32_out(micro_incorrect, input, 1, "micro_incorrect");
+  a.micro_total2 = f32_out(micro_total2, input, 1, "micro_total2");
+  a.cls_fp = f32_out(cls_fp, input, C, "cls_fp");
+  TORCH_CHECK(!(k > 1 && (a.cls_pred || a.confusion || a.cls_fp)),
               "cls_counts: predictions are undefined for k > 1");
-  TORCH_CHECK((a.cls_correct || a.cls_label || a.cls_pred || a.confusion) == false || C > 0,
+  TORCH_CHECK((a.cls_correct || a.cls_label || a.cls_pred || a.confusion || a.cls_fp) == false ||
+                  C > 0,
               "cls_counts: num_classes required for histograms");
   if (err.has_value()) {
     TORCH_CHECK(err->scalar_type() == at::kInt && err->numel() >= 1 && err->device() == input.device(),
@@ -131,7 +137,7 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
   }
   a.max_blocks = static_cast<int>(max_blocks);
   const hipStream_t stream = stream_for(input);
-  if (a.micro_correct) a.fold_ws = fold_workspace(input, stream);
+  if (a.micro_correct || a.micro_incorrect) a.fold_ws = fold_workspace(input, stream);
   const int rc = tea::launch_cls_counts(a, stream);
   TORCH_CHECK(rc != -1, "cls_counts: unsupported input dtype ", input.scalar_type());
   check_launch(rc, "cls_counts");
@@ -140,7 +146,9 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
 void binary_counts(const Tensor& input, const Tensor& target, const optional<Tensor>& weight,
                    double threshold, const optional<Tensor>& tp, const optional<Tensor>& fp,
                    const optional<Tensor>& tn, const optional<Tensor>& fn,
-                   const optional<Tensor>& total, int64_t strict, int64_t max_blocks) {
+                   const optional<Tensor>& total, int64_t strict, int64_t max_blocks,
+                   const optional<Tensor>& tp2, const optional<Tensor>& fp2,
+                   const optional<Tensor>& tn2, const optional<Tensor>& fn2) {
   check_gpu(input, "input");
   check_gpu(target, "target");
   TORCH_CHECK(input.numel() == target.numel(), "binary_counts: size mismatch");
@@ -167,8 +175,217 @@ void binary_counts(const Tensor& input, const Tensor& target, const optional<Ten
   a.out[2] = f32_out(tn, input, 1, "tn");
   a.out[3] = f32_out(fn, input, 1, "fn");
   a.total = f32_out(total, input, 1, "total");
+  a.out2[0] = f32_out(tp2, input, 1, "tp2");
+  a.out2[1] = f32_out(fp2, input, 1, "fp2");
+  a.out2[2] = f32_out(tn2, input, 1, "tn2");
+  a.out2[3] = f32_out(fn2, input, 1, "fn2");
   a.max_blocks = static_cast<int>(max_blocks);
   check_launch(tea::launch_binary_counts(a, stream_for(input)), "binary_counts");
+}
+
+// ---------------------------------------------------------------- K3 sort-scan
+// sorted/order: [rows, n] (descending scores and their permutation); target: [rows, n] binary
+// targets or (class_mode) [n] labels; weight: optional [rows, n]; outputs float64 [rows].
+void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
+              const optional<Tensor>& weight, bool class_mode, const optional<Tensor>& out_auroc,
+              const optional<Tensor>& out_auprc) {
+  check_gpu(sorted, "sorted");
+  TORCH_CHECK(sorted.dim() == 2 && order.dim() == 2 && sorted.sizes() == order.sizes(),
+              "auc_scan: sorted/order must be [rows, n]");
+  TORCH_CHECK(sorted.stride(1) == 1 && order.stride(1) == 1, "auc_scan: rows must be contiguous");
+  TORCH_CHECK(sorted.scalar_type() == at::kFloat || sorted.scalar_type() == at::kDouble,
+              "auc_scan: scores must be float32/float64");
+  TORCH_CHECK(order.scalar_type() == at::kLong, "auc_scan: order must be int64");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
+  const int64_t rows = sorted.size(0), n = sorted.size(1);
+  tea::AucScanArgs a;
+  a.sorted = sorted.data_ptr();
+  a.key_dt = dt_of(sorted);
+  a.key_stride = sorted.stride(0);
+  a.order = order.data_ptr<int64_t>();
+  a.order_stride = order.stride(0);
+  Tensor tg = target;
+  if (class_mode) {
+    TORCH_CHECK(tg.dim() == 1 && tg.size(0) == n, "auc_scan: class-mode target must be [n]");
+    tg = tg.contiguous();
+  } else {
+    TORCH_CHECK(tg.dim() == 2 && tg.size(0) == rows && tg.size(1) == n,
+                "auc_scan: target must be [rows, n]");
+    if (tg.stride(1) != 1) tg = tg.contiguous();
+    a.target_stride = tg.stride(0);
+  }
+  a.target = tg.data_ptr();
+  a.tg_dt = dt_of(tg);
+  Tensor w;
+  if (weight.has_value()) {
+    w = *weight;
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == rows && w.size(1) == n, "auc_scan: weight must be [rows, n]");
+    if (w.stride(1) != 1) w = w.contiguous();
+    a.weight = w.data_ptr();
+    a.w_dt = dt_of(w);
+    a.weight_stride = w.stride(0);
+  }
+  a.class_mode = class_mode ? 1 : 0;
+  a.rows = rows;
+  a.n = n;
+  auto f64_out = [&](const optional<Tensor>& t, const char* name) -> double* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kDouble && t->is_contiguous() && t->numel() == rows &&
+                    t->device() == sorted.device(),
+                "auc_scan: ", name, " must be a contiguous float64 [rows] tensor");
+    return t->data_ptr<double>();
+  };
+  a.out_auroc = f64_out(out_auroc, "out_auroc");
+  a.out_auprc = f64_out(out_auprc, "out_auprc");
+  Tensor ws = at::empty({tea::auc_scan_workspace_bytes(rows, n)},
+                        at::TensorOptions().dtype(at::kByte).device(sorted.device()));
+  check_launch(tea::launch_auc_scan(a, ws.data_ptr(), stream_for(sorted)), "auc_scan");
+}
+
+// ---------------------------------------------------------------- K4 binned histograms
+// input: [n, c] view (any strides); target: [n, c] view (mode 0) or [n] labels (mode 1);
+// thr: float32 [T] sorted; tp/fp/fn: float32 [T, c] views sharing strides (accumulated).
+void binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr, int64_t mode,
+                   const optional<Tensor>& tp, const optional<Tensor>& fp,
+                   const optional<Tensor>& fn) {
+  check_gpu(input, "input");
+  TORCH_CHECK(input.dim() == 2, "binned_counts: input must be a 2-D view [n, c]");
+  TORCH_CHECK(thr.dim() == 1 && thr.scalar_type() == at::kFloat && thr.is_contiguous(),
+              "binned_counts: thresholds must be a contiguous float32 vector");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(input.device());
+  tea::BinnedArgs a;
+  a.input = input.data_ptr();
+  a.in_dt = dt_of(input);
+  a.n = input.size(0);
+  a.c = input.size(1);
+  a.in_row_stride = input.stride(0);
+  a.in_col_stride = input.stride(1);
+  a.mode = static_cast<int>(mode);
+  if (mode == 1) {
+    TORCH_CHECK(target.dim() == 1 && target.size(0) == a.n, "binned_counts: labels must be [n]");
+    a.tg_row_stride = target.stride(0);
+  } else {
+    TORCH_CHECK(target.dim() == 2 && target.size(0) == a.n && target.size(1) == a.c,
+                "binned_counts: target must match input");
+    a.tg_row_stride = target.stride(0);
+    a.tg_col_stride = target.stride(1);
+  }
+  a.target = target.data_ptr();
+  a.tg_dt = dt_of(target);
+  a.thr = thr.data_ptr<float>();
+  a.T = static_cast<int>(thr.numel());
+  int64_t ks = -1, cs = -1;
+  auto out = [&](const optional<Tensor>& t, const char* name) -> float* {
+    if (!t.has_value()) return nullptr;
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->dim() == 2 && t->size(0) == a.T &&
+                    t->size(1) == a.c && t->device() == input.device(),
+                "binned_counts: ", name, " must be float32 [T, c] on the input device");
+    TORCH_CHECK(ks < 0 || (ks == t->stride(0) && cs == t->stride(1)),
+                "binned_counts: outputs must share strides");
+    ks = t->stride(0);
+    cs = t->stride(1);
+    return t->data_ptr<float>();
+  };
+  a.tp = out(tp, "tp");
+  a.fp = out(fp, "fp");
+  a.fn = out(fn, "fn");
+  a.out_k_stride = ks;
+  a.out_c_stride = cs;
+  Tensor hist = at::zeros({(a.T + 1) * a.c * 2},
+                          at::TensorOptions().dtype(at::kFloat).device(input.device()));
+  a.hist = hist.data_ptr<float>();
+  const int rc = tea::launch_binned(a, stream_for(input));
+  TORCH_CHECK(rc != -1, "binned_counts: too many thresholds (", a.T, ") for the LDS histogram");
+  check_launch(rc, "binned_counts");
+}
+
+// ---------------------------------------------------------------- K5 / K6 reductions
+// x, t: [n, d] views (t optional); w: optional [n]; outputs float32 (accumulated):
+// sse/st/stt/sx as [d] views sharing one stride, sw scalar.
+void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
+                    const optional<Tensor>& w, const optional<Tensor>& sse,
+                    const optional<Tensor>& st, const optional<Tensor>& stt,
+                    const optional<Tensor>& sx, const optional<Tensor>& sw) {
+  const Tensor& ref = x.has_value() ? *x : *t;
+  check_gpu(ref, "x/t");
+  TORCH_CHECK(ref.dim() == 2, "column_moments: inputs must be [n, d] views");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ref.device());
+  tea::MomentsArgs a;
+  a.n = ref.size(0);
+  a.d = ref.size(1);
+  if (x.has_value()) {
+    TORCH_CHECK(x->sizes() == ref.sizes(), "column_moments: x shape");
+    a.x = x->data_ptr();
+    a.x_dt = dt_of(*x);
+    a.x_row_stride = x->stride(0);
+    a.x_col_stride = x->stride(1);
+  }
+  if (t.has_value()) {
+    TORCH_CHECK(t->sizes() == ref.sizes(), "column_moments: t shape must match x");
+    a.t = t->data_ptr();
+    a.t_dt = dt_of(*t);
+    a.t_row_stride = t->stride(0);
+    a.t_col_stride = t->stride(1);
+  }
+  if (w.has_value()) {
+    TORCH_CHECK(w->dim() == 1 && w->size(0) == a.n, "column_moments: w must be [n]");
+    a.w = w->data_ptr();
+    a.w_dt = dt_of(*w);
+    a.w_stride = w->stride(0);
+  }
+  int64_t os = -1;
+  auto out = [&](const optional<Tensor>& o, const char* name) -> float* {
+    if (!o.has_value()) return nullptr;
+    TORCH_CHECK(o->scalar_type() == at::kFloat && o->numel() == a.d && o->device() == ref.device(),
+                "column_moments: ", name, " must be float32 with d elements");
+    const int64_t s = o->dim() == 0 ? 1 : o->stride(-1);
+    TORCH_CHECK(os < 0 || os == s, "column_moments: outputs must share a stride");
+    os = s;
+    return o->data_ptr<float>();
+  };
+  a.sse = out(sse, "sse");
+  a.st = out(st, "st");
+  a.stt = out(stt, "stt");
+  a.sx = out(sx, "sx");
+  a.out_stride = os < 0 ? 1 : os;
+  if (sw.has_value()) {
+    TORCH_CHECK(sw->scalar_type() == at::kFloat && sw->numel() == 1, "column_moments: sw scalar f32");
+    a.sw = sw->data_ptr<float>();
+  }
+  check_launch(tea::launch_column_moments(a, stream_for(ref)), "column_moments");
+}
+
+// x, t: [rows, n] (rows contiguous); w optional [rows, n]; out float64 [rows, 3] accumulated.
+void ne_sums(const Tensor& x, const Tensor& t, const optional<Tensor>& w, bool from_logits,
+             const Tensor& out, const optional<Tensor>& err) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && t.sizes() == x.sizes(), "ne_sums: x/t must be [rows, n]");
+  TORCH_CHECK(x.stride(1) == 1 && t.stride(1) == 1, "ne_sums: rows must be contiguous");
+  TORCH_CHECK(out.scalar_type() == at::kDouble && out.is_contiguous() && out.numel() == x.size(0) * 3,
+              "ne_sums: out must be float64 [rows, 3]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  tea::NeArgs a;
+  a.x = x.data_ptr();
+  a.x_dt = dt_of(x);
+  a.x_row_stride = x.stride(0);
+  a.t = t.data_ptr();
+  a.t_dt = dt_of(t);
+  a.t_row_stride = t.stride(0);
+  if (w.has_value()) {
+    TORCH_CHECK(w->sizes() == x.sizes() && w->stride(1) == 1, "ne_sums: weight must match x");
+    a.w = w->data_ptr();
+    a.w_dt = dt_of(*w);
+    a.w_row_stride = w->stride(0);
+  }
+  a.rows = x.size(0);
+  a.n = x.size(1);
+  a.from_logits = from_logits ? 1 : 0;
+  a.out = out.data_ptr<double>();
+  if (err.has_value()) {
+    TORCH_CHECK(err->scalar_type() == at::kInt, "ne_sums: err must be int32");
+    a.err = err->data_ptr<int>();
+  }
+  check_launch(tea::launch_ne_sums(a, stream_for(x)), "ne_sums");
 }
 
 }  // namespace
@@ -179,10 +396,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cls_counts", &cls_counts, "K1 fused classification counts", py::arg("input"),
         py::arg("target"), py::arg("k"), py::arg("num_classes"), py::arg("micro_correct"),
         py::arg("micro_total"), py::arg("cls_correct"), py::arg("cls_label"),
-        py::arg("cls_pred"), py::arg("confusion"), py::arg("err"), py::arg("max_blocks") = 0);
+        py::arg("cls_pred"), py::arg("confusion"), py::arg("err"), py::arg("max_blocks") = 0,
+        py::arg("micro_incorrect") = py::none(), py::arg("micro_total2") = py::none(),
+        py::arg("cls_fp") = py::none());
   m.def("binary_counts", &binary_counts, "K1b thresholded binary counts", py::arg("input"),
         py::arg("target"), py::arg("weight"), py::arg("threshold"), py::arg("tp"),
         py::arg("fp"), py::arg("tn"), py::arg("fn"), py::arg("total"), py::arg("strict") = 0,
-        py::arg("max_blocks") = 0);
+        py::arg("max_blocks") = 0, py::arg("tp2") = py::none(), py::arg("fp2") = py::none(),
+        py::arg("tn2") = py::none(), py::arg("fn2") = py::none());
+  m.def("auc_scan", &auc_scan, "K3 tie-aware scan -> AUROC / AUPRC per row", py::arg("sorted"),
+        py::arg("order"), py::arg("target"), py::arg("weight"), py::arg("class_mode"),
+        py::arg("out_auroc"), py::arg("out_auprc"));
+  m.def("binned_counts", &binned_counts, "K4 binned TP/FP/FN per (threshold, class)",
+        py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("mode"), py::arg("tp"),
+        py::arg("fp"), py::arg("fn"));
+  m.def("column_moments", &column_moments, "K5 weighted column moments", py::arg("x"),
+        py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),
+        py::arg("sw"));
+  m.def("ne_sums", &ne_sums, "K6 normalized-entropy row sums", py::arg("x"), py::arg("t"),
+        py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"));
   tea_register_runtime(m);
 }

@@ -22,10 +22,13 @@ struct ClsCountsArgs {
   int k = 1;                     // top-k (k > 1: rank-of-target)
   int64_t num_classes = 0;       // histogram width
   float* micro_correct = nullptr;
-  float* micro_total = nullptr;
+  float* micro_incorrect = nullptr;
+  float* micro_total = nullptr;   // += n
+  float* micro_total2 = nullptr;  // += n (second destination)
   float* cls_correct = nullptr;  // [num_classes] correct at target class
   float* cls_label = nullptr;    // [num_classes] samples per target class
   float* cls_pred = nullptr;     // [num_classes] samples per predicted class
+  float* cls_fp = nullptr;       // [num_classes] wrong predictions per predicted class
   float* confusion = nullptr;    // [num_classes, num_classes] (target, pred)
   int* err = nullptr;            // error bits (1: bad target, 2: bad prediction)
   int check_target = 0;          // flag bad targets even without histograms
@@ -44,10 +47,114 @@ struct BinaryCountsArgs {
   int64_t n = 0;
   float threshold = 0.5f;
   int strict_binary = 0;  // non-{0,1} targets count nowhere (1) or as the "other" class (0)
-  float* out[4] = {nullptr, nullptr, nullptr, nullptr};  // tp, fp, tn, fn
+  float* out[4] = {nullptr, nullptr, nullptr, nullptr};   // tp, fp, tn, fn
+  float* out2[4] = {nullptr, nullptr, nullptr, nullptr};  // optional second destinations
   float* total = nullptr;  // += n (sample count)
   int max_blocks = 0;
 };
 int launch_binary_counts(const BinaryCountsArgs& a, hipStream_t stream);
+
+}  // namespace tea
+
+namespace tea {
+
+// ------------------------------------------------------------------ K3 sort-scan (AUROC/AUPRC)
+struct AucScanArgs {
+  const void* sorted = nullptr;  // [rows, n] scores sorted descending (f32 or f64)
+  DType key_dt = DType::f32;
+  int64_t key_stride = 0;
+  const int64_t* order = nullptr;  // [rows, n] sort permutation
+  int64_t order_stride = 0;
+  const void* target = nullptr;  // binary: [rows, n] (row stride) / class mode: [n] labels
+  DType tg_dt = DType::f32;
+  int64_t target_stride = 0;
+  const void* weight = nullptr;  // optional [rows, n]
+  DType w_dt = DType::f32;
+  int64_t weight_stride = 0;
+  int class_mode = 0;  // positives are samples whose label == row index
+  int64_t rows = 0;
+  int64_t n = 0;
+  double* out_auroc = nullptr;  // [rows]
+  double* out_auprc = nullptr;  // [rows]
+  // workspace carve-up (set by the launcher)
+  void* ab = nullptr;
+  void* tsum = nullptr;
+  void* tstart = nullptr;
+  void* tarea = nullptr;
+  void* totals = nullptr;
+};
+int64_t auc_scan_workspace_bytes(int64_t rows, int64_t n);
+int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream);
+
+}  // namespace tea
+
+namespace tea {
+
+// ------------------------------------------------------------------ K4 binned histograms
+struct BinnedArgs {
+  const void* input = nullptr;  // element (i, j) at i * in_row_stride + j * in_col_stride
+  DType in_dt = DType::f32;
+  int64_t n = 0;  // samples
+  int64_t c = 0;  // classes / labels / tasks
+  int64_t in_row_stride = 0;
+  int64_t in_col_stride = 0;
+  const void* target = nullptr;
+  DType tg_dt = DType::i64;
+  int mode = 0;  // 0: target(i, j) == 1 is positive; 1: labels, target(i) == j
+  int64_t tg_row_stride = 0;
+  int64_t tg_col_stride = 0;
+  const float* thr = nullptr;  // [T] sorted ascending
+  int T = 0;
+  float* hist = nullptr;       // scratch [(T + 1), c, 2], zeroed by the caller
+  float* tp = nullptr;         // outputs (accumulated): index k * out_k_stride + j * out_c_stride
+  float* fp = nullptr;
+  float* fn = nullptr;
+  int64_t out_k_stride = 0;
+  int64_t out_c_stride = 0;
+};
+int launch_binned(const BinnedArgs& a, hipStream_t stream);
+
+}  // namespace tea
+
+namespace tea {
+
+// ------------------------------------------------------------------ K5 column moments
+struct MomentsArgs {
+  const void* x = nullptr;  // element (i, j) at i * x_row_stride + j * x_col_stride
+  DType x_dt = DType::f32;
+  int64_t x_row_stride = 0, x_col_stride = 0;
+  const void* t = nullptr;
+  DType t_dt = DType::f32;
+  int64_t t_row_stride = 0, t_col_stride = 0;
+  const void* w = nullptr;  // optional per-row weight
+  DType w_dt = DType::f32;
+  int64_t w_stride = 0;
+  int64_t n = 0, d = 0;
+  float* sse = nullptr;  // [d] outputs (accumulated), element j at j * out_stride
+  float* st = nullptr;
+  float* stt = nullptr;
+  float* sx = nullptr;
+  float* sw = nullptr;   // scalar
+  int64_t out_stride = 1;
+};
+int launch_column_moments(const MomentsArgs& a, hipStream_t stream);
+
+// ------------------------------------------------------------------ K6 normalized entropy
+struct NeArgs {
+  const void* x = nullptr;
+  DType x_dt = DType::f32;
+  int64_t x_row_stride = 0;
+  const void* t = nullptr;
+  DType t_dt = DType::f32;
+  int64_t t_row_stride = 0;
+  const void* w = nullptr;
+  DType w_dt = DType::f32;
+  int64_t w_row_stride = 0;
+  int64_t rows = 0, n = 0;
+  int from_logits = 0;
+  double* out = nullptr;  // [rows, 3]: sum w*bce, sum w*t, sum w (accumulated)
+  int* err = nullptr;
+};
+int launch_ne_sums(const NeArgs& a, hipStream_t stream);
 
 }  // namespace tea

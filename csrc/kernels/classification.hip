@@ -85,6 +85,7 @@ struct Hist {
   float* cls_correct;
   float* cls_label;
   float* cls_pred;
+  float* cls_fp;
   float* confusion;
 };
 
@@ -94,34 +95,51 @@ __device__ __forceinline__ void row_hist(const Hist& h, int64_t C, int64_t t, in
   const bool p_ok = pred >= 0 && pred < C;
   if (err) {
     if (!t_ok && (h.cls_label || h.cls_correct || h.confusion || check_target)) atomicOr(err, 1);
-    if (!p_ok && (h.cls_pred || h.confusion)) atomicOr(err, 2);
+    if (!p_ok && (h.cls_pred || h.confusion || (h.cls_fp && !correct))) atomicOr(err, 2);
   }
   if (t_ok) {
     if (h.cls_correct && correct) atomicAdd(h.cls_correct + t, 1.f);
     if (h.cls_label) atomicAdd(h.cls_label + t, 1.f);
   }
   if (p_ok && h.cls_pred) atomicAdd(h.cls_pred + pred, 1.f);
+  if (p_ok && h.cls_fp && !correct) atomicAdd(h.cls_fp + pred, 1.f);
   if (t_ok && p_ok && h.confusion) atomicAdd(h.confusion + t * C + pred, 1.f);
 }
 
 // Block epilogue for the micro counters: LDS reduce, then the sharded fold.
-__device__ __forceinline__ void block_micro(const ClsCountsArgs& a, uint32_t my_correct) {
-  __shared__ uint32_t lds[kWavesPerBlock];
+__device__ __forceinline__ void fold_or_add(unsigned long long* ws, uint32_t v, float* dst) {
+  if (ws) {
+    fold_count(ws, v, dst);
+  } else if (v) {
+    atomicAdd(dst, static_cast<float>(v));
+  }
+}
+
+// ``my_rows`` = rows this thread/lane accounted for; incorrect = rows - correct.
+__device__ __forceinline__ void block_micro(const ClsCountsArgs& a, uint32_t my_correct,
+                                            uint32_t my_rows) {
+  __shared__ uint32_t lds[2][kWavesPerBlock];
   const uint32_t w = static_cast<uint32_t>(wave_sum(static_cast<int>(my_correct)));
-  if (lane_id() == 0) lds[threadIdx.x >> 6] = w;
+  const uint32_t r = static_cast<uint32_t>(wave_sum(static_cast<int>(my_rows)));
+  if (lane_id() == 0) {
+    lds[0][threadIdx.x >> 6] = w;
+    lds[1][threadIdx.x >> 6] = r;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t s = 0;
+    uint32_t s = 0, rows = 0;
 #pragma unroll
-    for (int k = 0; k < kWavesPerBlock; ++k) s += lds[k];
-    if (a.micro_correct) {
-      if (a.fold_ws) {
-        fold_count(a.fold_ws, s, a.micro_correct);
-      } else if (s) {
-        atomicAdd(a.micro_correct, static_cast<float>(s));
-      }
+    for (int k = 0; k < kWavesPerBlock; ++k) {
+      s += lds[0][k];
+      rows += lds[1][k];
     }
-    if (a.micro_total && blockIdx.x == 0) atomicAdd(a.micro_total, static_cast<float>(a.n));
+    if (a.micro_correct) fold_or_add(a.fold_ws, s, a.micro_correct);
+    if (a.micro_incorrect)
+      fold_or_add(a.fold_ws ? a.fold_ws + kFoldCells : nullptr, rows - s, a.micro_incorrect);
+    if (blockIdx.x == 0) {
+      if (a.micro_total) atomicAdd(a.micro_total, static_cast<float>(a.n));
+      if (a.micro_total2) atomicAdd(a.micro_total2, static_cast<float>(a.n));
+    }
   }
 }
 
@@ -149,8 +167,8 @@ __global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
   constexpr int STEP = kWave * VEC;             // columns per wave-load
   constexpr int CHUNK = STEP * kChunkLoads;     // columns per chunk
   const int C = static_cast<int>(a.c);
-  const Hist h{a.cls_correct, a.cls_label, a.cls_pred, a.confusion};
-  uint32_t correct_acc = 0;
+  const Hist h{a.cls_correct, a.cls_label, a.cls_pred, a.cls_fp, a.confusion};
+  uint32_t correct_acc = 0, rows_acc = 0;
 
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id(); row < a.n;
        row += nwaves) {
@@ -229,10 +247,11 @@ __global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
     }
     if (lane == 0) {
       correct_acc += correct;
+      rows_acc += 1;
       row_hist(h, a.num_classes, t, pred, correct, a.err, a.check_target);
     }
   }
-  block_micro(a, correct_acc);
+  block_micro(a, correct_acc, rows_acc);
 }
 
 // Narrow rows (C <= 32): one thread per row, class histograms privatised in LDS.
@@ -240,6 +259,7 @@ template <int KIND, bool TOPK>
 __global__ __launch_bounds__(kBlock) void cls_narrow_kernel(ClsCountsArgs a) {
   constexpr int ELSIZE = KIND == 0 ? 4 : 2;
   __shared__ float s_correct[kNarrowMaxC], s_label[kNarrowMaxC], s_pred[kNarrowMaxC];
+  __shared__ float s_fp[kNarrowMaxC];
   __shared__ float s_conf[kNarrowMaxC * kNarrowMaxC];
   const int C = static_cast<int>(a.c);
   for (int i = threadIdx.x; i < C * C; i += kBlock) s_conf[i] = 0.f;
@@ -247,11 +267,13 @@ __global__ __launch_bounds__(kBlock) void cls_narrow_kernel(ClsCountsArgs a) {
     s_correct[threadIdx.x] = 0.f;
     s_label[threadIdx.x] = 0.f;
     s_pred[threadIdx.x] = 0.f;
+    s_fp[threadIdx.x] = 0.f;
   }
   __syncthreads();
   const Hist lh{a.cls_correct ? s_correct : nullptr, a.cls_label ? s_label : nullptr,
-                a.cls_pred ? s_pred : nullptr, a.confusion ? s_conf : nullptr};
-  uint32_t correct_acc = 0;
+                a.cls_pred ? s_pred : nullptr, a.cls_fp ? s_fp : nullptr,
+                a.confusion ? s_conf : nullptr};
+  uint32_t correct_acc = 0, rows_acc = 0;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; row < a.n;
        row += stride) {
@@ -279,6 +301,7 @@ __global__ __launch_bounds__(kBlock) void cls_narrow_kernel(ClsCountsArgs a) {
       correct = t_ok && cnt < a.k;
     }
     correct_acc += correct;
+    rows_acc += 1;
     row_hist(lh, C, t, pred, correct, a.err, a.check_target);
   }
   __syncthreads();
@@ -286,26 +309,28 @@ __global__ __launch_bounds__(kBlock) void cls_narrow_kernel(ClsCountsArgs a) {
     if (a.cls_correct && s_correct[i] != 0.f) atomicAdd(a.cls_correct + i, s_correct[i]);
     if (a.cls_label && s_label[i] != 0.f) atomicAdd(a.cls_label + i, s_label[i]);
     if (a.cls_pred && s_pred[i] != 0.f) atomicAdd(a.cls_pred + i, s_pred[i]);
+    if (a.cls_fp && s_fp[i] != 0.f) atomicAdd(a.cls_fp + i, s_fp[i]);
   }
   if (a.confusion)
     for (int i = threadIdx.x; i < C * C; i += kBlock)
       if (s_conf[i] != 0.f) atomicAdd(a.confusion + i, s_conf[i]);
-  block_micro(a, correct_acc);
+  block_micro(a, correct_acc, rows_acc);
 }
 
 // 1-D integer label predictions: elementwise compare + histograms.
 __global__ __launch_bounds__(kBlock) void cls_labels_kernel(ClsCountsArgs a) {
-  const Hist h{a.cls_correct, a.cls_label, a.cls_pred, a.confusion};
-  uint32_t correct_acc = 0;
+  const Hist h{a.cls_correct, a.cls_label, a.cls_pred, a.cls_fp, a.confusion};
+  uint32_t correct_acc = 0, rows_acc = 0;
   const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < a.n; i += stride) {
     const int64_t p = load_as_i64(a.input, a.in_dt, i);
     const int64_t t = load_target(a.target, a.tg_dt, i);
     const bool correct = p == t;
     correct_acc += correct;
+    rows_acc += 1;
     row_hist(h, a.num_classes, t, p, correct, a.err, a.check_target);
   }
-  block_micro(a, correct_acc);
+  block_micro(a, correct_acc, rows_acc);
 }
 
 // Binary: thresholded scores vs targets -> [tp, fp, tn, fn] (+ optional weights).
@@ -340,6 +365,8 @@ __global__ __launch_bounds__(kBlock) void binary_counts_kernel(BinaryCountsArgs 
     for (int w = 0; w < kWavesPerBlock; ++w) s += lds[threadIdx.x][w];
     float* dst = a.out[threadIdx.x];
     if (dst && s != 0.f) atomicAdd(dst, s);
+    float* dst2 = a.out2[threadIdx.x];
+    if (dst2 && s != 0.f) atomicAdd(dst2, s);
   }
   if (threadIdx.x == 0 && blockIdx.x == 0 && a.total) atomicAdd(a.total, static_cast<float>(a.n));
 }

@@ -1,0 +1,395 @@
+// K3: tie-aware scan + integrals over score-sorted samples (AUROC / AUPRC).
+//
+// Replaces the reference's post-sort op chains
+//   auroc.py:115-152, 206-235   diff != 0 -> pad -> gather x2 -> cumsum x2 -> masked_scatter x2
+//                               (host-synchronising) -> trapz -> where
+//   auprc.py / precision_recall_curve.py:156-231   same prefix + per-class Python loops
+// with four small launches that never leave the device:
+//   1 tile_sums : per 4096-sample tile, gather (target, weight) through the sort permutation,
+//                 write a = w*t, b = w*(1-t) (float2) and the tile totals (double).
+//   2 tile_scan : one block per row: exclusive scan of tile totals (TP / FP before each tile).
+//   3 tile_area : per tile, LDS block scans give TP/FP at every element; prefix-max / suffix-min
+//                 scans locate each sample's tie group (head / tail) inside the tile; groups that
+//                 straddle a tile edge are resolved once per block by a binary search on the
+//                 sorted scores plus a partial-tile reduction.  Per sample:
+//                   roc += b_i * (TP(head-) + TP(tail)) / 2      (Mann-Whitney with ties)
+//                   pr  += a_i * TP(tail) / (TP(tail) + FP(tail)) (average precision)
+//   4 finalize  : per row: AUROC = roc / (P * N) (0.5 if degenerate), AUPRC = pr / P (0 if P = 0).
+// Accumulation is in FP64 (the reference accumulates in FP32), so results are at least as
+// accurate as the reference's.
+#include "tea_common.h"
+#include "tea_kernels.h"
+
+namespace tea {
+
+namespace {
+
+constexpr int kT = 256;              // threads per block
+constexpr int kPer = 16;             // samples per thread
+constexpr int kTile = kT * kPer;     // samples per tile
+
+struct alignas(16) D2 {
+  double x, y;
+};
+
+__device__ __forceinline__ D2 d2add(D2 a, D2 b) { return {a.x + b.x, a.y + b.y}; }
+
+__device__ __forceinline__ D2 wave_incl_scan(D2 v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double x = __shfl_up(v.x, o, 64);
+    const double y = __shfl_up(v.y, o, 64);
+    if (lane >= o) {
+      v.x += x;
+      v.y += y;
+    }
+  }
+  return v;
+}
+
+// exclusive block scan of one D2 per thread (blockDim = kT)
+__device__ __forceinline__ D2 block_excl_scan(D2 v, D2* lds /* >= 4 */, D2& total) {
+  const D2 inc = wave_incl_scan(v);
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 63) lds[w] = inc;
+  __syncthreads();
+  D2 off{0.0, 0.0};
+  total = {0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < kT / 64; ++k) {
+    if (k < w) off = d2add(off, lds[k]);
+    total = d2add(total, lds[k]);
+  }
+  __syncthreads();
+  return {off.x + inc.x - v.x, off.y + inc.y - v.y};
+}
+
+__device__ __forceinline__ int wave_incl_max(int v) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_up(v, o, 64);
+    if (lane >= o) v = max(v, u);
+  }
+  return v;
+}
+__device__ __forceinline__ int wave_incl_min_rev(int v) {  // suffix min across lanes
+  const int lane = lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int u = __shfl_down(v, o, 64);
+    if (lane + o < 64) v = min(v, u);
+  }
+  return v;
+}
+
+template <typename K>
+__device__ __forceinline__ K key_at(const AucScanArgs& a, int r, int64_t i) {
+  return static_cast<const K*>(a.sorted)[r * a.key_stride + i];
+}
+
+__device__ __forceinline__ float2 sample_ab(const AucScanArgs& a, int r, int64_t i) {
+  const int64_t src = a.order[r * a.order_stride + i];
+  float t;
+  if (a.class_mode) {
+    t = load_as_i64(a.target, a.tg_dt, src) == r ? 1.f : 0.f;
+  } else {
+    t = load_as_f32(a.target, a.tg_dt, r * a.target_stride + src);
+  }
+  const float w = a.weight ? load_as_f32(a.weight, a.w_dt, r * a.weight_stride + src) : 1.f;
+  return make_float2(w * t, w * (1.f - t));
+}
+
+__global__ __launch_bounds__(kT) void tile_sums_kernel(AucScanArgs a) {
+  const int r = blockIdx.y;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile;
+  double sa = 0.0, sb = 0.0;
+  float2* ab = reinterpret_cast<float2*>(a.ab) + static_cast<int64_t>(r) * a.n;
+#pragma unroll 4
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t i = base + k * kT + threadIdx.x;  // coalesced gather order
+    if (i < a.n) {
+      const float2 v = sample_ab(a, r, i);
+      ab[i] = v;
+      sa += v.x;
+      sb += v.y;
+    }
+  }
+  __shared__ double lds[2][kT / 64];
+  sa = wave_sum(sa);
+  sb = wave_sum(sb);
+  if (lane_id() == 0) {
+    lds[0][threadIdx.x >> 6] = sa;
+    lds[1][threadIdx.x >> 6] = sb;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    D2 s{0.0, 0.0};
+    for (int w = 0; w < kT / 64; ++w) s = {s.x + lds[0][w], s.y + lds[1][w]};
+    reinterpret_cast<D2*>(a.tsum)[static_cast<int64_t>(r) * gridDim.x + blockIdx.x] = s;
+  }
+}
+
+// one block per row: exclusive scan of the tile totals, row totals
+__global__ __launch_bounds__(kT) void tile_scan_kernel(AucScanArgs a, int ntiles) {
+  const int r = blockIdx.x;
+  D2* ts = reinterpret_cast<D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
+  D2* st = reinterpret_cast<D2*>(a.tstart) + static_cast<int64_t>(r) * ntiles;
+  __shared__ D2 lds[kT / 64];
+  D2 carry{0.0, 0.0};
+  for (int b = 0; b < ntiles; b += kT) {
+    const int t = b + threadIdx.x;
+    const D2 v = t < ntiles ? ts[t] : D2{0.0, 0.0};
+    D2 tot;
+    const D2 ex = block_excl_scan(v, lds, tot);
+    if (t < ntiles) st[t] = d2add(carry, ex);
+    carry = d2add(carry, tot);
+  }
+  if (threadIdx.x == 0) reinterpret_cast<D2*>(a.totals)[r] = carry;
+}
+
+// sum of a/b over [lo, hi] (inclusive, hi may be < lo -> empty) of row r, block-cooperative
+__device__ D2 block_range_sum(const float2* ab, int64_t lo, int64_t hi, D2* lds) {
+  double sa = 0.0, sb = 0.0;
+  for (int64_t i = lo + threadIdx.x; i <= hi; i += kT) {
+    const float2 v = ab[i];
+    sa += v.x;
+    sb += v.y;
+  }
+  D2 tot;
+  block_excl_scan(D2{sa, sb}, lds, tot);
+  return tot;
+}
+
+template <typename K>
+__device__ int64_t first_equal(const AucScanArgs& a, int r, int64_t lo, int64_t hi, K v) {
+  // descending keys; first index in [lo, hi) with key == v, given key[hi] == v
+  while (lo < hi) {
+    const int64_t mid = lo + (hi - lo) / 2;
+    if (key_at<K>(a, r, mid) > v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+template <typename K>
+__device__ int64_t last_equal(const AucScanArgs& a, int r, int64_t lo, int64_t hi, K v) {
+  // descending keys; last index in [lo, hi) with key == v, given key[lo] == v
+  int64_t l = lo, h = hi;  // find first index with key < v in [lo, hi)
+  while (l < h) {
+    const int64_t mid = l + (h - l) / 2;
+    if (key_at<K>(a, r, mid) < v) h = mid;
+    else l = mid + 1;
+  }
+  return l - 1;
+}
+
+template <typename K>
+__global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
+  const int r = blockIdx.y;
+  const int ntiles = gridDim.x;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile;
+  const int tile_n = static_cast<int>(min(static_cast<int64_t>(kTile), a.n - base));
+  const float2* ab = reinterpret_cast<const float2*>(a.ab) + static_cast<int64_t>(r) * a.n;
+  const D2* st = reinterpret_cast<const D2*>(a.tstart) + static_cast<int64_t>(r) * ntiles;
+
+  __shared__ double s_tpx[kTile];  // TP before each element (exclusive)
+  __shared__ double s_fpi[kTile];  // FP up to each element (inclusive)
+  __shared__ D2 lds[kT / 64];
+  __shared__ double s_bound[3];    // TP before the entering group; TP, FP at the leaving group's tail
+  __shared__ int s_flags[2];
+  __shared__ int s_hmax[kT / 64], s_tmin[kT / 64];
+  __shared__ int64_t s_pos;
+
+  const int j0 = threadIdx.x * kPer;
+  K key[kPer];
+  float2 v[kPer];
+  double la = 0.0, lb = 0.0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t i = base + j0 + k;
+    if (j0 + k < tile_n) {
+      key[k] = key_at<K>(a, r, i);
+      v[k] = ab[i];
+    } else {
+      key[k] = K(0);
+      v[k] = make_float2(0.f, 0.f);
+    }
+    la += v[k].x;
+    lb += v[k].y;
+  }
+  D2 tot;
+  const D2 ex = block_excl_scan(D2{la, lb}, lds, tot);
+  const D2 t0 = st[blockIdx.x];
+  const K prev_key = (base > 0) ? key_at<K>(a, r, base - 1) : K(0);
+  const K next_key = (base + tile_n < a.n) ? key_at<K>(a, r, base + tile_n) : K(0);
+
+  bool headf[kPer], tailf[kPer];
+  int my_head = -1, my_tail = kTile;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int j = j0 + k;
+    const int64_t i = base + j;
+    bool h = false, tl = false;
+    if (j < tile_n) {
+      const K pk = (k > 0) ? key[k - 1] : ((j == 0) ? prev_key : key_at<K>(a, r, i - 1));
+      const K nk = (k + 1 < kPer && j + 1 < tile_n)
+                       ? key[k + 1]
+                       : ((j + 1 == tile_n) ? next_key : key_at<K>(a, r, i + 1));
+      h = (i == 0) || !(pk == key[k]);
+      tl = (i == a.n - 1) || !(nk == key[k]);
+    }
+    headf[k] = h;
+    tailf[k] = tl;
+    if (h) my_head = j;
+  }
+#pragma unroll
+  for (int k = kPer - 1; k >= 0; --k)
+    if (tailf[k]) my_tail = j0 + k;
+  {
+    double ca = t0.x + ex.x, cb = t0.y + ex.y;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int j = j0 + k;
+      s_tpx[j] = ca;
+      ca += v[k].x;
+      cb += v[k].y;
+      s_fpi[j] = cb;
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  const int hin = wave_incl_max(my_head);
+  const int tin = wave_incl_min_rev(my_tail);
+  if (lane_id() == 63) s_hmax[w] = hin;
+  if (lane_id() == 0) s_tmin[w] = tin;
+  if (threadIdx.x == 0) {
+    s_flags[0] = (base > 0 && key_at<K>(a, r, base) == prev_key) ? 1 : 0;
+    s_flags[1] = (base + tile_n < a.n && key_at<K>(a, r, base + tile_n - 1) == next_key) ? 1 : 0;
+    s_bound[0] = s_bound[1] = s_bound[2] = 0.0;
+  }
+  __syncthreads();
+  int hmax_before = -1, tmin_after = kTile;
+  for (int k = 0; k < w; ++k) hmax_before = max(hmax_before, s_hmax[k]);
+  for (int k = w + 1; k < kT / 64; ++k) tmin_after = min(tmin_after, s_tmin[k]);
+  int h_excl = __shfl_up(hin, 1, 64);
+  if (lane_id() == 0) h_excl = -1;
+  h_excl = max(h_excl, hmax_before);
+  int t_excl = __shfl_down(tin, 1, 64);
+  if (lane_id() == 63) t_excl = kTile;
+  t_excl = min(t_excl, tmin_after);
+
+  // tie groups straddling the tile edges (block-uniform branches, rare)
+  if (s_flags[0]) {
+    if (threadIdx.x == 0) s_pos = first_equal<K>(a, r, 0, base, key_at<K>(a, r, base));
+    __syncthreads();
+    const int64_t hpos = s_pos;
+    const int64_t ht = hpos / kTile;
+    const D2 part = block_range_sum(ab, ht * kTile, hpos - 1, lds);
+    if (threadIdx.x == 0) s_bound[0] = st[ht].x + part.x;
+    __syncthreads();
+  }
+  if (s_flags[1]) {
+    if (threadIdx.x == 0)
+      s_pos = last_equal<K>(a, r, base + tile_n, a.n, key_at<K>(a, r, base + tile_n - 1));
+    __syncthreads();
+    const int64_t epos = s_pos;
+    const int64_t et = epos / kTile;
+    const D2 part = block_range_sum(ab, et * kTile, epos, lds);
+    if (threadIdx.x == 0) {
+      s_bound[1] = st[et].x + part.x;
+      s_bound[2] = st[et].y + part.y;
+    }
+    __syncthreads();
+  }
+
+  // per-sample credit (group head: last head <= j; group tail: first tail >= j)
+  int ntail[kPer];
+  {
+    int nt = t_excl;
+#pragma unroll
+    for (int k = kPer - 1; k >= 0; --k) {
+      if (tailf[k]) nt = j0 + k;
+      ntail[k] = nt;
+    }
+  }
+  const double tile_tp_end = t0.x + tot.x;
+  double roc = 0.0, pr = 0.0;
+  int cur_head = h_excl;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int j = j0 + k;
+    if (headf[k]) cur_head = j;
+    if (j < tile_n) {
+      const int tail = ntail[k];
+      const double tps = (cur_head >= 0) ? s_tpx[cur_head] : s_bound[0];
+      double tpe, fpe;
+      if (tail < tile_n) {
+        tpe = (tail + 1 < tile_n) ? s_tpx[tail + 1] : tile_tp_end;
+        fpe = s_fpi[tail];
+      } else {
+        tpe = s_bound[1];
+        fpe = s_bound[2];
+      }
+      roc += static_cast<double>(v[k].y) * 0.5 * (tps + tpe);
+      const double den = tpe + fpe;
+      if (v[k].x != 0.f && den != 0.0) pr += static_cast<double>(v[k].x) * (tpe / den);
+    }
+  }
+  D2 area;
+  block_excl_scan(D2{roc, pr}, lds, area);
+  if (threadIdx.x == 0)
+    reinterpret_cast<D2*>(a.tarea)[static_cast<int64_t>(r) * ntiles + blockIdx.x] = area;
+}
+
+__global__ __launch_bounds__(kT) void finalize_kernel(AucScanArgs a, int ntiles) {
+  const int r = blockIdx.x;
+  const D2* ta = reinterpret_cast<const D2*>(a.tarea) + static_cast<int64_t>(r) * ntiles;
+  double roc = 0.0, pr = 0.0;
+  for (int t = threadIdx.x; t < ntiles; t += kT) {
+    roc += ta[t].x;
+    pr += ta[t].y;
+  }
+  __shared__ D2 lds[kT / 64];
+  D2 tot;
+  block_excl_scan(D2{roc, pr}, lds, tot);
+  if (threadIdx.x == 0) {
+    const D2 pn = reinterpret_cast<const D2*>(a.totals)[r];
+    const double factor = pn.x * pn.y;
+    if (a.out_auroc) a.out_auroc[r] = factor == 0.0 ? 0.5 : tot.x / factor;
+    if (a.out_auprc) a.out_auprc[r] = pn.x == 0.0 ? 0.0 : tot.y / pn.x;
+  }
+}
+
+}  // namespace
+
+int64_t auc_scan_workspace_bytes(int64_t rows, int64_t n) {
+  const int64_t ntiles = (n + kTile - 1) / kTile;
+  return rows * n * 8 + rows * ntiles * 16 * 3 + rows * 16 + 256;
+}
+
+int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream) {
+  if (a.n <= 0 || a.rows <= 0) return 0;
+  const int ntiles = static_cast<int>((a.n + kTile - 1) / kTile);
+  char* ws = static_cast<char*>(workspace);
+  a.ab = ws;
+  ws += a.rows * a.n * 8;
+  ws = reinterpret_cast<char*>((reinterpret_cast<uintptr_t>(ws) + 15) & ~uintptr_t(15));
+  a.tsum = ws;
+  ws += a.rows * ntiles * 16;
+  a.tstart = ws;
+  ws += a.rows * ntiles * 16;
+  a.tarea = ws;
+  ws += a.rows * ntiles * 16;
+  a.totals = ws;
+  const dim3 grid(ntiles, static_cast<unsigned>(a.rows));
+  hipLaunchKernelGGL(tile_sums_kernel, grid, dim3(kT), 0, stream, a);
+  hipLaunchKernelGGL(tile_scan_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles);
+  if (a.key_dt == DType::f64)
+    hipLaunchKernelGGL(tile_area_kernel<double>, grid, dim3(kT), 0, stream, a);
+  else
+    hipLaunchKernelGGL(tile_area_kernel<float>, grid, dim3(kT), 0, stream, a);
+  hipLaunchKernelGGL(finalize_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles);
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace tea

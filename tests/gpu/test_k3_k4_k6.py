@@ -1,0 +1,147 @@
+"""K3 (sort-scan AUROC/AUPRC), K4 (binned counts), K6 (NE sums) vs CPU fp64 references."""
+
+import pytest
+import torch
+
+from torcheval_amd.metrics.functional import (
+    binary_auprc,
+    binary_auroc,
+    binary_binned_auprc,
+    binary_binned_auroc,
+    binary_binned_precision_recall_curve,
+    binary_normalized_entropy,
+    multiclass_auprc,
+    multiclass_auroc,
+    multiclass_binned_auprc,
+    multiclass_binned_auroc,
+    multilabel_auprc,
+    multilabel_binned_auprc,
+)
+from torcheval_amd.metrics.functional.classification._curve import binary_areas
+from torcheval_amd.ops.binned import _binned_counts_aten, binned_counts
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _quantized(n, levels, g):
+    # many ties, including groups that straddle the 4096-sample tiles of K3
+    return (torch.randint(0, levels, (n,), generator=g).float() / levels)
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096, 4097, 50000, 1_000_003])
+@pytest.mark.parametrize("levels", [0, 3, 1000])
+def test_k3_binary_matches_cpu(n, levels):
+    g = torch.Generator().manual_seed(n + levels)
+    x = torch.rand(n, generator=g) if levels == 0 else _quantized(n, levels, g)
+    t = torch.randint(0, 2, (n,), generator=g)
+    roc_c, pr_c = binary_areas(x, t, None, roc=True, pr=True)
+    roc_g, pr_g = binary_areas(x.to(DEV), t.to(DEV), None, roc=True, pr=True)
+    torch.testing.assert_close(roc_g.cpu(), roc_c, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(pr_g.cpu(), pr_c, rtol=1e-9, atol=1e-12)
+
+
+def test_k3_all_equal_scores_and_degenerate():
+    for x, t in [
+        (torch.full((20000,), 0.5), torch.randint(0, 2, (20000,))),
+        (torch.rand(9000), torch.zeros(9000, dtype=torch.long)),
+        (torch.rand(9000), torch.ones(9000, dtype=torch.long)),
+    ]:
+        roc_c, pr_c = binary_areas(x, t, None, roc=True, pr=True)
+        roc_g, pr_g = binary_areas(x.to(DEV), t.to(DEV), None, roc=True, pr=True)
+        torch.testing.assert_close(roc_g.cpu(), roc_c)
+        torch.testing.assert_close(pr_g.cpu(), pr_c)
+
+
+def test_k3_weighted_multitask_and_dtypes():
+    g = torch.Generator().manual_seed(3)
+    x = _quantized(3 * 30000, 50, g).view(3, 30000)
+    t = torch.randint(0, 2, (3, 30000), generator=g).float()
+    w = torch.rand(3, 30000, generator=g)
+    exp = binary_auroc(x, t, num_tasks=3, weight=w)
+    got = binary_auroc(x.to(DEV), t.to(DEV), num_tasks=3, weight=w.to(DEV))
+    torch.testing.assert_close(got.cpu(), exp, rtol=1e-9, atol=1e-12)
+    assert got.dtype == torch.float64
+    xd = x.double()
+    torch.testing.assert_close(binary_auroc(xd[0].to(DEV), t[0].to(DEV)).cpu(), binary_auroc(xd[0], t[0]))
+    xb = x.bfloat16()
+    torch.testing.assert_close(binary_auprc(xb[1].to(DEV), t[1].to(DEV)).cpu(), binary_auprc(xb[1], t[1]))
+
+
+@pytest.mark.parametrize("C", [2, 10, 130])
+def test_k3_multiclass_multilabel(C):
+    g = torch.Generator().manual_seed(C)
+    X = _quantized(20000 * C, 97, g).view(20000, C)
+    y = torch.randint(0, C, (20000,), generator=g)
+    torch.testing.assert_close(
+        multiclass_auroc(X.to(DEV), y.to(DEV), num_classes=C, average=None).cpu(),
+        multiclass_auroc(X, y, num_classes=C, average=None),
+    )
+    torch.testing.assert_close(
+        multiclass_auprc(X.to(DEV), y.to(DEV), average=None).cpu(), multiclass_auprc(X, y, average=None)
+    )
+    if C >= 2:
+        Y = torch.randint(0, 2, (20000, C), generator=g)
+        torch.testing.assert_close(
+            multilabel_auprc(X.to(DEV), Y.to(DEV), average=None).cpu(), multilabel_auprc(X, Y, average=None)
+        )
+
+
+@pytest.mark.parametrize("T", [1, 5, 100, 200, 1000])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_k4_binned_counts(T, mode):
+    g = torch.Generator().manual_seed(T * 7 + mode)
+    C = 37
+    x = torch.rand(5003, C, generator=g)
+    x[:50] = 0.0
+    x[50:100] = 1.0
+    thr = torch.cat([torch.tensor([0.0, 1.0]), torch.rand(max(T - 2, 0), generator=g)]).sort().values[:T]
+    t = torch.randint(0, C, (5003,), generator=g) if mode == 1 else torch.randint(0, 2, (5003, C), generator=g)
+    exp = _binned_counts_aten(x, t, thr, mode)
+    got = binned_counts(x.to(DEV), t.to(DEV), thr.to(DEV), mode)
+    for a, b in zip(got, exp):
+        torch.testing.assert_close(a.cpu(), b)
+    # strided (task-major) view, as used by multi-task binned metrics
+    xt = x.t().contiguous()
+    got2 = binned_counts(xt.to(DEV).t(), t.to(DEV), thr.to(DEV), mode)
+    for a, b in zip(got2, exp):
+        torch.testing.assert_close(a.cpu(), b)
+
+
+def test_binned_metrics_gpu_vs_cpu():
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(4, 3000, generator=g)
+    t = torch.randint(0, 2, (4, 3000), generator=g)
+    for fn, kw in [(binary_binned_auroc, dict(num_tasks=4, threshold=50)),
+                   (binary_binned_auprc, dict(num_tasks=4, threshold=50))]:
+        a, _ = fn(x.to(DEV), t.to(DEV), **kw)
+        b, _ = fn(x, t, **kw)
+        torch.testing.assert_close(a.cpu(), b)
+    p1 = binary_binned_precision_recall_curve(x[0].to(DEV), t[0].to(DEV), threshold=10)
+    p2 = binary_binned_precision_recall_curve(x[0], t[0], threshold=10)
+    for a, b in zip(p1, p2):
+        torch.testing.assert_close(a.cpu(), b)
+    X = torch.rand(3000, 6, generator=g)
+    y = torch.randint(0, 6, (3000,), generator=g)
+    torch.testing.assert_close(multiclass_binned_auroc(X.to(DEV), y.to(DEV), num_classes=6)[0].cpu(),
+                               multiclass_binned_auroc(X, y, num_classes=6)[0])
+    torch.testing.assert_close(multiclass_binned_auprc(X.to(DEV), y.to(DEV))[0].cpu(), multiclass_binned_auprc(X, y)[0])
+    Y = torch.randint(0, 2, (3000, 6), generator=g)
+    torch.testing.assert_close(multilabel_binned_auprc(X.to(DEV), Y.to(DEV))[0].cpu(), multilabel_binned_auprc(X, Y)[0])
+
+
+@pytest.mark.parametrize("from_logits", [False, True])
+def test_k6_normalized_entropy(from_logits):
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(3, 20000, generator=g) if from_logits else torch.rand(3, 20000, generator=g)
+    x[0, :10] = 0.0 if not from_logits else -50.0
+    t = torch.randint(0, 2, (3, 20000), generator=g).float()
+    w = torch.rand(3, 20000, generator=g)
+    exp = binary_normalized_entropy(x, t, weight=w, num_tasks=3, from_logits=from_logits)
+    got = binary_normalized_entropy(x.to(DEV), t.to(DEV), weight=w.to(DEV), num_tasks=3, from_logits=from_logits)
+    torch.testing.assert_close(got.cpu(), exp, rtol=1e-6, atol=1e-9)
+
+
+def test_k6_range_error():
+    with pytest.raises(ValueError, match="should be probability in range"):
+        binary_normalized_entropy(torch.tensor([0.2, 1.5]).to(DEV), torch.tensor([0.0, 1.0]).to(DEV))

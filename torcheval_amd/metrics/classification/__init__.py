@@ -4,10 +4,66 @@ from torcheval_amd.metrics.classification.accuracy import (
     MultilabelAccuracy,
     TopKMultilabelAccuracy,
 )
+from torcheval_amd.metrics.classification.auprc import BinaryAUPRC, MulticlassAUPRC, MultilabelAUPRC
+from torcheval_amd.metrics.classification.auroc import BinaryAUROC, MulticlassAUROC
+from torcheval_amd.metrics.classification.binary_normalized_entropy import BinaryNormalizedEntropy
+from torcheval_amd.metrics.classification.binned import (
+    BinaryBinnedAUPRC,
+    BinaryBinnedAUROC,
+    BinaryBinnedPrecisionRecallCurve,
+    MulticlassBinnedAUPRC,
+    MulticlassBinnedAUROC,
+    MulticlassBinnedPrecisionRecallCurve,
+    MultilabelBinnedAUPRC,
+    MultilabelBinnedPrecisionRecallCurve,
+)
+from torcheval_amd.metrics.classification.confusion_matrix import (
+    BinaryConfusionMatrix,
+    MulticlassConfusionMatrix,
+)
+from torcheval_amd.metrics.classification.f1_score import BinaryF1Score, MulticlassF1Score
+from torcheval_amd.metrics.classification.precision import BinaryPrecision, MulticlassPrecision
+from torcheval_amd.metrics.classification.precision_recall_curve import (
+    BinaryPrecisionRecallCurve,
+    MulticlassPrecisionRecallCurve,
+    MultilabelPrecisionRecallCurve,
+)
+from torcheval_amd.metrics.classification.recall import BinaryRecall, MulticlassRecall
+from torcheval_amd.metrics.classification.recall_at_fixed_precision import (
+    BinaryRecallAtFixedPrecision,
+    MultilabelRecallAtFixedPrecision,
+)
 
 __all__ = [
     "BinaryAccuracy",
+    "BinaryAUPRC",
+    "BinaryAUROC",
+    "BinaryBinnedAUPRC",
+    "BinaryBinnedAUROC",
+    "BinaryBinnedPrecisionRecallCurve",
+    "BinaryConfusionMatrix",
+    "BinaryF1Score",
+    "BinaryNormalizedEntropy",
+    "BinaryPrecision",
+    "BinaryPrecisionRecallCurve",
+    "BinaryRecall",
+    "BinaryRecallAtFixedPrecision",
     "MulticlassAccuracy",
+    "MulticlassAUPRC",
+    "MulticlassAUROC",
+    "MulticlassBinnedAUPRC",
+    "MulticlassBinnedAUROC",
+    "MulticlassBinnedPrecisionRecallCurve",
+    "MulticlassConfusionMatrix",
+    "MulticlassF1Score",
+    "MulticlassPrecision",
+    "MulticlassPrecisionRecallCurve",
+    "MulticlassRecall",
     "MultilabelAccuracy",
+    "MultilabelAUPRC",
+    "MultilabelBinnedAUPRC",
+    "MultilabelBinnedPrecisionRecallCurve",
+    "MultilabelPrecisionRecallCurve",
+    "MultilabelRecallAtFixedPrecision",
     "TopKMultilabelAccuracy",
 ]

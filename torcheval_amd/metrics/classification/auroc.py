@@ -1,0 +1,148 @@
+"""AUROC, class API (parity: classification/auroc.py:34-235).
+
+Samples are kept on device as list states (``merge="cat"``: the distributed toolkit
+all-gathers them over RCCL without pickling).  Unweighted updates store an empty placeholder
+instead of the reference's float64 ones per sample (auroc.py:112-113), saving 8 B/sample of
+HBM and sync traffic; placeholders are expanded only if some update was weighted.
+"""
+
+from typing import Iterable, List, Optional, TypeVar
+
+import torch
+
+from torcheval_amd.metrics.functional.classification.auroc import (
+    _binary_auroc_compute,
+    _binary_auroc_update_input_check,
+    _multiclass_auroc_compute,
+    _multiclass_auroc_param_check,
+    _multiclass_auroc_update_input_check,
+)
+from torcheval_amd.metrics.metric import Metric
+
+TAUROC = TypeVar("TAUROC")
+TMulticlassAUROC = TypeVar("TMulticlassAUROC")
+
+
+def _cat_weights(inputs: List[torch.Tensor], weights: List[torch.Tensor]) -> Optional[torch.Tensor]:
+    if all(w.numel() == 0 for w in weights):
+        return None
+    full = [w if w.numel() else torch.ones_like(x, dtype=torch.float64) for x, w in zip(inputs, weights)]
+    return torch.cat(full, -1)
+
+
+class BinaryAUROC(Metric[torch.Tensor]):
+    """
+    Area under the ROC curve for ``[n]`` or ``[num_tasks, n]`` scores with optional
+    per-sample weights.  Functional version: ``binary_auroc``.
+    """
+
+    def __init__(
+        self: TAUROC,
+        *,
+        num_tasks: int = 1,
+        device: Optional[torch.device] = None,
+        use_fbgemm: Optional[bool] = False,
+    ) -> None:
+        super().__init__(device=device)
+        if num_tasks < 1:
+            raise ValueError(
+                "`num_tasks` value should be greater than or equal to 1, but received {num_tasks}. "
+            )
+        self.num_tasks = num_tasks
+        self.use_fbgemm = use_fbgemm
+        self._add_state("inputs", [], merge="cat")
+        self._add_state("targets", [], merge="cat")
+        self._add_state("weights", [], merge="cat")
+
+    @torch.inference_mode()
+    def update(
+        self: TAUROC,
+        input: torch.Tensor,
+        target: torch.Tensor,
+        weight: Optional[torch.Tensor] = None,
+    ) -> TAUROC:
+        """Append a batch of scores, {0,1} targets and optional weights."""
+        input = input.to(self.device)
+        target = target.to(self.device)
+        if weight is not None:
+            weight = weight.to(self.device)
+        _binary_auroc_update_input_check(input, target, self.num_tasks, weight)
+        self.inputs.append(input)
+        self.targets.append(target)
+        self.weights.append(weight if weight is not None else input.new_empty(0, dtype=torch.float64))
+        return self
+
+    @torch.inference_mode()
+    def compute(self: TAUROC) -> torch.Tensor:
+        """Return the AUROC (float64; per task when ``num_tasks > 1``)."""
+        inputs = torch.cat(self.inputs, -1)
+        targets = torch.cat(self.targets, -1)
+        return _binary_auroc_compute(inputs, targets, _cat_weights(self.inputs, self.weights), self.use_fbgemm)
+
+    @torch.inference_mode()
+    def merge_state(self: TAUROC, metrics: Iterable[TAUROC]) -> TAUROC:
+        for metric in metrics:
+            if metric.inputs:
+                self.inputs.append(torch.cat(metric.inputs, -1).to(self.device))
+                self.targets.append(torch.cat(metric.targets, -1).to(self.device))
+                w = _cat_weights(metric.inputs, metric.weights)
+                self.weights.append(
+                    w.to(self.device) if w is not None else self.inputs[-1].new_empty(0, dtype=torch.float64)
+                )
+        return self
+
+    @torch.inference_mode()
+    def _prepare_for_merge_state(self: TAUROC) -> None:
+        if self.inputs and self.targets:
+            w = _cat_weights(self.inputs, self.weights)
+            self.inputs = [torch.cat(self.inputs, -1)]
+            self.targets = [torch.cat(self.targets, -1)]
+            self.weights = [w if w is not None else self.inputs[0].new_empty(0, dtype=torch.float64)]
+
+
+class MulticlassAUROC(Metric[torch.Tensor]):
+    """One-vs-rest AUROC of ``[n, C]`` scores; ``average`` in macro | None.
+    Functional version: ``multiclass_auroc``."""
+
+    def __init__(
+        self: TMulticlassAUROC,
+        *,
+        num_classes: int,
+        average: Optional[str] = "macro",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        _multiclass_auroc_param_check(num_classes, average)
+        self.num_classes = num_classes
+        self.average = average
+        self._add_state("inputs", [], merge="cat")
+        self._add_state("targets", [], merge="cat")
+
+    @torch.inference_mode()
+    def update(self: TMulticlassAUROC, input: torch.Tensor, target: torch.Tensor) -> TMulticlassAUROC:
+        input = input.to(self.device)
+        target = target.to(self.device)
+        _multiclass_auroc_update_input_check(input, target, self.num_classes)
+        self.inputs.append(input)
+        self.targets.append(target)
+        return self
+
+    @torch.inference_mode()
+    def compute(self: TMulticlassAUROC) -> torch.Tensor:
+        return _multiclass_auroc_compute(
+            torch.cat(self.inputs), torch.cat(self.targets), self.num_classes, self.average
+        )
+
+    @torch.inference_mode()
+    def merge_state(self: TMulticlassAUROC, metrics: Iterable[TMulticlassAUROC]) -> TMulticlassAUROC:
+        for metric in metrics:
+            if metric.inputs:
+                self.inputs.append(torch.cat(metric.inputs).to(self.device))
+                self.targets.append(torch.cat(metric.targets).to(self.device))
+        return self
+
+    @torch.inference_mode()
+    def _prepare_for_merge_state(self: TMulticlassAUROC) -> None:
+        if self.inputs and self.targets:
+            self.inputs = [torch.cat(self.inputs)]
+            self.targets = [torch.cat(self.targets)]

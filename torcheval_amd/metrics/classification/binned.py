@@ -1,0 +1,335 @@
+"""Binned curve metrics, class API.
+
+Parity: classification/binned_precision_recall_curve.py (:31, :140, :278),
+binned_auroc.py (:31, :153), binned_auprc.py (:40, :180, :328).
+
+Count-state metrics accumulate the K4 histogram output directly into their float32 states
+(one histogram + one suffix launch per update, no [T, N, C] temporaries); states are
+``merge="sum"`` (one RCCL all-reduce per sync).  The binned-AUROC classes keep raw samples
+like the reference (list states, ``merge="cat"``) and bin at ``compute()``.
+"""
+
+from typing import Iterable, List, Optional, Tuple, Union
+
+import torch
+
+from torcheval_amd.metrics.classification._sample_store import SampleStoreMetric
+from torcheval_amd.metrics.functional.classification.binned_auprc import (
+    _binary_binned_auprc_param_check,
+    _binary_binned_auprc_update_input_check,
+    _binned_riemann,
+    _multiclass_binned_auprc_param_check,
+    _multiclass_binned_auprc_update_input_check,
+    _multilabel_binned_auprc_param_check,
+    _multilabel_binned_auprc_update_input_check,
+)
+from torcheval_amd.metrics.functional.classification.binned_auroc import (
+    _binary_binned_auroc_compute,
+    _binary_binned_auroc_param_check,
+    _binary_binned_auroc_update_input_check,
+    _multiclass_binned_auroc_compute,
+    _multiclass_binned_auroc_param_check,
+    _multiclass_binned_auroc_update_input_check,
+)
+from torcheval_amd.metrics.functional.classification.binned_precision_recall_curve import (
+    _binary_binned_precision_recall_curve_compute,
+    _binned_precision_recall_curve_param_check,
+    _multiclass_binned_precision_recall_curve_compute,
+    _optimization_param_check,
+)
+from torcheval_amd.metrics.functional.classification.precision_recall_curve import (
+    _binary_precision_recall_curve_update_input_check,
+    _multiclass_precision_recall_curve_update_input_check,
+    _multilabel_precision_recall_curve_update_input_check,
+)
+from torcheval_amd.metrics.functional.tensor_utils import _create_threshold_tensor
+from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.ops.binned import binned_counts
+
+
+def _as_threshold(threshold, device) -> torch.Tensor:
+    if isinstance(threshold, int):
+        return torch.linspace(0, 1.0, threshold, device=device)
+    return torch.as_tensor(threshold, device=device)
+
+
+class _BinnedCountsMetric(Metric):
+    """States num_tp / num_fp / num_fn of shape ``shape``; ``_views`` maps them to [T, C]."""
+
+    def _init_counts(self, shape) -> None:
+        for name in ("num_tp", "num_fp", "num_fn"):
+            self._add_state(name, torch.zeros(shape, device=self.device), merge="sum")
+
+    def _views(self):
+        return self.num_tp, self.num_fp, self.num_fn
+
+    def _accumulate(self, scores: torch.Tensor, target: torch.Tensor, mode: int) -> None:
+        binned_counts(scores, target, self.threshold, mode, out=self._views())
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["_BinnedCountsMetric"]):
+        for metric in metrics:
+            self.num_tp += metric.num_tp.to(self.device)
+            self.num_fp += metric.num_fp.to(self.device)
+            self.num_fn += metric.num_fn.to(self.device)
+        return self
+
+
+class BinaryBinnedPrecisionRecallCurve(_BinnedCountsMetric):
+    """Binned PR curve of ``[n]`` scores.  Functional: ``binary_binned_precision_recall_curve``."""
+
+    def __init__(
+        self, *, threshold: Union[int, List[float], torch.Tensor] = 100, device: Optional[torch.device] = None
+    ) -> None:
+        super().__init__(device=device)
+        threshold = _as_threshold(threshold, self.device)
+        _binned_precision_recall_curve_param_check(threshold)
+        self.threshold = threshold
+        self._init_counts(len(threshold))
+
+    def _views(self):
+        return self.num_tp[:, None], self.num_fp[:, None], self.num_fn[:, None]
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "BinaryBinnedPrecisionRecallCurve":
+        input = input.to(self.device)
+        target = target.to(self.device)
+        _binary_precision_recall_curve_update_input_check(input, target)
+        self._accumulate(input[:, None], target[:, None], 0)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        return _binary_binned_precision_recall_curve_compute(self.num_tp, self.num_fp, self.num_fn, self.threshold)
+
+
+class MulticlassBinnedPrecisionRecallCurve(_BinnedCountsMetric):
+    """One-vs-rest binned PR curves.  Functional: ``multiclass_binned_precision_recall_curve``."""
+
+    def __init__(
+        self,
+        *,
+        num_classes: int,
+        threshold: Union[int, List[float], torch.Tensor] = 100,
+        optimization: str = "vectorized",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        _optimization_param_check(optimization)
+        threshold = _as_threshold(threshold, self.device)
+        _binned_precision_recall_curve_param_check(threshold)
+        self.num_classes = num_classes
+        self.threshold = threshold
+        self.optimization = optimization
+        self._init_counts((len(threshold), num_classes))
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "MulticlassBinnedPrecisionRecallCurve":
+        input = input.to(self.device)
+        target = target.to(self.device)
+        _multiclass_precision_recall_curve_update_input_check(input, target, self.num_classes)
+        self._accumulate(input, target, 1)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> Tuple[List[torch.Tensor], List[torch.Tensor], torch.Tensor]:
+        return _multiclass_binned_precision_recall_curve_compute(
+            self.num_tp, self.num_fp, self.num_fn, self.num_classes, self.threshold
+        )
+
+
+class MultilabelBinnedPrecisionRecallCurve(_BinnedCountsMetric):
+    """Per-label binned PR curves.  Functional: ``multilabel_binned_precision_recall_curve``."""
+
+    def __init__(
+        self,
+        *,
+        num_labels: int,
+        threshold: Union[int, List[float], torch.Tensor] = 100,
+        optimization: str = "vectorized",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        _optimization_param_check(optimization)
+        threshold = _as_threshold(threshold, self.device)
+        _binned_precision_recall_curve_param_check(threshold)
+        self.num_labels = num_labels
+        self.threshold = threshold
+        self.optimization = optimization
+        self._init_counts((len(threshold), num_labels))
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "MultilabelBinnedPrecisionRecallCurve":
+        input = input.to(self.device)
+        target = target.to(self.device)
+        _multilabel_precision_recall_curve_update_input_check(input, target, self.num_labels)
+        self._accumulate(input, target, 0)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> Tuple[List[torch.Tensor], List[torch.Tensor], torch.Tensor]:
+        return _multiclass_binned_precision_recall_curve_compute(
+            self.num_tp, self.num_fp, self.num_fn, self.num_labels, self.threshold
+        )
+
+
+class BinaryBinnedAUPRC(_BinnedCountsMetric):
+    """Binned AUPRC of ``[n]`` / ``[num_tasks, n]`` scores (states [num_tasks, T]).
+    Functional: ``binary_binned_auprc``."""
+
+    def __init__(
+        self,
+        *,
+        num_tasks: int = 1,
+        threshold: Union[int, List[float], torch.Tensor] = 100,
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        threshold = _create_threshold_tensor(threshold, self.device)
+        _binary_binned_auprc_param_check(num_tasks, threshold)
+        self.num_tasks = num_tasks
+        self.threshold = threshold
+        self._init_counts((num_tasks, len(threshold)))
+
+    def _views(self):
+        return self.num_tp.t(), self.num_fp.t(), self.num_fn.t()
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "BinaryBinnedAUPRC":
+        input = input.to(self.device)
+        target = target.to(self.device)
+        _binary_binned_auprc_update_input_check(input, target, self.num_tasks, self.threshold)
+        if input.ndim == 1:
+            input, target = input[None, :], target[None, :]
+        self._accumulate(input.t(), target.t(), 0)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        auprc = _binned_riemann(self.num_tp.t(), self.num_fp.t(), self.num_fn.t())
+        return auprc[0] if self.num_tasks == 1 else auprc
+
+
+class MulticlassBinnedAUPRC(_BinnedCountsMetric):
+    """One-vs-rest binned AUPRC.  Functional: ``multiclass_binned_auprc``."""
+
+    def __init__(
+        self,
+        *,
+        num_classes: int,
+        threshold: Union[int, List[float], torch.Tensor] = 100,
+        average: Optional[str] = "macro",
+        optimization: str = "vectorized",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        _optimization_param_check(optimization)
+        threshold = _create_threshold_tensor(threshold, self.device)
+        _multiclass_binned_auprc_param_check(num_classes, threshold, average)
+        self.num_classes = num_classes
+        self.threshold = threshold
+        self.average = average
+        self.optimization = optimization
+        self._init_counts((len(threshold), num_classes))
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "MulticlassBinnedAUPRC":
+        input = input.to(self.device)
+        target = target.to(self.device)
+        _multiclass_binned_auprc_update_input_check(input, target, self.num_classes)
+        self._accumulate(input, target, 1)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        auprc = _binned_riemann(self.num_tp, self.num_fp, self.num_fn)
+        return auprc.mean() if self.average == "macro" else auprc
+
+
+class MultilabelBinnedAUPRC(_BinnedCountsMetric):
+    """Per-label binned AUPRC.  Functional: ``multilabel_binned_auprc``."""
+
+    def __init__(
+        self,
+        *,
+        num_labels: int,
+        threshold: Union[int, List[float], torch.Tensor] = 100,
+        average: Optional[str] = "macro",
+        optimization: str = "vectorized",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        _optimization_param_check(optimization)
+        threshold = _create_threshold_tensor(threshold, self.device)
+        _multilabel_binned_auprc_param_check(num_labels, threshold, average)
+        self.num_labels = num_labels
+        self.threshold = threshold
+        self.average = average
+        self.optimization = optimization
+        self._init_counts((len(threshold), num_labels))
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "MultilabelBinnedAUPRC":
+        input = input.to(self.device)
+        target = target.to(self.device)
+        _multilabel_binned_auprc_update_input_check(input, target, self.num_labels)
+        self._accumulate(input, target, 0)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        auprc = _binned_riemann(self.num_tp, self.num_fp, self.num_fn)
+        return auprc.mean() if self.average == "macro" else auprc
+
+
+class BinaryBinnedAUROC(SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
+    """(binned AUROC, thresholds) of ``[n]`` / ``[num_tasks, n]`` scores.
+    Functional: ``binary_binned_auroc``."""
+
+    _cat_dim = -1
+
+    def __init__(
+        self,
+        *,
+        num_tasks: int = 1,
+        threshold: Union[int, List[float], torch.Tensor] = 200,
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        threshold = _create_threshold_tensor(threshold, self.device)
+        _binary_binned_auroc_param_check(num_tasks, threshold)
+        self.num_tasks = num_tasks
+        self.threshold = threshold
+
+    def _check(self, input, target) -> None:
+        _binary_binned_auroc_update_input_check(input, target, self.num_tasks, self.threshold)
+
+    @torch.inference_mode()
+    def compute(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        return _binary_binned_auroc_compute(*self._cat(), self.threshold)
+
+
+class MulticlassBinnedAUROC(SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
+    """(one-vs-rest binned AUROC, thresholds).  Functional: ``multiclass_binned_auroc``."""
+
+    def __init__(
+        self,
+        *,
+        num_classes: int,
+        threshold: Union[int, List[float], torch.Tensor] = 200,
+        average: Optional[str] = "macro",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        threshold = _create_threshold_tensor(threshold, self.device)
+        _multiclass_binned_auroc_param_check(num_classes, threshold, average)
+        self.num_classes = num_classes
+        self.threshold = threshold
+        self.average = average
+
+    def _check(self, input, target) -> None:
+        _multiclass_binned_auroc_update_input_check(input, target, self.num_classes)
+
+    @torch.inference_mode()
+    def compute(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        return _multiclass_binned_auroc_compute(*self._cat(), self.num_classes, self.threshold, self.average)

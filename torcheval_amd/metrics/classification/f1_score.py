@@ -1,0 +1,97 @@
+"""F1 score, class API (parity: classification/f1_score.py:26-273)."""
+
+from typing import Iterable, Optional, TypeVar
+
+import torch
+
+from torcheval_amd.metrics.functional.classification.f1_score import (
+    _binary_f1_score_update,
+    _f1_score_compute,
+    _f1_score_param_check,
+    _f1_score_update,
+    _f1_score_update_input_check,
+)
+from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.ops.classification import cls_counts, native_cls
+
+TF1Score = TypeVar("TF1Score")
+TBinaryF1Score = TypeVar("TBinaryF1Score")
+
+
+class MulticlassF1Score(Metric[torch.Tensor]):
+    """
+    F1 score for ``[N]`` labels or ``[N, C]`` scores; ``average`` in micro | macro |
+    weighted | None.  Functional version: ``multiclass_f1_score``.
+    """
+
+    def __init__(
+        self: TF1Score,
+        *,
+        num_classes: Optional[int] = None,
+        average: Optional[str] = "micro",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        _f1_score_param_check(num_classes, average)
+        self.num_classes = num_classes
+        self.average = average
+        self._err: Optional[torch.Tensor] = None
+        shape = () if average == "micro" else (num_classes,)
+        for name in ("num_tp", "num_label", "num_prediction"):
+            self._add_state(name, torch.zeros(shape, device=self.device), merge="sum")
+
+    def update(self: TF1Score, input: torch.Tensor, target: torch.Tensor) -> TF1Score:
+        input = input.to(self.device)
+        target = target.to(self.device)
+        if native_cls(input, target, self.num_tp, self.num_label, self.num_prediction):
+            _f1_score_update_input_check(input, target, self.num_classes)
+            if self.average == "micro":
+                cls_counts(input, target, micro_correct=self.num_tp, micro_total=self.num_label,
+                           micro_total2=self.num_prediction)
+            else:
+                if self._err is None:
+                    self._err = torch.zeros(1, dtype=torch.int32, device=input.device)
+                cls_counts(input, target, num_classes=self.num_classes, cls_correct=self.num_tp,
+                           cls_label=self.num_label, cls_pred=self.num_prediction, err=self._err)
+            return self
+        with torch.inference_mode():
+            num_tp, num_label, num_prediction = _f1_score_update(
+                input, target, self.num_classes, self.average
+            )
+            self.num_tp += num_tp
+            self.num_label += num_label
+            self.num_prediction += num_prediction
+        return self
+
+    @torch.inference_mode()
+    def compute(self: TF1Score) -> torch.Tensor:
+        from torcheval_amd.metrics.classification.accuracy import _raise_on_device_error
+
+        _raise_on_device_error(self._err)
+        return _f1_score_compute(self.num_tp, self.num_label, self.num_prediction, self.average)
+
+    @torch.inference_mode()
+    def merge_state(self: TF1Score, metrics: Iterable[TF1Score]) -> TF1Score:
+        for metric in metrics:
+            self.num_tp += metric.num_tp.to(self.device)
+            self.num_label += metric.num_label.to(self.device)
+            self.num_prediction += metric.num_prediction.to(self.device)
+        return self
+
+
+class BinaryF1Score(MulticlassF1Score):
+    """F1 of thresholded ``input``.  Functional version: ``binary_f1_score``."""
+
+    def __init__(self: TBinaryF1Score, *, threshold: float = 0.5, device: Optional[torch.device] = None) -> None:
+        super().__init__(average="micro", device=device)
+        self.threshold = threshold
+
+    @torch.inference_mode()
+    def update(self: TBinaryF1Score, input: torch.Tensor, target: torch.Tensor) -> TBinaryF1Score:
+        input = input.to(self.device)
+        target = target.to(self.device)
+        num_tp, num_label, num_prediction = _binary_f1_score_update(input, target, self.threshold)
+        self.num_tp += num_tp
+        self.num_label += num_label
+        self.num_prediction += num_prediction
+        return self

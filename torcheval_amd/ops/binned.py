@@ -1,0 +1,58 @@
+"""K4 binned-histogram wrapper (csrc/kernels/binned.hip) + the equivalent ATen path.
+
+``binned_counts(scores, target, thr, mode)`` returns float32 (tp, fp, fn) of shape [T, C] for
+a [n, C] score view: tp[k, j] = #positives of column j with score >= thr[k], fp likewise for
+negatives, fn = positives - tp.  ``mode`` 0: ``target`` is a [n, C] {0,1} view; mode 1:
+``target`` is [n] class labels (positive when label == j).
+"""
+
+from typing import Optional, Tuple
+
+import torch
+
+from torcheval_amd.ops import native, use_native
+
+
+def binned_counts(
+    scores: torch.Tensor,
+    target: torch.Tensor,
+    thr: torch.Tensor,
+    mode: int,
+    out: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
+) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Accumulate into ``out`` ([T, C] float32 views) or return fresh counts."""
+    T, C = thr.numel(), scores.shape[1]
+    thr = thr.to(device=scores.device)
+    if out is None:
+        buf = torch.zeros(3, T, C, dtype=torch.float32, device=scores.device)
+        out = (buf[0], buf[1], buf[2])
+    if use_native(scores) and target.is_cuda and T <= 2048:
+        t = target
+        if t.dtype == torch.bool:
+            t = t.to(torch.uint8)
+        native().binned_counts(scores, t, thr.to(torch.float32).contiguous(), int(mode), *out)
+        return out
+    tp, fp, fn = _binned_counts_aten(scores, target, thr, mode)
+    out[0].add_(tp)
+    out[1].add_(fp)
+    out[2].add_(fn)
+    return out
+
+
+def _binned_counts_aten(
+    scores: torch.Tensor, target: torch.Tensor, thr: torch.Tensor, mode: int
+) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    n, C = scores.shape
+    T = thr.numel()
+    bins = torch.searchsorted(thr.to(scores.dtype).contiguous(), scores.contiguous(), right=True)
+    if mode == 1:
+        pos = (target[:, None] == torch.arange(C, device=scores.device)[None, :]).long()
+    else:
+        pos = (target == 1).long()
+    flat = (bins * C + torch.arange(C, device=scores.device)[None, :]) * 2 + pos
+    hist = torch.bincount(flat.reshape(-1), minlength=(T + 1) * C * 2).view(T + 1, C, 2).to(torch.float64)
+    suffix = hist.flip(0).cumsum(0).flip(0)
+    tp = suffix[1:, :, 1]
+    fp = suffix[1:, :, 0]
+    fn = hist[:, :, 1].sum(0)[None, :] - tp
+    return tp.float(), fp.float(), fn.float()

@@ -8,10 +8,11 @@ from typing import Optional
 
 import torch
 
-from torcheval_amd.ops import MAX_BLOCKS, native
+from torcheval_amd.ops import MAX_BLOCKS, native, use_native
 
 _SCORE_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
 _LABEL_DTYPES = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
+_BINARY_DTYPES = _LABEL_DTYPES + (torch.float32, torch.float16, torch.bfloat16, torch.float64)
 
 
 def cls_counts_supported(input: torch.Tensor, target: torch.Tensor) -> bool:
@@ -25,6 +26,26 @@ def cls_counts_supported(input: torch.Tensor, target: torch.Tensor) -> bool:
     return False
 
 
+def native_cls(input: torch.Tensor, target: torch.Tensor, *states: torch.Tensor) -> bool:
+    """True when (input, target) go through K1 and every destination state is float32."""
+    return (
+        use_native(input)
+        and target.is_cuda
+        and cls_counts_supported(input, target)
+        and all(s.dtype == torch.float32 and s.is_contiguous() for s in states)
+    )
+
+
+def native_binary(input: torch.Tensor, target: torch.Tensor, *states: torch.Tensor) -> bool:
+    return (
+        use_native(input)
+        and target.is_cuda
+        and input.dtype in _BINARY_DTYPES
+        and target.dtype in _BINARY_DTYPES
+        and all(s.dtype == torch.float32 and s.is_contiguous() for s in states)
+    )
+
+
 def cls_counts(
     input: torch.Tensor,
     target: torch.Tensor,
@@ -32,16 +53,26 @@ def cls_counts(
     k: int = 1,
     num_classes: int = 0,
     micro_correct: Optional[torch.Tensor] = None,
+    micro_incorrect: Optional[torch.Tensor] = None,
     micro_total: Optional[torch.Tensor] = None,
+    micro_total2: Optional[torch.Tensor] = None,
     cls_correct: Optional[torch.Tensor] = None,
     cls_label: Optional[torch.Tensor] = None,
     cls_pred: Optional[torch.Tensor] = None,
+    cls_fp: Optional[torch.Tensor] = None,
     confusion: Optional[torch.Tensor] = None,
     err: Optional[torch.Tensor] = None,
 ) -> None:
-    """Accumulate argmax / top-k correctness counts and class histograms in one pass."""
+    """Accumulate argmax / top-k correctness counts and class histograms in one pass.
+
+    micro_*: scalars (correct rows, wrong rows, += N twice); cls_*: [num_classes]
+    (correct at target, rows per target, rows per prediction, wrong rows per prediction);
+    confusion: [num_classes, num_classes] indexed (target, prediction).
+    """
     if not target.is_contiguous():
         target = target.contiguous()
+    if input.dim() == 2 and num_classes <= 0:
+        num_classes = input.shape[1]
     native().cls_counts(
         input,
         target,
@@ -55,6 +86,9 @@ def cls_counts(
         confusion,
         err,
         MAX_BLOCKS,
+        micro_incorrect,
+        micro_total2,
+        cls_fp,
     )
 
 
@@ -69,9 +103,19 @@ def binary_counts(
     tn: Optional[torch.Tensor] = None,
     fn: Optional[torch.Tensor] = None,
     total: Optional[torch.Tensor] = None,
+    tp2: Optional[torch.Tensor] = None,
+    fp2: Optional[torch.Tensor] = None,
+    tn2: Optional[torch.Tensor] = None,
+    fn2: Optional[torch.Tensor] = None,
     strict: bool = False,
 ) -> None:
-    """Accumulate thresholded binary confusion counts (tp, fp, tn, fn) in one pass."""
+    """Accumulate thresholded binary confusion counts in one pass.
+
+    pred = ``input >= threshold``; tp/fp/tn/fn (optionally weighted) are added to each given
+    destination and to its optional second destination (``*2``); ``total`` += N.  With
+    ``strict`` a target outside {0, 1} counts nowhere; otherwise it is a wrong prediction.
+    """
     native().binary_counts(
-        input, target, weight, float(threshold), tp, fp, tn, fn, total, int(strict), MAX_BLOCKS
+        input, target, weight, float(threshold), tp, fp, tn, fn, total, int(strict), MAX_BLOCKS,
+        tp2, fp2, tn2, fn2,
     )

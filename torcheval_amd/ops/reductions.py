@@ -1,0 +1,57 @@
+"""Wrappers of the K5 / K6 fused reductions (csrc/kernels/reductions.hip)."""
+
+from typing import Optional, Tuple
+
+import torch
+
+from torcheval_amd.ops import native
+
+_FLOATISH = (torch.float32, torch.float64, torch.float16, torch.bfloat16)
+_ANY = _FLOATISH + (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
+
+
+def moments_supported(*ts: Optional[torch.Tensor]) -> bool:
+    return all(t is None or (t.is_cuda and t.dtype in _ANY) for t in ts)
+
+
+def column_moments(
+    x: Optional[torch.Tensor],
+    t: Optional[torch.Tensor],
+    w: Optional[torch.Tensor] = None,
+    *,
+    sse: Optional[torch.Tensor] = None,
+    st: Optional[torch.Tensor] = None,
+    stt: Optional[torch.Tensor] = None,
+    sx: Optional[torch.Tensor] = None,
+    sw: Optional[torch.Tensor] = None,
+) -> None:
+    """Accumulate weighted column moments of [n, d] (or [n]) x / t into float32 outputs."""
+    if x is not None and x.dim() == 1:
+        x = x[:, None]
+    if t is not None and t.dim() == 1:
+        t = t[:, None]
+    if t is not None and t.dtype == torch.bool:
+        t = t.to(torch.uint8)
+    native().column_moments(x, t, w, sse, st, stt, sx, sw)
+
+
+def ne_sums(
+    input: torch.Tensor,
+    target: torch.Tensor,
+    weight: Optional[torch.Tensor],
+    from_logits: bool,
+    err: Optional[torch.Tensor] = None,
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """float64 [rows, 3] = (sum w*BCE, sum w*t, sum w) per row, and the range flag."""
+    x = input if input.dim() == 2 else input[None, :]
+    t = target if target.dim() == 2 else target[None, :]
+    w = None if weight is None else (weight if weight.dim() == 2 else weight[None, :])
+    x, t = x.contiguous(), t.contiguous()
+    if t.dtype == torch.bool:
+        t = t.to(torch.uint8)
+    if w is not None:
+        w = w.contiguous()
+    out = torch.zeros(x.shape[0], 3, dtype=torch.float64, device=x.device)
+    flag = err if err is not None else torch.zeros(1, dtype=torch.int32, device=x.device)
+    native().ne_sums(x, t, w, bool(from_logits), out, flag)
+    return out, flag
