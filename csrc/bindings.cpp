@@ -388,6 +388,62 @@ void ne_sums(const Tensor& x, const Tensor& t, const optional<Tensor>& w, bool f
   check_launch(tea::launch_ne_sums(a, stream_for(x)), "ne_sums");
 }
 
+// ---------------------------------------------------------------- K7 perplexity
+// input: [rows, v] logits (unit column stride); target: [rows]; out float64 [2] accumulated.
+void perplexity_sums(const Tensor& input, const Tensor& target, optional<int64_t> ignore_index,
+                     const Tensor& out, const optional<Tensor>& err) {
+  check_gpu(input, "input");
+  TORCH_CHECK(input.dim() == 2 && input.stride(1) == 1, "perplexity: input must be [rows, v]");
+  TORCH_CHECK(target.dim() == 1 && target.size(0) == input.size(0), "perplexity: target must be [rows]");
+  TORCH_CHECK(out.scalar_type() == at::kDouble && out.numel() == 2 && out.is_contiguous(),
+              "perplexity: out must be float64 [2]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(input.device());
+  tea::PerplexityArgs a;
+  a.input = input.data_ptr();
+  a.in_dt = dt_of(input);
+  a.rows = input.size(0);
+  a.v = input.size(1);
+  a.row_stride = input.stride(0);
+  a.target = target.data_ptr();
+  a.tg_dt = dt_of(target);
+  a.tg_stride = target.stride(0);
+  if (ignore_index.has_value()) {
+    a.has_ignore = 1;
+    a.ignore_index = *ignore_index;
+  }
+  a.out = out.data_ptr<double>();
+  if (err.has_value()) a.err = err->data_ptr<int>();
+  const int rc = tea::launch_perplexity(a, stream_for(input));
+  TORCH_CHECK(rc != -1, "perplexity: unsupported logits dtype ", input.scalar_type());
+  check_launch(rc, "perplexity");
+}
+
+// ---------------------------------------------------------------- K8 FID covariance
+void fid_cov_update(const Tensor& act, const Tensor& cov, const optional<Tensor>& colsum) {
+  check_gpu(act, "activations");
+  TORCH_CHECK(act.dim() == 2 && act.scalar_type() == at::kFloat && act.stride(1) == 1,
+              "fid_cov_update: activations must be float32 [n, d] with unit column stride");
+  TORCH_CHECK(act.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(act.data_ptr()) % 16 == 0,
+              "fid_cov_update: activation rows must be 16-byte aligned");
+  const int64_t d = act.size(1);
+  TORCH_CHECK(cov.scalar_type() == at::kFloat && cov.is_contiguous() && cov.numel() == d * d &&
+                  cov.device() == act.device(),
+              "fid_cov_update: cov must be a contiguous float32 [d, d] on the same device");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(act.device());
+  tea::FidCovArgs a;
+  a.act = act.data_ptr<float>();
+  a.n = act.size(0);
+  a.d = d;
+  a.row_stride = act.stride(0);
+  a.cov = cov.data_ptr<float>();
+  if (colsum.has_value()) {
+    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->is_contiguous() && colsum->numel() == d,
+                "fid_cov_update: colsum must be float32 [d]");
+    a.colsum = colsum->data_ptr<float>();
+  }
+  check_launch(tea::launch_fid_cov(a, stream_for(act)), "fid_cov_update");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -415,5 +471,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("sw"));
   m.def("ne_sums", &ne_sums, "K6 normalized-entropy row sums", py::arg("x"), py::arg("t"),
         py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"));
+  m.def("perplexity_sums", &perplexity_sums, "K7 fused log-softmax gather", py::arg("input"),
+        py::arg("target"), py::arg("ignore_index"), py::arg("out"), py::arg("err"));
+  m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
+        py::arg("act"), py::arg("cov"), py::arg("colsum"));
   tea_register_runtime(m);
 }

@@ -158,3 +158,35 @@ struct NeArgs {
 int launch_ne_sums(const NeArgs& a, hipStream_t stream);
 
 }  // namespace tea
+
+namespace tea {
+
+// ------------------------------------------------------------------ K7 perplexity
+struct PerplexityArgs {
+  const void* input = nullptr;  // [rows, v] logits (row stride)
+  DType in_dt = DType::f32;
+  int64_t rows = 0, v = 0, row_stride = 0;
+  const void* target = nullptr;  // [rows] (stride)
+  DType tg_dt = DType::i64;
+  int64_t tg_stride = 1;
+  int has_ignore = 0;
+  int64_t ignore_index = 0;
+  double* out = nullptr;  // [2]: sum of -log p(target), token count (accumulated)
+  int* err = nullptr;
+};
+int launch_perplexity(const PerplexityArgs& a, hipStream_t stream);
+
+}  // namespace tea
+
+namespace tea {
+
+// ------------------------------------------------------------------ K8 FID covariance
+struct FidCovArgs {
+  const float* act = nullptr;  // [n, d] activations (row stride, unit column stride)
+  int64_t n = 0, d = 0, row_stride = 0;
+  float* cov = nullptr;     // [d, d] contiguous, += act^T act
+  float* colsum = nullptr;  // [d], += column sums (optional)
+};
+int launch_fid_cov(const FidCovArgs& a, hipStream_t stream);
+
+}  // namespace tea

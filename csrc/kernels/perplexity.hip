@@ -1,0 +1,160 @@
+// K7: fused log-softmax + target gather for perplexity.
+//
+// Replaces perplexity.py:92-107: softmax over the vocabulary, then ``probs[:, target]
+// .diagonal()`` which materialises an (N x N) matrix for N = batch * seq tokens (1.7e7
+// elements at N = 4096), then log + sum.  Here one wave64 streams each token's logit row
+// once with 16-B loads, keeping a per-lane online (max, sum-exp) pair that is rescaled once per
+// 16-value chunk; lanes combine their pairs with xor shuffles; lane 0 adds
+//   -log p(target) = logsumexp(row) - row[target]
+// in FP64.  ``ignore_index`` rows are skipped and counted out; targets outside [0, V) are
+// flagged on device (``err``) instead of the reference's host-synchronising max() check.
+#include "tea_common.h"
+#include "tea_kernels.h"
+
+namespace tea {
+
+namespace {
+
+constexpr int kB = 256;
+constexpr int kWpb = kB / kWave;
+
+template <int KIND>
+__device__ __forceinline__ void load8(const void* row, int64_t col, float (&v)[8]);
+
+template <>
+__device__ __forceinline__ void load8<0>(const void* row, int64_t col, float (&v)[8]) {
+  const float4* p = reinterpret_cast<const float4*>(static_cast<const float*>(row) + col);
+  const float4 a = p[0], b = p[1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <int KIND>
+__device__ __forceinline__ void load8_16(const void* row, int64_t col, float (&v)[8]) {
+  const uint4 x = *reinterpret_cast<const uint4*>(static_cast<const uint16_t*>(row) + col);
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const uint16_t lo = static_cast<uint16_t>(w[e] & 0xffffu), hi = static_cast<uint16_t>(w[e] >> 16);
+    v[2 * e] = KIND == 1 ? bf16_to_f32(lo) : f16_to_f32(lo);
+    v[2 * e + 1] = KIND == 1 ? bf16_to_f32(hi) : f16_to_f32(hi);
+  }
+}
+template <>
+__device__ __forceinline__ void load8<1>(const void* row, int64_t col, float (&v)[8]) {
+  load8_16<1>(row, col, v);
+}
+template <>
+__device__ __forceinline__ void load8<2>(const void* row, int64_t col, float (&v)[8]) {
+  load8_16<2>(row, col, v);
+}
+
+template <int KIND>
+__device__ __forceinline__ float load1(const void* row, int64_t col) {
+  if constexpr (KIND == 0) return static_cast<const float*>(row)[col];
+  const uint16_t b = static_cast<const uint16_t*>(row)[col];
+  return KIND == 1 ? bf16_to_f32(b) : f16_to_f32(b);
+}
+
+__device__ __forceinline__ void combine(float& m, float& s, float m2, float s2) {
+  const float mn = fmaxf(m, m2);
+  if (mn == -__builtin_huge_valf()) return;  // both empty
+  s = s * __expf(m - mn) + s2 * __expf(m2 - mn);
+  m = mn;
+}
+
+template <int KIND, bool VEC>
+__global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
+  const int lane = lane_id();
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * kWpb;
+  constexpr int ELS = KIND == 0 ? 4 : 2;
+  double acc = 0.0, cnt = 0.0;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWpb + wave_id(); row < a.rows; row += nw) {
+    const int64_t t = load_as_i64(a.target, a.tg_dt, row * a.tg_stride);
+    if (a.has_ignore && t == a.ignore_index) continue;
+    const void* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELS;
+    float m = -__builtin_huge_valf(), s = 0.f;
+    if constexpr (VEC) {
+      for (int64_t base = static_cast<int64_t>(lane) * 16; base < a.v; base += kWave * 16) {
+        float v[2][8];
+        load8<KIND>(rp, base, v[0]);
+        if (base + 8 < a.v) {
+          load8<KIND>(rp, base + 8, v[1]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[1][e] = -__builtin_huge_valf();
+        }
+        float cm = v[0][0];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cm = fmaxf(cm, v[h][e]);
+        float cs = 0.f;
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) cs += __expf(v[h][e] - cm);
+        combine(m, s, cm, cs);
+      }
+    } else {
+      for (int64_t c = lane; c < a.v; c += kWave) {
+        const float x = load1<KIND>(rp, c);
+        combine(m, s, x, 1.f);
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const float m2 = __shfl_xor(m, o, kWave);
+      const float s2 = __shfl_xor(s, o, kWave);
+      combine(m, s, m2, s2);
+    }
+    if (lane == 0) {
+      if (t < 0 || t >= a.v) {
+        if (a.err) atomicOr(a.err, 1);
+      } else {
+        const double lse = static_cast<double>(m) + log(static_cast<double>(s));
+        acc += lse - static_cast<double>(load1<KIND>(rp, t));
+        cnt += 1.0;
+      }
+    }
+  }
+  __shared__ double lds[2][kWpb];
+  if (lane == 0) {
+    lds[0][threadIdx.x >> 6] = acc;
+    lds[1][threadIdx.x >> 6] = cnt;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double tot = 0.0;
+#pragma unroll
+    for (int w = 0; w < kWpb; ++w) tot += lds[threadIdx.x][w];
+    if (tot != 0.0) atomicAdd(a.out + threadIdx.x, tot);
+  }
+}
+
+template <int KIND>
+void launch_kind(const PerplexityArgs& a, int grid, bool vec, hipStream_t s) {
+  if (vec)
+    hipLaunchKernelGGL((perplexity_kernel<KIND, true>), dim3(grid), dim3(kB), 0, s, a);
+  else
+    hipLaunchKernelGGL((perplexity_kernel<KIND, false>), dim3(grid), dim3(kB), 0, s, a);
+}
+
+}  // namespace
+
+int launch_perplexity(const PerplexityArgs& a, hipStream_t stream) {
+  if (a.rows <= 0) return 0;
+  int64_t grid = (a.rows + kWpb - 1) / kWpb;
+  if (grid > 512) grid = 512;
+  const uintptr_t base = reinterpret_cast<uintptr_t>(a.input);
+  const int vw = a.in_dt == DType::f32 ? 4 : 8;
+  const bool vec = a.v % 16 == 0 && a.row_stride % vw == 0 && base % 16 == 0;
+  switch (a.in_dt) {
+    case DType::f32: launch_kind<0>(a, static_cast<int>(grid), vec, stream); break;
+    case DType::bf16: launch_kind<1>(a, static_cast<int>(grid), vec, stream); break;
+    case DType::f16: launch_kind<2>(a, static_cast<int>(grid), vec, stream); break;
+    default: return -1;
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace tea

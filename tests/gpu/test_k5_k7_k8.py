@@ -1,0 +1,193 @@
+"""K5 (column moments: MSE / R2), K7 (fused log-softmax perplexity), K8 (FP32-MFMA FID
+covariance) and the families built on them, vs CPU fp64 references."""
+
+import math
+
+import pytest
+import torch
+
+from torcheval_amd.metrics import (
+    FrechetInceptionDistance,
+    MeanSquaredError,
+    Perplexity,
+    R2Score,
+    WindowedBinaryNormalizedEntropy,
+    WindowedMeanSquaredError,
+)
+from torcheval_amd.metrics.functional import (
+    binary_normalized_entropy,
+    mean_squared_error,
+    perplexity,
+    r2_score,
+)
+from torcheval_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+# ----------------------------------------------------------------------------- K5
+@pytest.mark.parametrize("shape", [(1,), (1000,), (4097, 3), (100_003, 16), (64, 257)])
+@pytest.mark.parametrize("weighted", [False, True])
+def test_k5_mse_matches_cpu(shape, weighted):
+    g = torch.Generator().manual_seed(sum(shape))
+    x, y = torch.randn(shape, generator=g), torch.randn(shape, generator=g)
+    w = torch.rand(shape[0], generator=g) if weighted else None
+    for mo in ("uniform_average", "raw_values"):
+        ref = mean_squared_error(x.double(), y.double(), sample_weight=None if w is None else w.double(), multioutput=mo)
+        got = mean_squared_error(x.to(DEV), y.to(DEV), sample_weight=None if w is None else w.to(DEV), multioutput=mo)
+        torch.testing.assert_close(got.cpu().double(), ref, rtol=2e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16, torch.int64])
+def test_k5_mixed_dtypes(dtype):
+    g = torch.Generator().manual_seed(7)
+    x = (torch.randn(5000, 4, generator=g) * 3).to(dtype)
+    y = torch.randn(5000, 4, generator=g)
+    ref = mean_squared_error(x.double(), y.double())
+    got = mean_squared_error(x.to(DEV), y.to(DEV))
+    torch.testing.assert_close(got.cpu().double(), ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("mo", ["uniform_average", "raw_values", "variance_weighted"])
+def test_k5_r2_matches_cpu(mo):
+    g = torch.Generator().manual_seed(11)
+    x, y = torch.randn(20000, 5, generator=g), torch.randn(20000, 5, generator=g) + 2
+    ref = r2_score(x.double(), y.double(), multioutput=mo)
+    got = r2_score(x.to(DEV), y.to(DEV), multioutput=mo)
+    torch.testing.assert_close(got.cpu().double(), ref, rtol=1e-4, atol=1e-5)
+    m = R2Score(multioutput=mo, device=DEV)
+    for i in range(4):
+        m.update(x[i::4].to(DEV), y[i::4].to(DEV))
+    torch.testing.assert_close(m.compute().cpu().double(), ref, rtol=1e-4, atol=1e-5)
+
+
+def test_k5_class_and_window():
+    g = torch.Generator().manual_seed(12)
+    xs = [torch.randn(3000, generator=g) for _ in range(6)]
+    ys = [torch.randn(3000, generator=g) for _ in range(6)]
+    m = MeanSquaredError(device=DEV)
+    wm = WindowedMeanSquaredError(max_num_updates=2, device=DEV)
+    for x, y in zip(xs, ys):
+        m.update(x.to(DEV), y.to(DEV))
+        wm.update(x.to(DEV), y.to(DEV))
+    ref = mean_squared_error(torch.cat(xs).double(), torch.cat(ys).double())
+    torch.testing.assert_close(m.compute().cpu().double(), ref, rtol=1e-5, atol=1e-6)
+    life, win = wm.compute()
+    torch.testing.assert_close(life.cpu().double(), ref, rtol=1e-5, atol=1e-6)
+    ref_w = mean_squared_error(torch.cat(xs[-2:]).double(), torch.cat(ys[-2:]).double())
+    torch.testing.assert_close(win.cpu().double(), ref_w, rtol=1e-5, atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- K7
+def _ppl_ref(x, t, ignore=None):
+    lp = torch.log_softmax(x.double().reshape(-1, x.shape[-1]), -1)
+    tt = t.reshape(-1)
+    keep = tt != ignore if ignore is not None else torch.ones_like(tt, dtype=torch.bool)
+    return math.exp(-float(lp[keep].gather(1, tt[keep, None]).sum()) / int(keep.sum()))
+
+
+@pytest.mark.parametrize("vocab", [3, 17, 1001, 32000, 50257])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_k7_perplexity_matches_fp64(vocab, dtype):
+    g = torch.Generator().manual_seed(vocab)
+    x = (torch.randn(4, 33, vocab, generator=g) * 4).to(dtype)
+    t = torch.randint(0, vocab, (4, 33), generator=g)
+    ref = _ppl_ref(x, t)
+    got = float(perplexity(x.to(DEV), t.to(DEV)))
+    assert got == pytest.approx(ref, rel=2e-5)
+    ign = int(t[0, 0])
+    assert float(perplexity(x.to(DEV), t.to(DEV), ignore_index=ign)) == pytest.approx(_ppl_ref(x, t, ign), rel=2e-5)
+
+
+def test_k7_strided_rows_and_class():
+    g = torch.Generator().manual_seed(5)
+    big = torch.randn(2, 16, 1024 + 64, generator=g)
+    x = big[..., :1024]  # row stride != vocab
+    t = torch.randint(0, 1024, (2, 16), generator=g)
+    assert float(perplexity(x.to(DEV), t.to(DEV))) == pytest.approx(_ppl_ref(x, t), rel=2e-5)
+    m = Perplexity(device=DEV)
+    m.update(x.to(DEV), t.to(DEV))
+    m.update(x.to(DEV) * 0.5, t.to(DEV))
+    ref = _ppl_ref(torch.cat([x, x * 0.5]), torch.cat([t, t]))
+    assert float(m.compute()) == pytest.approx(ref, rel=2e-5)
+
+
+def test_k7_invalid_target_raises():
+    with pytest.raises(ValueError, match="vocab_size minus one"):
+        perplexity(torch.rand(3, 2, 3, device=DEV), torch.tensor([[4, 2], [1, 0], [0, 0]], device=DEV))
+
+
+# ----------------------------------------------------------------------------- K8
+@pytest.mark.parametrize("n,d", [(1, 8), (37, 100), (64, 128), (200, 300), (256, 2048), (1000, 2048)])
+def test_k8_cov_matches_fp64(n, d):
+    g = torch.Generator().manual_seed(n * 7 + d)
+    act = torch.randn(n, d, generator=g)
+    cov0 = torch.randn(d, d, generator=g)
+    cov0 = cov0 + cov0.T
+    s0 = torch.randn(d, generator=g)
+    cov, s = cov0.to(DEV), s0.to(DEV)
+    native().fid_cov_update(act.to(DEV), cov, s)
+    torch.cuda.synchronize()
+    ref = cov0.double() + act.double().T @ act.double()
+    torch.testing.assert_close(cov.cpu().double(), ref, rtol=1e-4, atol=1e-3 * math.sqrt(n))
+    torch.testing.assert_close(s.cpu().double(), s0.double() + act.double().sum(0), rtol=1e-5, atol=1e-3)
+    # result must be exactly symmetric (mirrored tiles)
+    c = cov.cpu() - cov0
+    assert torch.equal(c, c.T)
+
+
+def test_k8_strided_activations():
+    g = torch.Generator().manual_seed(3)
+    big = torch.randn(50, 2048 + 32, generator=g)
+    act = big[:, :2048]
+    cov = torch.zeros(2048, 2048, device=DEV)
+    native().fid_cov_update(act.to(DEV), cov, None)
+    torch.testing.assert_close(cov.cpu().double(), act.double().T @ act.double(), rtol=1e-4, atol=1e-2)
+
+
+def test_fid_class_gpu_matches_cpu():
+    torch.manual_seed(0)
+    d = 256
+
+    class Feat(torch.nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.register_buffer("p", torch.randn(3 * 64, d))
+
+        def forward(self, x):
+            return torch.nn.functional.adaptive_avg_pool2d(x, 8).flatten(1) @ self.p
+
+    model = Feat()
+    real, fake = torch.rand(96, 3, 16, 16), torch.rand(96, 3, 16, 16) ** 2
+    cpu = FrechetInceptionDistance(model=model, feature_dim=d)
+    gpu = FrechetInceptionDistance(model=Feat().to(DEV), feature_dim=d, device=DEV)
+    gpu.model.load_state_dict(model.state_dict())
+    for i in range(3):
+        sl = slice(32 * i, 32 * (i + 1))
+        cpu.update(real[sl], True).update(fake[sl], False)
+        gpu.update(real[sl].to(DEV), True).update(fake[sl].to(DEV), False)
+    torch.testing.assert_close(gpu.compute().cpu(), cpu.compute(), rtol=1e-3, atol=1e-2)
+
+
+def test_fid_default_inception_gpu():
+    with pytest.warns(RuntimeWarning):
+        m = FrechetInceptionDistance(device=DEV)
+    imgs = torch.rand(4, 3, 299, 299, device=DEV)
+    m.update(imgs, True).update(imgs.flip(-1), False)
+    v = m.compute()
+    assert torch.isfinite(v)
+
+
+# ----------------------------------------------------------------------------- window on GPU (K6)
+def test_windowed_ne_gpu():
+    g = torch.Generator().manual_seed(9)
+    m = WindowedBinaryNormalizedEntropy(num_tasks=2, max_num_updates=3, device=DEV)
+    xs, ts = [], []
+    for _ in range(5):
+        x, t = torch.rand(2, 500, generator=g), torch.randint(0, 2, (2, 500), generator=g).float()
+        m.update(x.to(DEV), t.to(DEV))
+        xs.append(x), ts.append(t)
+    life, win = m.compute()
+    torch.testing.assert_close(life.cpu(), binary_normalized_entropy(torch.cat(xs, 1).double(), torch.cat(ts, 1).double(), num_tasks=2), rtol=1e-6, atol=1e-8)
+    torch.testing.assert_close(win.cpu(), binary_normalized_entropy(torch.cat(xs[-3:], 1).double(), torch.cat(ts[-3:], 1).double(), num_tasks=2), rtol=1e-6, atol=1e-8)

@@ -1,0 +1,174 @@
+"""Frechet Inception Distance (parity: metrics/image/fid.py:53-274).
+
+MI355X path:
+* update: features from the model, then the K8 FP32-MFMA symmetric rank-k kernel adds
+  act^T act (upper-triangle tiles, mirrored) and the column sums straight into the states -
+  half the FLOPs of the reference's dense ``act.T @ act`` and no separate ``sum``;
+* compute: tr sqrt(S1 S2) via two symmetric eigendecompositions in FP64,
+  tr sqrt(S1^1/2 S2 S1^1/2), instead of the reference's non-symmetric ``linalg.eigvals``
+  (better conditioned; identical in exact arithmetic);
+* sync: every state is ``merge="sum"``, so syncing is one RCCL all-reduce of 2 x D^2 + 2 x D
+  floats; the model itself is never pickled or transferred (the reference all-gathers the
+  whole pickled metric, Inception-v3 included).
+"""
+
+import warnings
+from typing import Any, Iterable, Optional, Union
+
+import torch
+from torch import nn, Tensor
+
+from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.models.inception import FIDInceptionV3
+from torcheval_amd.ops import use_native
+
+__all__ = ["FrechetInceptionDistance", "FIDInceptionV3"]
+
+
+def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
+    if (
+        use_native(act)
+        and act.dtype == torch.float32
+        and cov_sum.dtype == torch.float32
+        and col_sum.dtype == torch.float32
+        and act.dim() == 2
+    ):
+        from torcheval_amd.ops import native
+
+        a = act if (act.stride(1) == 1 and act.stride(0) % 4 == 0 and act.data_ptr() % 16 == 0) else act.contiguous()
+        native().fid_cov_update(a, cov_sum, col_sum)
+        return
+    col_sum += torch.sum(act, dim=0)
+    cov_sum += torch.matmul(act.T, act)
+
+
+def frechet_distance(mu1: Tensor, sigma1: Tensor, mu2: Tensor, sigma2: Tensor) -> Tensor:
+    """||mu1 - mu2||^2 + tr S1 + tr S2 - 2 tr sqrt(S1^1/2 S2 S1^1/2)  (FP64 symmetric eigh)."""
+    mu1, mu2 = mu1.double(), mu2.double()
+    s1 = sigma1.double()
+    s2 = sigma2.double()
+    s1 = (s1 + s1.T) / 2
+    s2 = (s2 + s2.T) / 2
+    lam, vec = torch.linalg.eigh(s1)
+    root = (vec * lam.clamp(min=0).sqrt()) @ vec.T
+    m = root @ s2 @ root
+    ev = torch.linalg.eigvalsh((m + m.T) / 2)
+    tr_sqrt = ev.clamp(min=0).sqrt().sum()
+    return (mu1 - mu2).square().sum() + s1.trace() + s2.trace() - 2 * tr_sqrt
+
+
+class FrechetInceptionDistance(Metric[torch.Tensor]):
+    """
+    FID between real and generated images.
+
+    Args:
+        model: feature extractor mapping images to [B, feature_dim] activations; default the
+            native Inception-v3 (``FIDInceptionV3``, random weights unless a local checkpoint
+            is supplied - see ``torcheval_amd.models.inception``).
+        feature_dim: activation width (2048 for the default model).
+    """
+
+    def __init__(
+        self,
+        model: Optional[nn.Module] = None,
+        feature_dim: int = 2048,
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        self._FID_parameter_check(model=model, feature_dim=feature_dim)
+        if model is None:
+            model = FIDInceptionV3()
+        self.model = model.to(self.device)
+        self.model.eval()
+        d = feature_dim
+        self._add_state("real_sum", torch.zeros(d, device=self.device), merge="sum")
+        self._add_state("real_cov_sum", torch.zeros((d, d), device=self.device), merge="sum")
+        self._add_state("fake_sum", torch.zeros(d, device=self.device), merge="sum")
+        self._add_state("fake_cov_sum", torch.zeros((d, d), device=self.device), merge="sum")
+        self._add_state("num_real_images", torch.tensor(0, device=self.device).int(), merge="sum")
+        self._add_state("num_fake_images", torch.tensor(0, device=self.device).int(), merge="sum")
+
+    @torch.inference_mode()
+    def update(self, images: Tensor, is_real: bool) -> "FrechetInceptionDistance":
+        """Add a batch of [B, 3, H, W] images (float32 in [0, 1] for the default model)."""
+        self._FID_update_input_check(images=images, is_real=is_real)
+        images = images.to(self.device)
+        activations = self.model(images)
+        return self.update_activations(activations, is_real)
+
+    @torch.inference_mode()
+    def update_activations(self, activations: Tensor, is_real: bool) -> "FrechetInceptionDistance":
+        """Add precomputed [B, feature_dim] activations (skips the feature extractor)."""
+        activations = activations.to(self.device)
+        b = activations.shape[0]
+        if is_real:
+            self.num_real_images += b
+            _cov_update(activations, self.real_cov_sum, self.real_sum)
+        else:
+            self.num_fake_images += b
+            _cov_update(activations, self.fake_cov_sum, self.fake_sum)
+        return self
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["FrechetInceptionDistance"]) -> "FrechetInceptionDistance":
+        for metric in metrics:
+            self.real_sum += metric.real_sum.to(self.device)
+            self.real_cov_sum += metric.real_cov_sum.to(self.device)
+            self.fake_sum += metric.fake_sum.to(self.device)
+            self.fake_cov_sum += metric.fake_cov_sum.to(self.device)
+            self.num_real_images += metric.num_real_images.to(self.device)
+            self.num_fake_images += metric.num_fake_images.to(self.device)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> Tensor:
+        nr, nf = int(self.num_real_images), int(self.num_fake_images)
+        if nr == 0 or nf == 0:
+            warnings.warn(
+                "Computing FID requires at least 1 real image and 1 fake image,"
+                f"but currently running with {nr} real images and {nf} fake images."
+                "Returning 0.0",
+                RuntimeWarning,
+            )
+            return torch.tensor(0.0)
+        real_mean = self.real_sum.double() / nr
+        fake_mean = self.fake_sum.double() / nf
+        real_cov = (self.real_cov_sum.double() - nr * torch.outer(real_mean, real_mean)) / (nr - 1)
+        fake_cov = (self.fake_cov_sum.double() - nf * torch.outer(fake_mean, fake_mean)) / (nf - 1)
+        return frechet_distance(real_mean, real_cov, fake_mean, fake_cov).to(torch.float32)
+
+    def _calculate_frechet_distance(self, mu1: Tensor, sigma1: Tensor, mu2: Tensor, sigma2: Tensor) -> Tensor:
+        return frechet_distance(mu1, sigma1, mu2, sigma2)
+
+    def _FID_parameter_check(self, model: Optional[nn.Module], feature_dim: int) -> None:
+        if feature_dim is None or feature_dim <= 0:
+            raise RuntimeError("feature_dim has to be a positive integer")
+        if model is None and feature_dim != 2048:
+            raise RuntimeError(
+                "When the default Inception v3 model is used, feature_dim needs to be set to 2048"
+            )
+
+    def _FID_update_input_check(self, images: Tensor, is_real: bool) -> None:
+        if not torch.is_tensor(images):
+            raise ValueError(f"Expected tensor as input, but got {type(images)}.")
+        if images.dim() != 4:
+            raise ValueError(f"Expected 4D tensor as input. But input has {images.dim()} dimenstions.")
+        if images.size()[1] != 3:
+            raise ValueError(f"Expected 3 channels as input. Got {images.size()[1]}.")
+        if type(is_real) != bool:
+            raise ValueError(f"Expected 'real' to be of type bool but got {type(is_real)}.")
+        if isinstance(self.model, FIDInceptionV3):
+            if images.dtype != torch.float32:
+                raise ValueError(
+                    "When default inception-v3 model is used, images expected to be `torch.float32`, "
+                    f"but got {images.dtype}."
+                )
+            if images.min() < 0 or images.max() > 1:
+                raise ValueError(
+                    "When default inception-v3 model is used, images are expected to be in the [0, 1] interval"
+                )
+
+    def to(self, device: Union[str, torch.device], *args: Any, **kwargs: Any) -> "FrechetInceptionDistance":
+        super().to(device, *args, **kwargs)
+        self.model.to(self.device)
+        return self

@@ -1,0 +1,53 @@
+"""PSNR, class API (parity: metrics/image/psnr.py:24-129).
+
+``data_range`` is recomputed from the merged target min / max when auto-ranging, so the
+states use the metric's own ``merge_state`` during sync (merge kind ``None``).
+"""
+
+from typing import Iterable, Optional
+
+import torch
+
+from torcheval_amd.metrics.functional.image import _psnr_compute, _psnr_param_check, _psnr_update
+from torcheval_amd.metrics.metric import Metric
+
+
+class PeakSignalNoiseRatio(Metric[torch.Tensor]):
+    """Peak signal-to-noise ratio over all updates; ``data_range=None`` tracks the target range."""
+
+    def __init__(self, data_range: Optional[float] = None, *, device: Optional[torch.device] = None) -> None:
+        super().__init__(device=device)
+        _psnr_param_check(data_range=data_range)
+        self.auto_range = data_range is None
+        self._add_state("data_range", torch.tensor(0.0 if data_range is None else data_range, device=self.device))
+        self._add_state("num_observations", torch.tensor(0.0, device=self.device))
+        self._add_state("sum_squared_error", torch.tensor(0.0, device=self.device))
+        self._add_state("min_target", torch.tensor(torch.inf, device=self.device))
+        self._add_state("max_target", torch.tensor(-torch.inf, device=self.device))
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "PeakSignalNoiseRatio":
+        sse, n = _psnr_update(input, target)
+        self.sum_squared_error = self.sum_squared_error + sse
+        self.num_observations = self.num_observations + n
+        if self.auto_range:
+            self.min_target = torch.minimum(target.min(), self.min_target)
+            self.max_target = torch.maximum(target.max(), self.max_target)
+            self.data_range = self.max_target - self.min_target
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        return _psnr_compute(self.sum_squared_error, self.num_observations, self.data_range)
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["PeakSignalNoiseRatio"]) -> "PeakSignalNoiseRatio":
+        for metric in metrics:
+            self.num_observations = self.num_observations + metric.num_observations.to(self.device)
+            self.sum_squared_error = self.sum_squared_error + metric.sum_squared_error.to(self.device)
+            if self.auto_range:
+                self.min_target = torch.minimum(self.min_target, metric.min_target.to(self.device))
+                self.max_target = torch.maximum(self.max_target, metric.max_target.to(self.device))
+        if self.auto_range:
+            self.data_range = self.max_target - self.min_target
+        return self

@@ -1,0 +1,124 @@
+"""Shared ring-buffer machinery for the windowed metrics (parity: metrics/window/*.py).
+
+The reference re-implements the same ring bookkeeping in five classes.  Here one base class
+owns it:
+
+* every windowed quantity is a ``[num_tasks, width]`` state whose column ``next_inserted`` is
+  overwritten per update; untouched columns are zero, so the windowed total is simply a sum
+  over the width (no data-dependent slicing, no host sync);
+* ``_filled`` counts valid columns so ``merge_state`` can *compact* the valid columns of all
+  ranks into one window of width ``sum(max_num_updates)`` and keep a well-defined ring
+  afterwards (the reference leaves ``max_num_updates`` at the local width after a merge, so a
+  later ``update()`` lands inside another rank's columns);
+* lifetime accumulators are ordinary per-task states.
+"""
+
+from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+
+import torch
+
+from torcheval_amd.metrics.metric import Metric
+
+
+def _check_window_args(num_tasks: int, max_num: int, what: str) -> None:
+    if num_tasks < 1:
+        raise ValueError(
+            "`num_tasks` value should be greater than and equal to 1, but received {num_tasks}. "
+        )
+    if max_num < 1:
+        raise ValueError(
+            f"`{what}` value should be greater than and equal to 1, but received {{{what}}}. "
+        )
+
+
+class _WindowedSums(Metric):
+    """Base for windows of per-update sums; subclasses declare ``_WINDOW`` and ``_LIFETIME``
+    (state name -> dtype) and call ``_push(values)`` from ``update``."""
+
+    _WINDOW: Sequence[Tuple[str, torch.dtype]] = ()
+    _LIFETIME: Sequence[Tuple[str, torch.dtype]] = ()
+
+    def __init__(
+        self,
+        *,
+        num_tasks: int,
+        max_num_updates: int,
+        enable_lifetime: bool,
+        device: Optional[torch.device],
+        lifetime_shape: Optional[Tuple[int, ...]] = None,
+        check_max: bool = True,
+    ) -> None:
+        super().__init__(device=device)
+        if check_max:
+            _check_window_args(num_tasks, max_num_updates, "max_num_updates")
+        elif num_tasks < 1:
+            _check_window_args(num_tasks, 1, "max_num_updates")
+        self.num_tasks = num_tasks
+        self.enable_lifetime = enable_lifetime
+        self.next_inserted = 0
+        self._filled = 0
+        self._add_state("max_num_updates", max_num_updates)
+        self._add_state("total_updates", 0)
+        shape = lifetime_shape if lifetime_shape is not None else (num_tasks,)
+        if enable_lifetime:
+            for name, dt in self._LIFETIME:
+                self._add_state(name, torch.zeros(shape, dtype=dt, device=self.device))
+        for name, dt in self._WINDOW:
+            self._add_state(name, torch.zeros(num_tasks, max_num_updates, dtype=dt, device=self.device))
+
+    # ---------------------------------------------------------------- ring bookkeeping
+    def _push(self, values: Sequence[torch.Tensor]) -> None:
+        slot = self.next_inserted
+        for (name, _), v in zip(self._WINDOW, values):
+            getattr(self, name)[:, slot] = v
+        width = getattr(self, self._WINDOW[0][0]).shape[1]
+        self.next_inserted = (slot + 1) % width
+        self._filled = min(self._filled + 1, width)
+        self.total_updates += 1
+
+    def _window_totals(self) -> List[torch.Tensor]:
+        return [getattr(self, name).sum(dim=-1) for name, _ in self._WINDOW]
+
+    def _empty_result(self):
+        if self.enable_lifetime:
+            return torch.empty(0), torch.empty(0)
+        return torch.empty(0)
+
+    def reset(self):
+        super().reset()
+        self.next_inserted = 0
+        self._filled = 0
+        return self
+
+    def load_state_dict(self, state_dict: Dict, strict: bool = True) -> None:
+        super().load_state_dict(state_dict, strict)
+        width = getattr(self, self._WINDOW[0][0]).shape[1]
+        self._filled = min(int(self.total_updates), width)
+        self.next_inserted = int(self.total_updates) % width
+
+    def _merge_lifetime(self, metric: "_WindowedSums") -> None:
+        for name, _ in self._LIFETIME:
+            setattr(self, name, getattr(self, name) + getattr(metric, name).to(self.device))
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["_WindowedSums"]):
+        metrics = list(metrics)
+        everyone = [self] + metrics
+        width = sum(int(m.max_num_updates) for m in everyone)
+        for name, dt in self._WINDOW:
+            merged = torch.zeros(self.num_tasks, width, dtype=dt, device=self.device)
+            idx = 0
+            for m in everyone:
+                k = m._filled
+                merged[:, idx : idx + k] = getattr(m, name)[:, :k].to(self.device)
+                idx += k
+            setattr(self, name, merged)
+        if self.enable_lifetime:
+            for m in metrics:
+                self._merge_lifetime(m)
+        filled = sum(m._filled for m in everyone)
+        self.total_updates = sum(int(m.total_updates) for m in everyone)
+        self.max_num_updates = width
+        self._filled = filled
+        self.next_inserted = filled % width
+        return self

@@ -1,0 +1,52 @@
+"""Windowed click-through rate (parity: metrics/window/click_through_rate.py:19)."""
+
+from typing import Optional, Tuple, Union
+
+import torch
+
+from torcheval_amd.metrics.functional.ranking import (
+    _click_through_rate_compute,
+    _click_through_rate_update,
+)
+from torcheval_amd.metrics.window._ring import _WindowedSums
+
+
+class WindowedClickThroughRate(_WindowedSums):
+    """CTR over the last ``max_num_updates`` updates (and lifetime when ``enable_lifetime``).
+
+    ``compute()`` returns ``(lifetime, windowed)`` or ``windowed``; empty tensors before any update."""
+
+    _WINDOW = (("windowed_click_total", torch.float64), ("windowed_weight_total", torch.float64))
+    _LIFETIME = (("click_total", torch.float64), ("weight_total", torch.float64))
+
+    def __init__(
+        self,
+        *,
+        num_tasks: int = 1,
+        max_num_updates: int = 100,
+        enable_lifetime: bool = True,
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(
+            num_tasks=num_tasks, max_num_updates=max_num_updates,
+            enable_lifetime=enable_lifetime, device=device,
+        )
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, weights: Union[torch.Tensor, float, int] = 1.0):
+        click_total, weight_total = _click_through_rate_update(input, weights, num_tasks=self.num_tasks)
+        if self.enable_lifetime:
+            self.click_total += click_total
+            self.weight_total += weight_total
+        self._push((click_total, weight_total))
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
+        if self.total_updates == 0:
+            return self._empty_result()
+        click, weight = self._window_totals()
+        windowed = _click_through_rate_compute(click, weight)
+        if self.enable_lifetime:
+            return _click_through_rate_compute(self.click_total, self.weight_total), windowed
+        return windowed
