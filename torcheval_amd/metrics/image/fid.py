@@ -36,8 +36,9 @@ def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
         from torcheval_amd.ops import native
 
         a = act if (act.stride(1) == 1 and act.stride(0) % 4 == 0 and act.data_ptr() % 16 == 0) else act.contiguous()
-        native().fid_cov_update(a, cov_sum, col_sum)
-        return
+        if a.stride(0) % 4 == 0:  # K8 streams 16-B row segments
+            native().fid_cov_update(a, cov_sum, col_sum)
+            return
     col_sum += torch.sum(act, dim=0)
     cov_sum += torch.matmul(act.T, act)
 
