@@ -1,0 +1,245 @@
+"""Per-config benchmark suite for the BASELINE.md table on ONE MI355X.
+
+Every row runs twice on the same GPU and the same tensors:
+  * ``native``  - the framework's HIP/CDNA4 kernels (the default path);
+  * ``aten``    - the same metric with ``TORCHEVAL_AMD_DISABLE_HIP`` semantics, i.e. the eager
+                  ATen op chains (the reference's execution model) on the GPU.
+The CPU numbers of the reference itself are in BASELINE.md and are quoted per row.
+
+Usage: python benchmarks/bench_suite.py [--only NAME] [--out profiles/bench_suite.json]
+       python benchmarks/bench_suite.py --smoke      (tiny shapes on CPU: plumbing check)
+"""
+
+import argparse
+import json
+import os
+import sys
+import time
+from typing import Callable, Dict, List, Optional
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torcheval_amd.ops as ops  # noqa: E402
+from torcheval_amd import metrics as M  # noqa: E402
+from torcheval_amd.metrics import functional as F  # noqa: E402
+
+# BASELINE.md "measured here" reference numbers (8-core CPU), ms per call
+REF_CPU_MS = {
+    "MulticlassAccuracy.update micro bs8192 C1000": 1000 / 351,
+    "MulticlassAccuracy.update macro bs8192 C1000": 1000 / 423,
+    "MulticlassConfusionMatrix(1000).update bs8192": 1000 / 224,
+    "binary_auroc N=1M": 124.0,
+    "BinaryAUROC.update+compute N=1M": 132.0,
+    "binary_binned_auroc N=1M T=200": 730.0,
+    "binary_binned_precision_recall_curve N=1M T=100": 12.4,
+    "BinaryBinnedAUPRC(200).update N=1M": 13.5,
+    "multiclass_auroc N=100k C=100": 637.0,
+    "multiclass_auprc N=100k C=100": 668.0,
+    "MulticlassBinnedAUPRC(C=100,T=100).update N=100k": 200.0,
+    "MultilabelAccuracy(hamming).update 8192x1000": 29.3,
+    "topk_multilabel_accuracy 8192x1000": 12.9,
+    "perplexity (4,1024,32000)": 123.0,
+    "mean_squared_error 8192x1000": 6.7,
+    "r2_score 8192x1000": 15.7,
+    "FID update 1000x2048 activations": 1570.0 / 100,
+    "FID compute D=2048": 2850.0,
+}
+
+
+def _time(fn: Callable[[], object], dev: torch.device, min_time: float, max_iters: int) -> float:
+    fn()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    # calibrate
+    t0 = time.perf_counter()
+    fn()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    one = max(time.perf_counter() - t0, 1e-6)
+    iters = int(max(3, min(max_iters, min_time / one)))
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e3
+
+
+def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], object]]]:
+    """name -> factory returning a zero-arg callable; ``s`` scales sizes (1.0 = BASELINE)."""
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def n(x: int) -> int:
+        return max(8, int(x * s))
+
+    def rand(*shape):
+        return torch.rand(*shape, device=dev, generator=g)
+
+    def randint(hi, *shape):
+        return torch.randint(0, hi, shape, device=dev, generator=g)
+
+    B, C = n(8192), 1000 if s >= 1 else 10
+
+    def acc(avg):
+        def make():
+            x, y = torch.randn(B, C, device=dev, generator=g), randint(C, B)
+            m = M.MulticlassAccuracy(average=avg, num_classes=C, device=dev)
+            return lambda: m.update(x, y)
+        return make
+
+    def confusion():
+        x, y = torch.randn(B, C, device=dev, generator=g), randint(C, B)
+        m = M.MulticlassConfusionMatrix(C, device=dev)
+        return lambda: m.update(x, y)
+
+    N1M = n(1_000_000)
+
+    def bauroc():
+        x, y = rand(N1M), randint(2, N1M)
+        return lambda: F.binary_auroc(x, y)
+
+    def bauroc_cls():
+        x, y = rand(N1M), randint(2, N1M)
+
+        def run():
+            m = M.BinaryAUROC(device=dev)
+            m.update(x, y)
+            return m.compute()
+        return run
+
+    def binned_auroc():
+        x, y = rand(N1M), randint(2, N1M)
+        return lambda: F.binary_binned_auroc(x, y, threshold=200)
+
+    def binned_prc():
+        x, y = rand(N1M), randint(2, N1M)
+        return lambda: F.binary_binned_precision_recall_curve(x, y, threshold=100)
+
+    def binned_auprc_cls():
+        x, y = rand(N1M), randint(2, N1M)
+        m = M.BinaryBinnedAUPRC(threshold=200, device=dev)
+        return lambda: m.update(x, y)
+
+    N100k, C100 = n(100_000), 100 if s >= 1 else 5
+
+    def mc_auroc():
+        x, y = rand(N100k, C100), randint(C100, N100k)
+        return lambda: F.multiclass_auroc(x, y, num_classes=C100)
+
+    def mc_auprc():
+        x, y = rand(N100k, C100), randint(C100, N100k)
+        return lambda: F.multiclass_auprc(x, y, num_classes=C100)
+
+    def mc_binned_auprc_cls():
+        x, y = rand(N100k, C100), randint(C100, N100k)
+        m = M.MulticlassBinnedAUPRC(num_classes=C100, threshold=100, device=dev)
+        return lambda: m.update(x, y)
+
+    def ml_hamming():
+        x, y = rand(B, C), randint(2, B, C)
+        m = M.MultilabelAccuracy(criteria="hamming", device=dev)
+        return lambda: m.update(x, y)
+
+    def topk_ml():
+        x, y = rand(B, C), randint(2, B, C)
+        return lambda: F.topk_multilabel_accuracy(x, y, k=2)
+
+    def ppl():
+        V = 32000 if s >= 1 else 50
+        x, y = torch.randn(4, n(1024), V, device=dev, generator=g), randint(V, 4, n(1024))
+        return lambda: F.perplexity(x, y)
+
+    def mse():
+        x, y = rand(B, C), rand(B, C)
+        return lambda: F.mean_squared_error(x, y)
+
+    def r2():
+        x, y = rand(B, C), rand(B, C)
+        return lambda: F.r2_score(x, y)
+
+    D = 2048 if s >= 1 else 64
+
+    def fid_update():
+        from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
+
+        act = torch.randn(n(1000), D, device=dev, generator=g)
+        m = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=D, device=dev)
+        return lambda: m.update_activations(act, True)
+
+    def fid_compute():
+        from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
+
+        m = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=D, device=dev)
+        for real in (True, False):
+            m.update_activations(torch.randn(4 * D, D, device=dev, generator=g) * (1.0 if real else 1.1), real)
+        return m.compute
+
+    return {
+        "MulticlassAccuracy.update micro bs8192 C1000": acc("micro"),
+        "MulticlassAccuracy.update macro bs8192 C1000": acc("macro"),
+        "MulticlassConfusionMatrix(1000).update bs8192": confusion,
+        "binary_auroc N=1M": bauroc,
+        "BinaryAUROC.update+compute N=1M": bauroc_cls,
+        "binary_binned_auroc N=1M T=200": binned_auroc,
+        "binary_binned_precision_recall_curve N=1M T=100": binned_prc,
+        "BinaryBinnedAUPRC(200).update N=1M": binned_auprc_cls,
+        "multiclass_auroc N=100k C=100": mc_auroc,
+        "multiclass_auprc N=100k C=100": mc_auprc,
+        "MulticlassBinnedAUPRC(C=100,T=100).update N=100k": mc_binned_auprc_cls,
+        "MultilabelAccuracy(hamming).update 8192x1000": ml_hamming,
+        "topk_multilabel_accuracy 8192x1000": topk_ml,
+        "perplexity (4,1024,32000)": ppl,
+        "mean_squared_error 8192x1000": mse,
+        "r2_score 8192x1000": r2,
+        "FID update 1000x2048 activations": fid_update,
+        "FID compute D=2048": fid_compute,
+    }
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--smoke", action="store_true")
+    ap.add_argument("--min-time", type=float, default=0.5)
+    ap.add_argument("--no-aten", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cpu") if args.smoke else torch.device("cuda", 0)
+    scale = 0.001 if args.smoke else 1.0
+    rows: List[Dict[str, object]] = []
+    for name, make in cases(dev, scale).items():
+        if args.only and args.only not in name:
+            continue
+        row: Dict[str, object] = {"case": name}
+        for mode in ("native", "aten"):
+            if mode == "aten" and args.no_aten:
+                continue
+            ops.DISABLE_HIP = mode == "aten"
+            try:
+                fn = make()
+                row[f"{mode}_ms"] = round(_time(fn, dev, args.min_time, 20000), 4)
+            except Exception as e:  # report, keep going
+                row[f"{mode}_ms"] = None
+                row[f"{mode}_error"] = f"{type(e).__name__}: {e}"[:200]
+            finally:
+                ops.DISABLE_HIP = False
+            if dev.type == "cuda":
+                torch.cuda.empty_cache()
+        ref = REF_CPU_MS.get(name)
+        row["reference_cpu_ms"] = None if ref is None else round(ref, 3)
+        if row.get("native_ms"):
+            if row.get("aten_ms"):
+                row["speedup_vs_aten_same_gpu"] = round(row["aten_ms"] / row["native_ms"], 2)
+            if ref:
+                row["speedup_vs_reference_cpu"] = round(ref / row["native_ms"], 1)
+        rows.append(row)
+        print(json.dumps(row), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump({"device": torch.cuda.get_device_name(0) if dev.type == "cuda" else "cpu", "rows": rows}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

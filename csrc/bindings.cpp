@@ -352,6 +352,11 @@ void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
     TORCH_CHECK(sw->scalar_type() == at::kFloat && sw->numel() == 1, "column_moments: sw scalar f32");
     a.sw = sw->data_ptr<float>();
   }
+  if (a.n == 0 || a.d == 0) return;
+  a.ws_blocks = tea::column_moments_blocks(a.n, a.d);
+  const int64_t nstats = (a.sse != nullptr) + (a.st != nullptr) + (a.stt != nullptr) + (a.sx != nullptr);
+  Tensor ws = at::empty({a.ws_blocks * (nstats * a.d + 1)}, ref.options().dtype(at::kDouble));
+  a.ws = ws.data_ptr<double>();
   check_launch(tea::launch_column_moments(a, stream_for(ref)), "column_moments");
 }
 
@@ -444,6 +449,53 @@ void fid_cov_update(const Tensor& act, const Tensor& cov, const optional<Tensor>
   check_launch(tea::launch_fid_cov(a, stream_for(act)), "fid_cov_update");
 }
 
+
+// K2: multilabel accuracy counts straight into float32 state scalars.
+void multilabel_counts(const Tensor& input, const Tensor& target, double threshold, int64_t k,
+                       int64_t criteria, const Tensor& num_correct, const optional<Tensor>& num_total,
+                       double total) {
+  check_gpu(input, "input");
+  check_gpu(target, "target");
+  TORCH_CHECK(input.dim() == 2 && target.sizes() == input.sizes(),
+              "multilabel_counts: input/target must be [n, c] of equal shape");
+  TORCH_CHECK(input.stride(1) == 1 && target.stride(1) == 1,
+              "multilabel_counts: rows must be contiguous");
+  TORCH_CHECK(num_correct.scalar_type() == at::kFloat && num_correct.numel() == 1 &&
+                  num_correct.device() == input.device(),
+              "multilabel_counts: num_correct must be a float32 scalar on the input device");
+  TORCH_CHECK(criteria >= 0 && criteria <= 4, "multilabel_counts: bad criteria");
+  TORCH_CHECK(k == 0 || (k >= 1 && k <= input.size(1) && input.size(1) <= tea::multilabel_max_topk_cols()),
+              "multilabel_counts: top-k needs 1 <= k <= c <= ", tea::multilabel_max_topk_cols());
+  TORCH_CHECK(criteria != 1 || input.numel() < (int64_t{1} << 31),
+              "multilabel_counts: hamming counts must fit 31 bits per launch");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(input.device());
+  hipStream_t stream = stream_for(input);
+  tea::MultilabelArgs a;
+  a.x = input.data_ptr();
+  a.x_dt = dt_of(input);
+  a.x_row_stride = input.stride(0);
+  a.t = target.data_ptr();
+  a.t_dt = dt_of(target);
+  a.t_row_stride = target.stride(0);
+  a.n = input.size(0);
+  a.c = input.size(1);
+  a.threshold = static_cast<float>(threshold);
+  a.k = static_cast<int>(k);
+  a.criteria = static_cast<int>(criteria);
+  a.num_correct = num_correct.data_ptr<float>();
+  if (num_total.has_value()) {
+    TORCH_CHECK(num_total->scalar_type() == at::kFloat && num_total->numel() == 1,
+                "multilabel_counts: num_total must be a float32 scalar");
+    a.num_total = num_total->data_ptr<float>();
+    a.total = total;
+  }
+  a.fold_ws = fold_workspace(input, stream);
+  const int rc = tea::launch_multilabel(a, stream);
+  TORCH_CHECK(rc != -1, "multilabel_counts: unsupported dtypes ", input.scalar_type(), "/",
+              target.scalar_type());
+  check_launch(rc, "multilabel_counts");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -473,6 +525,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"));
   m.def("perplexity_sums", &perplexity_sums, "K7 fused log-softmax gather", py::arg("input"),
         py::arg("target"), py::arg("ignore_index"), py::arg("out"), py::arg("err"));
+  m.def("multilabel_counts", &multilabel_counts, "K2 multilabel accuracy counts", py::arg("input"),
+        py::arg("target"), py::arg("threshold"), py::arg("k"), py::arg("criteria"),
+        py::arg("num_correct"), py::arg("num_total") = py::none(), py::arg("total") = 0.0);
   m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
         py::arg("act"), py::arg("cov"), py::arg("colsum"));
   tea_register_runtime(m);

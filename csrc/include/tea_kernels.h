@@ -136,7 +136,10 @@ struct MomentsArgs {
   float* sx = nullptr;
   float* sw = nullptr;   // scalar
   int64_t out_stride = 1;
+  double* ws = nullptr;  // [ws_blocks, n_requested_stats * d + 1] FP64 partials (caller-allocated)
+  int ws_blocks = 0;
 };
+int column_moments_blocks(int64_t n, int64_t d);
 int launch_column_moments(const MomentsArgs& a, hipStream_t stream);
 
 // ------------------------------------------------------------------ K6 normalized entropy
@@ -189,4 +192,26 @@ struct FidCovArgs {
 };
 int launch_fid_cov(const FidCovArgs& a, hipStream_t stream);
 
+}  // namespace tea
+
+// ------------------------------------------------------------------ K2 multilabel accuracy
+namespace tea {
+struct MultilabelArgs {
+  const void* x = nullptr;  // [n, c] scores (f32 / bf16 / f16), rows at x_row_stride
+  DType x_dt = DType::f32;
+  int64_t x_row_stride = 0;
+  const void* t = nullptr;  // [n, c] targets (f32 / i64 / i32 / u8 / bool)
+  DType t_dt = DType::f32;
+  int64_t t_row_stride = 0;
+  int64_t n = 0, c = 0;
+  float threshold = 0.5f;
+  int k = 0;         // > 0: top-k labels instead of thresholding
+  int criteria = 0;  // 0 exact_match, 1 hamming, 2 overlap, 3 contain, 4 belong
+  float* num_correct = nullptr;  // accumulated
+  float* num_total = nullptr;    // optional: += total (block 0)
+  double total = 0.0;
+  unsigned long long* fold_ws = nullptr;
+};
+int multilabel_max_topk_cols();
+int launch_multilabel(const MultilabelArgs& a, hipStream_t stream);
 }  // namespace tea

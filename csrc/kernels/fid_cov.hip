@@ -1,19 +1,26 @@
 // K8: FID covariance update C += A^T A, s += colsum(A) on FP32 MFMA.
 //
 // Replaces fid.py:120-127 (a full D x D x B SGEMM plus a separate column sum) with one
-// symmetric rank-k update that computes only the upper-triangle 128 x 128 tiles (half the
-// FLOPs) and mirrors them, with the column sums fused into the diagonal tiles.
+// symmetric rank-k update that computes only the upper-triangle tiles (half the FLOPs),
+// mirrors them, and fuses the column sums into the diagonal tiles.
 //
-// gfx950 mapping:
-//  * v_mfma_f32_32x32x2_f32 (exact FP32 fmaf chains, 64 FLOP/clk/SIMD): the A-operand lane
-//    holds A^T[i][k] = act[k][i], the B-operand lane act[k][j] - both are reads of row k of
-//    the activation matrix, so the K loop streams rows of ``act`` (128 consecutive floats =
-//    512 B per row segment, fully coalesced) into LDS.
-//  * 256-thread blocks, 4 waves, each wave a 64 x 64 sub-tile = 2 x 2 MFMA tiles
-//    (4 x 16 accumulator registers); LDS double buffer of 2 x (BK x 128) floats per operand.
-//  * epilogue stages the 128 x 128 tile in LDS (padded rows) so both C[I,J] and the mirrored
-//    C[J,I] are read-modify-written with coalesced rows.  Each output tile is owned by one
-//    block, so no atomics.
+// gfx950 mapping (v2, after profiling v1's 128 x 128 tiles: 136 blocks for D = 2048 left half
+// of the 256 CUs idle and the "prefetch" stalled on its own loads):
+//  * 64 x 64 output tiles, 256 threads = 4 waves, each wave one 32 x 32 block accumulated by
+//    v_mfma_f32_32x32x2_f32 (exact FP32 products, 16 accumulator VGPRs).  D = 2048 gives 528
+//    tiles (> 2 per CU) and ~5 resident blocks per CU by LDS.
+//  * the K loop streams rows of ``act``: both MFMA operands of sample k are reads of row k
+//    (A-operand lane = act[k][I0 + i], B-operand lane = act[k][J0 + j]), 64 consecutive floats
+//    = 256 B per row segment, loaded as float4 (16 threads per row).
+//  * BK = 32 rows per stage, LDS double buffer, register-staged prefetch: the next stage's
+//    global loads are issued before the current stage's 16 MFMAs and only written to LDS
+//    after them, so HBM/L2 latency overlaps the matrix work.
+//  * XCD-aware tile order: blocks are dealt round-robin to the 8 XCDs, so block b is remapped
+//    to tile (b % 8) * (nb / 8) + b / 8 - each XCD owns a contiguous run of row-panel tiles and
+//    reuses the same activation panel from its own L2.
+//  * epilogue stages the tile in LDS (64 x 65, conflict-free for the transposed read) and
+//    read-modify-writes C[I, J] and the mirrored C[J, I] with coalesced rows; one block owns
+//    each output tile, so there are no atomics and the result is deterministic.
 #include "tea_common.h"
 #include "tea_kernels.h"
 
@@ -21,10 +28,11 @@ namespace tea {
 
 namespace {
 
-constexpr int kTile = 128;
-constexpr int kBK = 16;
+constexpr int kTile = 64;
+constexpr int kBK = 32;
 constexpr int kThreads = 256;
 constexpr int kPad = kTile + 1;
+constexpr int kStage = kBK * kTile;  // floats per operand per stage
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -39,107 +47,93 @@ __device__ __forceinline__ void tile_coords(int bid, int T, int& ti, int& tj) {
   tj = row + rem;
 }
 
+__device__ __forceinline__ float4 load_seg(const float* row, int64_t c, int64_t d) {
+  if (c + 3 < d) return *reinterpret_cast<const float4*>(row + c);
+  float t[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int e = 0; e < 4; ++e)
+    if (c + e < d) t[e] = row[c + e];
+  return make_float4(t[0], t[1], t[2], t[3]);
+}
+
 __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a) {
   const int T = static_cast<int>((a.d + kTile - 1) / kTile);
+  const int nb = gridDim.x;
+  int bid = blockIdx.x;
+  if (nb % 8 == 0) bid = (bid % 8) * (nb / 8) + bid / 8;
   int ti, tj;
-  tile_coords(blockIdx.x, T, ti, tj);
+  tile_coords(bid, T, ti, tj);
   const int64_t I0 = static_cast<int64_t>(ti) * kTile, J0 = static_cast<int64_t>(tj) * kTile;
   const bool diag = ti == tj;
 
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  float* sI = smem;                         // [2][kBK][kTile]
-  float* sJ = smem + 2 * kBK * kTile;       // [2][kBK][kTile]
+  __shared__ __attribute__((aligned(16))) float smem[4 * kStage];  // 32 KB
+  float* sI = smem;               // [2][kBK][kTile]
+  float* sJ = smem + 2 * kStage;  // [2][kBK][kTile]
+  const float* sJr = diag ? sI : sJ;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int wr = w >> 1, wc = w & 1;
+  const int lr = threadIdx.x >> 4;         // 0..15: staged rows lr, lr + 16
+  const int lc = (threadIdx.x & 15) * 4;   // 0..60
 
-  f32x16 acc[2][2];
+  f32x16 acc;
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[m][n][r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
   float colsum = 0.f;
 
-  // each thread stages 8 floats per operand per stage: rows (tid / 32) and (tid / 32 + 8),
-  // columns 4 * (tid % 32) .. +3
-  const int lr = threadIdx.x >> 5;          // 0..7
-  const int lc = (threadIdx.x & 31) * 4;    // 0..124
-  auto stage = [&](int buf, int64_t b0) {
+  float4 pI[2], pJ[2];
+  auto fetch = [&](int64_t b0) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int r = lr + 8 * h;
-      const int64_t b = b0 + r;
-      float4 vi = make_float4(0.f, 0.f, 0.f, 0.f), vj = vi;
+      const int64_t b = b0 + lr + 16 * h;
+      pI[h] = pJ[h] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (b < a.n) {
         const float* row = a.act + b * a.row_stride;
-        if (I0 + lc + 3 < a.d) {
-          vi = *reinterpret_cast<const float4*>(row + I0 + lc);
-        } else {
-          float t4[4] = {0.f, 0.f, 0.f, 0.f};
-          for (int e = 0; e < 4; ++e)
-            if (I0 + lc + e < a.d) t4[e] = row[I0 + lc + e];
-          vi = make_float4(t4[0], t4[1], t4[2], t4[3]);
-        }
-        if (!diag) {
-          if (J0 + lc + 3 < a.d) {
-            vj = *reinterpret_cast<const float4*>(row + J0 + lc);
-          } else {
-            float t4[4] = {0.f, 0.f, 0.f, 0.f};
-            for (int e = 0; e < 4; ++e)
-              if (J0 + lc + e < a.d) t4[e] = row[J0 + lc + e];
-            vj = make_float4(t4[0], t4[1], t4[2], t4[3]);
-          }
-        }
+        pI[h] = load_seg(row, I0 + lc, a.d);
+        if (!diag) pJ[h] = load_seg(row, J0 + lc, a.d);
       }
-      *reinterpret_cast<float4*>(sI + (buf * kBK + r) * kTile + lc) = vi;
-      if (!diag) *reinterpret_cast<float4*>(sJ + (buf * kBK + r) * kTile + lc) = vj;
+    }
+  };
+  auto commit = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      *reinterpret_cast<float4*>(sI + buf * kStage + (lr + 16 * h) * kTile + lc) = pI[h];
+      if (!diag) *reinterpret_cast<float4*>(sJ + buf * kStage + (lr + 16 * h) * kTile + lc) = pJ[h];
     }
   };
 
-  const float* sJbase = diag ? sI : sJ;
-  int buf = 0;
-  stage(0, 0);
+  fetch(0);
+  commit(0);
   __syncthreads();
+  int buf = 0;
   for (int64_t b0 = 0; b0 < a.n; b0 += kBK) {
-    if (b0 + kBK < a.n) stage(buf ^ 1, b0 + kBK);  // prefetch next stage into the other buffer
-    const float* cI = sI + buf * kBK * kTile;
-    const float* cJ = sJbase + buf * kBK * kTile;
+    const bool more = b0 + kBK < a.n;
+    if (more) fetch(b0 + kBK);  // in flight during this stage's MFMAs
+    const float* cI = sI + buf * kStage;
+    const float* cJ = sJr + buf * kStage;
+#pragma unroll
+    for (int kk = 0; kk < kBK; kk += 2) {
+      const int k = kk + (lane >> 5);
+      const float av = cI[k * kTile + wr * 32 + (lane & 31)];
+      const float bv = cJ[k * kTile + wc * 32 + (lane & 31)];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    }
     if (diag && threadIdx.x < kTile) {
 #pragma unroll
       for (int k = 0; k < kBK; ++k) colsum += cI[k * kTile + threadIdx.x];
     }
-#pragma unroll
-    for (int kk = 0; kk < kBK; kk += 2) {
-      const int k = kk + (lane >> 5);
-      float av[2], bv[2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) av[m] = cI[k * kTile + wr * 64 + m * 32 + (lane & 31)];
-#pragma unroll
-      for (int n = 0; n < 2; ++n) bv[n] = cJ[k * kTile + wc * 64 + n * 32 + (lane & 31)];
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m], bv[n], acc[m][n], 0, 0, 0);
-    }
+    if (more) commit(buf ^ 1);
     __syncthreads();
     buf ^= 1;
   }
 
-  // epilogue: stage the tile in LDS (reuses the operand buffers: 128 x 129 floats = 66 KB)
+  // epilogue: tile -> LDS (64 x 65 floats, reusing the operand buffers) -> coalesced RMW
   float* sC = smem;
 #pragma unroll
-  for (int m = 0; m < 2; ++m)
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wr * 64 + m * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        const int col = wc * 64 + n * 32 + (lane & 31);
-        sC[row * kPad + col] = acc[m][n][r];
-      }
+  for (int r = 0; r < 16; ++r) {
+    const int row = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+    const int col = wc * 32 + (lane & 31);
+    sC[row * kPad + col] = acc[r];
+  }
   __syncthreads();
   for (int e = threadIdx.x; e < kTile * kTile; e += kThreads) {
     const int row = e / kTile, col = e % kTile;
@@ -161,16 +155,7 @@ int launch_fid_cov(const FidCovArgs& a, hipStream_t stream) {
   if (a.n <= 0 || a.d <= 0) return 0;
   const int T = static_cast<int>((a.d + kTile - 1) / kTile);
   const int blocks = T * (T + 1) / 2;
-  const size_t smem_ops = 4 * kBK * kTile * sizeof(float);
-  const size_t smem_c = static_cast<size_t>(kTile) * kPad * sizeof(float);
-  const size_t smem = smem_ops > smem_c ? smem_ops : smem_c;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(fid_syrk_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, static_cast<int>(smem));
-    attr_set = true;
-  }
-  hipLaunchKernelGGL(fid_syrk_kernel, dim3(blocks), dim3(kThreads), smem, stream, a);
+  hipLaunchKernelGGL(fid_syrk_kernel, dim3(blocks), dim3(kThreads), 0, stream, a);
   return static_cast<int>(hipGetLastError());
 }
 

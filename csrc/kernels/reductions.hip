@@ -19,65 +19,169 @@ namespace {
 
 constexpr int kB = 256;
 
-__global__ __launch_bounds__(kB) void column_moments_kernel(MomentsArgs a) {
-  const int D = static_cast<int>(a.d);
-  const int Dt = D < kB ? D : kB;           // columns per block pass
-  const int rows_per_pass = kB / Dt;        // rows handled together
-  const int my_col_in_tile = threadIdx.x % Dt;
-  const int my_row_off = threadIdx.x / Dt;
-  const bool active = my_row_off < rows_per_pass;
-  __shared__ double lds[5][kB];
-  __shared__ double s_w[kB];
-  for (int c0 = 0; c0 < D; c0 += Dt) {
-    const int j = c0 + my_col_in_tile;
-    double sse = 0, st = 0, stt = 0, sx = 0, sw = 0;
-    if (active && j < D) {
-      for (int64_t i = static_cast<int64_t>(blockIdx.x) * rows_per_pass + my_row_off; i < a.n;
-           i += static_cast<int64_t>(gridDim.x) * rows_per_pass) {
-        const double x = a.x ? load_as_f64(a.x, a.x_dt, i * a.x_row_stride + j * a.x_col_stride) : 0.0;
-        const double t = a.t ? load_as_f64(a.t, a.t_dt, i * a.t_row_stride + j * a.t_col_stride) : 0.0;
-        const double w = a.w ? load_as_f64(a.w, a.w_dt, i * a.w_stride) : 1.0;
-        const double r = t - x;
-        sse += w * r * r;
-        st += w * t;
-        stt += w * t * t;
-        sx += w * x;
-        sw += w;
-      }
-    }
-    lds[0][threadIdx.x] = sse;
-    lds[1][threadIdx.x] = st;
-    lds[2][threadIdx.x] = stt;
-    lds[3][threadIdx.x] = sx;
-    s_w[threadIdx.x] = (j == c0) ? sw : 0.0;  // count weights once (column c0 threads)
-    __syncthreads();
-    if (threadIdx.x < Dt && c0 + threadIdx.x < D) {
-      double acc[4] = {0, 0, 0, 0};
-      for (int r = 0; r < rows_per_pass; ++r) {
-        const int src = r * Dt + threadIdx.x;
+// ---------------------------------------------------------------- K5 column moments
+// Two deterministic passes, no atomics:
+//   A) grid (P row-chunks) x (column tiles of 64 column groups).  A thread owns V consecutive
+//      columns (V = 4 with 16-B loads for contiguous f32 inputs, else 1) and walks its chunk's
+//      rows with a U-row unroll so 2 x U independent loads are in flight; FP64 accumulators.
+//      The block folds its row lanes through LDS and writes only the requested statistics to
+//      ws[chunk][slot][col] (compact slots: MSE writes 1 stat, R2 3).
+//   B) 16 columns x 16 partial groups per block sum the P partials and add the FP64 total to
+//      the float32 output once (single writer per column: deterministic, no same-address
+//      atomics - v1 issued P x d float atomics, 256-way contended per column).
+constexpr int kStats = 4;  // sse, st, stt, sx
+constexpr int kColGroups = 64;
+
+struct Slots {
+  int s[kStats];
+  int n;
+};
+
+__device__ __forceinline__ Slots slots_of(const MomentsArgs& a) {
+  Slots r;
+  const float* outs[kStats] = {a.sse, a.st, a.stt, a.sx};
+  r.n = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) acc[k] += lds[k][src];
+  for (int k = 0; k < kStats; ++k) r.s[k] = outs[k] ? r.n++ : -1;
+  return r;
+}
+
+template <int V>
+__device__ __forceinline__ void load_v(const void* p, DType dt, int64_t off, int64_t cstride, float (&v)[V]) {
+  if constexpr (V == 4) {
+    const float4 q = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + off);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e) v[e] = static_cast<float>(load_as_f64(p, dt, off + e * cstride));
+  }
+}
+
+template <int V>
+__global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
+  constexpr int U = 4;
+  const int64_t d = a.d;
+  const int64_t dv = (d + V - 1) / V;
+  const int64_t c0 = static_cast<int64_t>(blockIdx.y) * kColGroups;
+  const int CG = static_cast<int>(dv - c0 < kColGroups ? dv - c0 : kColGroups);
+  const int RPP = kB / CG;
+  const int cg = threadIdx.x % CG;
+  const int rl = threadIdx.x / CG;
+  const bool active = rl < RPP;
+  const int64_t chunk = (a.n + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * chunk;
+  const int64_t r1 = r0 + chunk < a.n ? r0 + chunk : a.n;
+  const bool want_x = a.sse || a.sx, want_t = a.sse || a.st || a.stt;
+  const Slots sl = slots_of(a);
+  const int64_t stride = sl.n * d + 1;
+  __shared__ double lds[kStats * V][kB];
+  __shared__ double lds_w[kB];
+  double* ws = a.ws + static_cast<int64_t>(blockIdx.x) * stride;
+
+  double acc[kStats][V];
+#pragma unroll
+  for (int k = 0; k < kStats; ++k)
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[k][e] = 0.0;
+  double wsum = 0.0;
+  const int64_t col = (c0 + cg) * V;
+  const int nv = static_cast<int>(d - col < V ? d - col : V);
+  if (active) {
+    for (int64_t i = r0 + rl; i < r1; i += static_cast<int64_t>(RPP) * U) {
+      float xv[U][V], tv[U][V], wv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t row = i + static_cast<int64_t>(u) * RPP;
+        const bool ok = row < r1;
+#pragma unroll
+        for (int e = 0; e < V; ++e) xv[u][e] = tv[u][e] = 0.f;
+        wv[u] = ok ? (a.w ? static_cast<float>(load_as_f64(a.w, a.w_dt, row * a.w_stride)) : 1.f) : 0.f;
+        if (ok && V == 4 && nv == 4) {
+          if (want_x) load_v<V>(a.x, a.x_dt, row * a.x_row_stride + col, 1, xv[u]);
+          if (want_t) load_v<V>(a.t, a.t_dt, row * a.t_row_stride + col, 1, tv[u]);
+        } else if (ok) {
+          for (int e = 0; e < nv; ++e) {
+            if (want_x) xv[u][e] = static_cast<float>(load_as_f64(a.x, a.x_dt, row * a.x_row_stride + (col + e) * a.x_col_stride));
+            if (want_t) tv[u][e] = static_cast<float>(load_as_f64(a.t, a.t_dt, row * a.t_row_stride + (col + e) * a.t_col_stride));
+          }
+        }
       }
-      const int jj = c0 + threadIdx.x;
-      if (a.sse && acc[0] != 0.0) atomicAdd(a.sse + jj * a.out_stride, static_cast<float>(acc[0]));
-      if (a.st && acc[1] != 0.0) atomicAdd(a.st + jj * a.out_stride, static_cast<float>(acc[1]));
-      if (a.stt && acc[2] != 0.0) atomicAdd(a.stt + jj * a.out_stride, static_cast<float>(acc[2]));
-      if (a.sx && acc[3] != 0.0) atomicAdd(a.sx + jj * a.out_stride, static_cast<float>(acc[3]));
-    }
-    if (c0 == 0 && a.sw) {
-      // reduce the weight sum over the whole block
-      double v = s_w[threadIdx.x];
-      v = wave_sum(v);
-      __shared__ double s_ws[kB / 64];
-      if (lane_id() == 0) s_ws[threadIdx.x >> 6] = v;
-      __syncthreads();
-      if (threadIdx.x == 0) {
-        double tot = 0;
-        for (int k = 0; k < kB / 64; ++k) tot += s_ws[k];
-        if (tot != 0.0) atomicAdd(a.sw, static_cast<float>(tot));
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const double w = wv[u];
+        wsum += w;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          const double x = xv[u][e], t = tv[u][e], r = t - x;
+          acc[0][e] += w * r * r;
+          acc[1][e] += w * t;
+          acc[2][e] += w * t * t;
+          acc[3][e] += w * x;
+        }
       }
     }
-    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < kStats; ++k)
+#pragma unroll
+    for (int e = 0; e < V; ++e) lds[k * V + e][threadIdx.x] = acc[k][e];
+  lds_w[threadIdx.x] = (cg == 0 && active) ? wsum : 0.0;  // one column group counts weights
+  __syncthreads();
+  if (threadIdx.x < CG) {
+#pragma unroll
+    for (int k = 0; k < kStats; ++k) {
+      if (sl.s[k] < 0) continue;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        double s = 0.0;
+        for (int r = 0; r < RPP; ++r) s += lds[k * V + e][r * CG + threadIdx.x];
+        const int64_t cc = (c0 + threadIdx.x) * V + e;
+        if (cc < d) ws[sl.s[k] * d + cc] = s;
+      }
+    }
+  }
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
+    double s = 0.0;
+    for (int r = 0; r < kB; ++r) s += lds_w[r];
+    ws[sl.n * d] = s;
+  }
+}
+
+__global__ __launch_bounds__(kB) void moments_finalize_kernel(MomentsArgs a, int P) {
+  constexpr int G = 16, C = kB / G;  // partial groups x columns per block
+  const int64_t d = a.d;
+  const int c = threadIdx.x % C, grp = threadIdx.x / C;
+  const int64_t col = static_cast<int64_t>(blockIdx.x) * C + c;
+  const Slots sl = slots_of(a);
+  const int64_t stride = sl.n * d + 1;
+  __shared__ double lds[G][kStats + 1][C];
+  double s[kStats + 1] = {0, 0, 0, 0, 0};
+  for (int p = grp; p < P; p += G) {
+    const double* ws = a.ws + p * stride;
+    if (col < d) {
+#pragma unroll
+      for (int k = 0; k < kStats; ++k)
+        if (sl.s[k] >= 0) s[k] += ws[sl.s[k] * d + col];
+    }
+    if (blockIdx.x == 0 && c == 0) s[kStats] += ws[sl.n * d];
+  }
+#pragma unroll
+  for (int k = 0; k <= kStats; ++k) lds[grp][k][c] = s[k];
+  __syncthreads();
+  if (grp == 0) {
+    double t[kStats + 1];
+#pragma unroll
+    for (int k = 0; k <= kStats; ++k) {
+      t[k] = 0.0;
+      for (int g = 0; g < G; ++g) t[k] += lds[g][k][c];
+    }
+    if (col < d) {
+      float* outs[kStats] = {a.sse, a.st, a.stt, a.sx};
+#pragma unroll
+      for (int k = 0; k < kStats; ++k)
+        if (outs[k]) outs[k][col * a.out_stride] += static_cast<float>(t[k]);
+    }
+    if (blockIdx.x == 0 && c == 0 && a.sw) *a.sw += static_cast<float>(t[kStats]);
   }
 }
 
@@ -127,15 +231,32 @@ __global__ __launch_bounds__(kB) void ne_sums_kernel(NeArgs a) {
 
 }  // namespace
 
+int column_moments_blocks(int64_t n, int64_t d) {
+  // row chunks: ~32 rows each (>= 8 per row lane with the U = 4 unroll), at most 256 partials
+  // per column so the finalize pass stays one latency round per thread
+  int64_t p = (n + 31) / 32;
+  if (d < 16) p = (n * d + 2047) / 2048;
+  if (p > 256) p = 256;
+  if (p < 1) p = 1;
+  return static_cast<int>(p);
+}
+
 int launch_column_moments(const MomentsArgs& a, hipStream_t stream) {
   if (a.n <= 0 || a.d <= 0) return 0;
-  const int Dt = a.d < kB ? static_cast<int>(a.d) : kB;
-  const int rows_per_pass = kB / Dt;
-  int64_t blocks = (a.n + rows_per_pass * 16 - 1) / (rows_per_pass * 16);
-  const int64_t cap = a.d == 1 ? 64 : 256;
-  if (blocks > cap) blocks = cap;
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(column_moments_kernel, dim3(static_cast<unsigned>(blocks)), dim3(kB), 0, stream, a);
+  const int P = a.ws_blocks;
+  const bool vec = (a.x == nullptr || (a.x_dt == DType::f32 && a.x_col_stride == 1 && a.x_row_stride % 4 == 0 &&
+                                       reinterpret_cast<uintptr_t>(a.x) % 16 == 0)) &&
+                   (a.t == nullptr || (a.t_dt == DType::f32 && a.t_col_stride == 1 && a.t_row_stride % 4 == 0 &&
+                                       reinterpret_cast<uintptr_t>(a.t) % 16 == 0)) &&
+                   a.d % 4 == 0;
+  const int V = vec ? 4 : 1;
+  const unsigned ct = static_cast<unsigned>(((a.d + V - 1) / V + kColGroups - 1) / kColGroups);
+  if (vec)
+    hipLaunchKernelGGL(moments_partial_kernel<4>, dim3(P, ct), dim3(kB), 0, stream, a);
+  else
+    hipLaunchKernelGGL(moments_partial_kernel<1>, dim3(P, ct), dim3(kB), 0, stream, a);
+  const unsigned fb = static_cast<unsigned>((a.d + 15) / 16);
+  hipLaunchKernelGGL(moments_finalize_kernel, dim3(fb), dim3(kB), 0, stream, a, P);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -48,3 +48,61 @@ def test_binary_gpu():
 def test_ws1_sync_returns_same_object():
     m = MulticlassAccuracy(device=torch.device("cuda"))
     assert get_synced_metric(m) is m
+
+
+# ----------------------------------------------------------------------------- K2 multilabel
+_CRIT = ["exact_match", "hamming", "overlap", "contain", "belong"]
+
+
+@pytest.mark.parametrize("criteria", _CRIT)
+@pytest.mark.parametrize("shape", [(1, 1), (37, 5), (8192, 1000), (300, 1001)])
+@pytest.mark.parametrize("tdtype", [torch.int64, torch.float32, torch.bool, torch.uint8, torch.int32])
+def test_k2_multilabel_threshold(criteria, shape, tdtype):
+    from torcheval_amd.metrics.functional import multilabel_accuracy
+
+    g = torch.Generator().manual_seed(shape[0] * 31 + shape[1])
+    x = torch.rand(shape, generator=g)
+    x[0, 0] = float("nan")  # NaN >= threshold in the reference (where(x < thr, 0, 1))
+    # sparse targets so overlap / contain / belong rows are a mix of true and false
+    t = (torch.rand(shape, generator=g) < 0.3).to(tdtype)
+    ref = multilabel_accuracy(x, t, criteria=criteria)
+    got = multilabel_accuracy(x.cuda(), t.cuda(), criteria=criteria)
+    torch.testing.assert_close(got.cpu(), ref, rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("criteria", _CRIT)
+@pytest.mark.parametrize("k", [1, 2, 5])
+@pytest.mark.parametrize("c", [3, 64, 65, 1000, 2048])
+def test_k2_topk_multilabel(criteria, k, c):
+    from torcheval_amd.metrics.functional import topk_multilabel_accuracy
+
+    if k > c:
+        pytest.skip("k > c")
+    g = torch.Generator().manual_seed(c * 7 + k)
+    x = torch.rand(257, c, generator=g)
+    t = (torch.rand(257, c, generator=g) < 0.05).long()
+    # plant exact matches so exact / contain rows exist
+    top = x[:50].topk(k, dim=-1).indices
+    t[:50] = 0
+    t[:50].scatter_(1, top, 1)
+    ref = topk_multilabel_accuracy(x, t, criteria=criteria, k=k)
+    got = topk_multilabel_accuracy(x.cuda(), t.cuda(), criteria=criteria, k=k)
+    torch.testing.assert_close(got.cpu(), ref, rtol=0, atol=1e-6)
+
+
+def test_k2_class_states_and_bf16():
+    from torcheval_amd.metrics import MultilabelAccuracy, TopKMultilabelAccuracy
+    from torcheval_amd.metrics.functional import multilabel_accuracy, topk_multilabel_accuracy
+
+    g = torch.Generator().manual_seed(0)
+    xs = [torch.rand(512, 100, generator=g) for _ in range(4)]
+    ts = [(torch.rand(512, 100, generator=g) < 0.5).long() for _ in range(4)]
+    for crit in _CRIT:
+        m = MultilabelAccuracy(criteria=crit, device="cuda")
+        mk = TopKMultilabelAccuracy(criteria=crit, k=3, device="cuda")
+        for x, t in zip(xs, ts):
+            m.update(x.cuda().bfloat16(), t.cuda())
+            mk.update(x.cuda(), t.cuda())
+        X, T = torch.cat(xs), torch.cat(ts)
+        torch.testing.assert_close(m.compute().cpu(), multilabel_accuracy(X.bfloat16().float(), T, criteria=crit))
+        torch.testing.assert_close(mk.compute().cpu(), topk_multilabel_accuracy(X, T, criteria=crit, k=3))

@@ -23,12 +23,20 @@ from torcheval_amd.metrics.functional.classification.accuracy import (
     _multiclass_accuracy_update_aten,
     _multilabel_accuracy_param_check,
     _multilabel_accuracy_update,
+    _multilabel_accuracy_update_input_check,
     _topk_multilabel_accuracy_param_check,
     _topk_multilabel_accuracy_update,
+    _topk_multilabel_accuracy_update_input_check,
 )
 from torcheval_amd.metrics.metric import Metric
 from torcheval_amd.ops import use_native
-from torcheval_amd.ops.classification import binary_counts, cls_counts, cls_counts_supported
+from torcheval_amd.ops.classification import (
+    binary_counts,
+    cls_counts,
+    cls_counts_supported,
+    multilabel_counts,
+    native_multilabel,
+)
 
 TAccuracy = TypeVar("TAccuracy")
 TBinaryAccuracy = TypeVar("TBinaryAccuracy")
@@ -177,6 +185,16 @@ class BinaryAccuracy(MulticlassAccuracy):
         return self
 
 
+def _k2_state_ok(metric: Metric, input: torch.Tensor, target: torch.Tensor, k: int) -> bool:
+    return (
+        native_multilabel(input, target, k)
+        and metric.num_correct.dtype == torch.float32
+        and metric.num_total.dtype == torch.float32
+        and metric.num_correct.numel() == 1
+        and metric.num_total.numel() == 1
+    )
+
+
 class MultilabelAccuracy(MulticlassAccuracy):
     """
     Multilabel accuracy; ``criteria`` in ``exact_match`` (default) | ``hamming`` |
@@ -203,6 +221,13 @@ class MultilabelAccuracy(MulticlassAccuracy):
         """Update states with ``[N, L]`` scores/labels and ``[N, L]`` ground truth."""
         input = input.to(self.device)
         target = target.to(self.device)
+        if _k2_state_ok(self, input, target, 0):
+            _multilabel_accuracy_update_input_check(input, target)
+            multilabel_counts(
+                input, target, threshold=self.threshold, k=0, criteria=self.criteria,
+                num_correct=self.num_correct, num_total=self.num_total,
+            )
+            return self
         num_correct, num_total = _multilabel_accuracy_update(
             input, target, self.threshold, self.criteria
         )
@@ -237,6 +262,13 @@ class TopKMultilabelAccuracy(MulticlassAccuracy):
         """Update states with ``[N, L]`` scores and ``[N, L]`` ground truth."""
         input = input.to(self.device)
         target = target.to(self.device)
+        if _k2_state_ok(self, input, target, self.k):
+            _topk_multilabel_accuracy_update_input_check(input, target, self.k)
+            multilabel_counts(
+                input, target, threshold=0.5, k=self.k, criteria=self.criteria,
+                num_correct=self.num_correct, num_total=self.num_total,
+            )
+            return self
         num_correct, num_total = _topk_multilabel_accuracy_update(
             input, target, self.criteria, self.k
         )

@@ -15,7 +15,13 @@ from typing import Optional, Tuple
 import torch
 
 from torcheval_amd.ops import use_native
-from torcheval_amd.ops.classification import binary_counts, cls_counts, cls_counts_supported
+from torcheval_amd.ops.classification import (
+    binary_counts,
+    cls_counts,
+    cls_counts_supported,
+    multilabel_counts,
+    native_multilabel,
+)
 
 
 @torch.inference_mode()
@@ -227,8 +233,21 @@ def _multilabel_accuracy_update(
     criteria: str = "exact_match",
 ) -> Tuple[torch.Tensor, torch.Tensor]:
     _multilabel_accuracy_update_input_check(input, target)
+    if native_multilabel(input, target):
+        return _multilabel_native(input, target, threshold, 0, criteria)
     input_label = torch.where(input < threshold, 0, 1)
     return _multilabel_update(input_label, target, criteria)
+
+
+def _multilabel_native(
+    input: torch.Tensor, target: torch.Tensor, threshold: float, k: int, criteria: str
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    # K2: one pass, counts straight into a device scalar (no [N, L] label matrix)
+    out = torch.zeros(2, dtype=torch.float32, device=input.device)
+    multilabel_counts(
+        input, target, threshold=threshold, k=k, criteria=criteria, num_correct=out[0], num_total=out[1]
+    )
+    return out[0], out[1]
 
 
 def _topk_multilabel_accuracy_update(
@@ -238,6 +257,8 @@ def _topk_multilabel_accuracy_update(
     k: int = 2,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
     _topk_multilabel_accuracy_update_input_check(input, target, k)
+    if native_multilabel(input, target, k):
+        return _multilabel_native(input, target, 0.5, k, criteria)
     topk_idx = input.topk(k=k, dim=-1).indices
     input_label = torch.zeros(input.size(), device=input.device).scatter_(-1, topk_idx, 1.0)
     return _multilabel_update(input_label, target, criteria)

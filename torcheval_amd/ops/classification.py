@@ -119,3 +119,43 @@ def binary_counts(
         input, target, weight, float(threshold), tp, fp, tn, fn, total, int(strict), MAX_BLOCKS,
         tp2, fp2, tn2, fn2,
     )
+
+
+# ----------------------------------------------------------------------------- K2 multilabel
+_ML_SCORE = (torch.float32, torch.bfloat16, torch.float16)
+_ML_TARGET = (torch.float32, torch.int64, torch.int32, torch.uint8, torch.bool)
+ML_CRITERIA = {"exact_match": 0, "hamming": 1, "overlap": 2, "contain": 3, "belong": 4}
+ML_MAX_TOPK_COLS = 2048
+
+
+def native_multilabel(input: torch.Tensor, target: torch.Tensor, k: int = 0) -> bool:
+    """True when (input, target) can go through K2 (``k > 0``: top-k mode)."""
+    return (
+        use_native(input)
+        and target.is_cuda
+        and input.dim() == 2
+        and input.shape == target.shape
+        and input.dtype in _ML_SCORE
+        and target.dtype in _ML_TARGET
+        and input.stride(1) == 1
+        and target.stride(1) == 1
+        and (k == 0 or input.shape[1] <= ML_MAX_TOPK_COLS)
+        and input.numel() < 2**31
+    )
+
+
+def multilabel_counts(
+    input: torch.Tensor,
+    target: torch.Tensor,
+    *,
+    threshold: float,
+    k: int,
+    criteria: str,
+    num_correct: torch.Tensor,
+    num_total: "torch.Tensor | None" = None,
+) -> None:
+    """K2: add the update's correct count (and total) into float32 scalar states."""
+    total = float(target.numel() if criteria == "hamming" else target.shape[0])
+    native().multilabel_counts(
+        input, target, float(threshold), int(k), ML_CRITERIA[criteria], num_correct, num_total, total
+    )
