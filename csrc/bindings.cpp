@@ -74,6 +74,24 @@ unsigned long long* fold_workspace(const Tensor& like, hipStream_t stream) {
   return reinterpret_cast<unsigned long long*>(it->second.data_ptr<int64_t>());
 }
 
+// Self-cleaning scratch: zeroed once per (device, stream, slot), grown on demand; kernels that
+// use it leave it zeroed again, so no memset launch per call.
+void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, Tensor> cache;
+  const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
+                       (static_cast<uint64_t>(slot) << 48) ^ reinterpret_cast<uint64_t>(stream);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it == cache.end() || it->second.numel() < bytes) {
+    Tensor ws = at::zeros({std::max<int64_t>(bytes, 1 << 16)},
+                          at::TensorOptions().dtype(at::kByte).device(like.device()));
+    if (it == cache.end()) it = cache.emplace(key, ws).first;
+    else it->second = ws;
+  }
+  return it->second.data_ptr();
+}
+
 void check_launch(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "torcheval_amd._C: ", what, " launch failed (code ", rc, ")");
 }
@@ -195,14 +213,16 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
   TORCH_CHECK(sorted.stride(1) == 1 && order.stride(1) == 1, "auc_scan: rows must be contiguous");
   TORCH_CHECK(sorted.scalar_type() == at::kFloat || sorted.scalar_type() == at::kDouble,
               "auc_scan: scores must be float32/float64");
-  TORCH_CHECK(order.scalar_type() == at::kLong, "auc_scan: order must be int64");
+  TORCH_CHECK(order.scalar_type() == at::kLong || order.scalar_type() == at::kInt,
+              "auc_scan: order must be int64 or int32");
   c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
   const int64_t rows = sorted.size(0), n = sorted.size(1);
   tea::AucScanArgs a;
   a.sorted = sorted.data_ptr();
   a.key_dt = dt_of(sorted);
   a.key_stride = sorted.stride(0);
-  a.order = order.data_ptr<int64_t>();
+  if (order.scalar_type() == at::kLong) a.order = order.data_ptr<int64_t>();
+  else a.order32 = order.data_ptr<int32_t>();
   a.order_stride = order.stride(0);
   Tensor tg = target;
   if (class_mode) {
@@ -291,9 +311,8 @@ void binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr,
   a.fn = out(fn, "fn");
   a.out_k_stride = ks;
   a.out_c_stride = cs;
-  Tensor hist = at::zeros({(a.T + 1) * a.c * 2},
-                          at::TensorOptions().dtype(at::kFloat).device(input.device()));
-  a.hist = hist.data_ptr<float>();
+  a.ws = reinterpret_cast<unsigned*>(
+      zeroed_workspace(input, stream_for(input), tea::binned_workspace_words(a.T, a.c) * 4, 1));
   const int rc = tea::launch_binned(a, stream_for(input));
   TORCH_CHECK(rc != -1, "binned_counts: too many thresholds (", a.T, ") for the LDS histogram");
   check_launch(rc, "binned_counts");
@@ -496,6 +515,50 @@ void multilabel_counts(const Tensor& input, const Tensor& target, double thresho
   check_launch(rc, "multilabel_counts");
 }
 
+
+// [n, c] (unit column stride) -> contiguous [c, n]
+void transpose_f32(const Tensor& x, const Tensor& out) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kFloat && x.stride(1) == 1, "transpose_f32: x [n, c] f32");
+  TORCH_CHECK(out.is_contiguous() && out.scalar_type() == at::kFloat && out.size(0) == x.size(1) &&
+                  out.size(1) == x.size(0), "transpose_f32: out must be contiguous [c, n]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  check_launch(tea::launch_transpose_f32(x.data_ptr<float>(), x.size(0), x.size(1), x.stride(0),
+                                         out.data_ptr<float>(), stream_for(x)), "transpose_f32");
+}
+
+// K3a: segmented descending radix sort of f32 rows -> (sorted scores, int32 permutation)
+void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_order) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kFloat && x.stride(1) == 1,
+              "sort_desc: x must be float32 [rows, n] with contiguous rows");
+  TORCH_CHECK(out_sorted.scalar_type() == at::kFloat && out_sorted.is_contiguous() &&
+                  out_sorted.sizes() == x.sizes(), "sort_desc: out_sorted must be contiguous f32 [rows, n]");
+  TORCH_CHECK(out_order.scalar_type() == at::kInt && out_order.is_contiguous() &&
+                  out_order.sizes() == x.sizes(), "sort_desc: out_order must be contiguous int32 [rows, n]");
+  TORCH_CHECK(x.size(1) < (int64_t{1} << 31), "sort_desc: rows longer than 2^31");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  tea::RadixArgs a;
+  a.in = x.data_ptr<float>();
+  a.in_row_stride = x.stride(0);
+  a.rows = x.size(0);
+  a.n = x.size(1);
+  if (a.rows == 0 || a.n == 0) return;
+  a.tiles = tea::radix_sort_tiles(a.n);
+  const int64_t m = a.rows * a.n;
+  Tensor ws = at::empty({4 * m + a.rows * 256 * a.tiles + a.rows * 256}, x.options().dtype(at::kInt));
+  uint32_t* base = reinterpret_cast<uint32_t*>(ws.data_ptr<int32_t>());
+  a.keys0 = base;
+  a.vals0 = base + m;
+  a.keys1 = base + 2 * m;
+  a.vals1 = base + 3 * m;
+  a.hist = base + 4 * m;
+  a.dtotal = a.hist + a.rows * 256 * a.tiles;
+  a.out_sorted = out_sorted.data_ptr<float>();
+  a.out_order = out_order.data_ptr<int32_t>();
+  check_launch(tea::launch_radix_sort_desc(a, stream_for(x)), "sort_desc");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -528,6 +591,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multilabel_counts", &multilabel_counts, "K2 multilabel accuracy counts", py::arg("input"),
         py::arg("target"), py::arg("threshold"), py::arg("k"), py::arg("criteria"),
         py::arg("num_correct"), py::arg("num_total") = py::none(), py::arg("total") = 0.0);
+  m.def("transpose_f32", &transpose_f32, "LDS-tiled [n, c] -> [c, n] float32 transpose", py::arg("x"),
+        py::arg("out"));
+  m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
+        py::arg("x"), py::arg("out_sorted"), py::arg("out_order"));
   m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
         py::arg("act"), py::arg("cov"), py::arg("colsum"));
   tea_register_runtime(m);

@@ -82,6 +82,11 @@ __device__ __forceinline__ int wave_sum(int v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
   return v;
 }
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));

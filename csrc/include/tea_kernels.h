@@ -63,7 +63,8 @@ struct AucScanArgs {
   const void* sorted = nullptr;  // [rows, n] scores sorted descending (f32 or f64)
   DType key_dt = DType::f32;
   int64_t key_stride = 0;
-  const int64_t* order = nullptr;  // [rows, n] sort permutation
+  const int64_t* order = nullptr;  // [rows, n] sort permutation (int64, torch.sort) ...
+  const int32_t* order32 = nullptr;  // ... or int32 (K3a radix sort); exactly one is set
   int64_t order_stride = 0;
   const void* target = nullptr;  // binary: [rows, n] (row stride) / class mode: [n] labels
   DType tg_dt = DType::f32;
@@ -105,13 +106,14 @@ struct BinnedArgs {
   int64_t tg_col_stride = 0;
   const float* thr = nullptr;  // [T] sorted ascending
   int T = 0;
-  float* hist = nullptr;       // scratch [(T + 1), c, 2], zeroed by the caller
+  unsigned* ws = nullptr;      // [16 replicas, T + 1, c, 2] u32, zero on entry, left zeroed
   float* tp = nullptr;         // outputs (accumulated): index k * out_k_stride + j * out_c_stride
   float* fp = nullptr;
   float* fn = nullptr;
   int64_t out_k_stride = 0;
   int64_t out_c_stride = 0;
 };
+int64_t binned_workspace_words(int T, int64_t c);
 int launch_binned(const BinnedArgs& a, hipStream_t stream);
 
 }  // namespace tea
@@ -214,4 +216,25 @@ struct MultilabelArgs {
 };
 int multilabel_max_topk_cols();
 int launch_multilabel(const MultilabelArgs& a, hipStream_t stream);
+}  // namespace tea
+
+// ------------------------------------------------------------------ K3a radix sort
+namespace tea {
+struct RadixArgs {
+  const float* in = nullptr;  // [rows, n] scores, rows at in_row_stride (unit column stride)
+  int64_t in_row_stride = 0;
+  int64_t rows = 0, n = 0;
+  int64_t tiles = 0;          // radix_sort_tiles(n)
+  uint32_t* keys0 = nullptr;  // ping-pong [rows * n]
+  uint32_t* vals0 = nullptr;
+  uint32_t* keys1 = nullptr;
+  uint32_t* vals1 = nullptr;
+  uint32_t* hist = nullptr;   // [rows, tiles, 256]
+  uint32_t* dtotal = nullptr; // [rows, 256]
+  float* out_sorted = nullptr;  // [rows, n] descending
+  int32_t* out_order = nullptr; // [rows, n] source index within the row
+};
+int64_t radix_sort_tiles(int64_t n);
+int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream);
+int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream);
 }  // namespace tea

@@ -75,9 +75,11 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a) {
   const int lr = threadIdx.x >> 4;         // 0..15: staged rows lr, lr + 16
   const int lc = (threadIdx.x & 15) * 4;   // 0..60
 
-  f32x16 acc;
+  // two accumulators on alternating k-steps: consecutive MFMAs are independent, so a wave
+  // does not serialise on its own accumulator (2-3 resident waves per SIMD at D = 2048)
+  f32x16 acc, acc2;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int r = 0; r < 16; ++r) acc[r] = acc2[r] = 0.f;
   float colsum = 0.f;
 
   float4 pI[2], pJ[2];
@@ -111,11 +113,14 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a) {
     const float* cI = sI + buf * kStage;
     const float* cJ = sJr + buf * kStage;
 #pragma unroll
-    for (int kk = 0; kk < kBK; kk += 2) {
+    for (int kk = 0; kk < kBK; kk += 4) {
       const int k = kk + (lane >> 5);
       const float av = cI[k * kTile + wr * 32 + (lane & 31)];
       const float bv = cJ[k * kTile + wc * 32 + (lane & 31)];
+      const float av2 = cI[(k + 2) * kTile + wr * 32 + (lane & 31)];
+      const float bv2 = cJ[(k + 2) * kTile + wc * 32 + (lane & 31)];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+      acc2 = __builtin_amdgcn_mfma_f32_32x32x2f32(av2, bv2, acc2, 0, 0, 0);
     }
     if (diag && threadIdx.x < kTile) {
 #pragma unroll
@@ -132,7 +137,7 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a) {
   for (int r = 0; r < 16; ++r) {
     const int row = wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
     const int col = wc * 32 + (lane & 31);
-    sC[row * kPad + col] = acc[r];
+    sC[row * kPad + col] = acc[r] + acc2[r];
   }
   __syncthreads();
   for (int e = threadIdx.x; e < kTile * kTile; e += kThreads) {

@@ -1,0 +1,304 @@
+// K3a: segmented descending LSD radix sort of f32 scores with an int32 permutation payload
+// (SURVEY.md §7.3 K3 "segmented descending radix sort").
+//
+// Replaces torch.sort(descending=True) in the AUROC / AUPRC pipelines: on MI355X that call
+// costs ~230 us for 1M scores (rocPRIM onesweep + a post-processing pass + an index iota /
+// gather pass), i.e. most of binary_auroc's time.  Here:
+//   * keys are mapped to order-preserving u32 (sign flip, NaN canonicalised to +NaN so it
+//     sorts first like torch, -0 folded into +0) and complemented so an ascending LSD sort
+//     yields descending scores; the permutation payload is generated in the first pass (no
+//     iota kernel) and the last pass writes the scores back as floats;
+//   * 4 passes x 8 bits; each pass = upsweep (per-tile digit histogram, tile-major rows of
+//     1 KB) -> digit-parallel scan (grid = 256 digits x rows; each block scans one digit's
+//     counts across the row's tiles with one independent load per thread and emits the digit
+//     total) -> downsweep (each block re-scans the 256 digit totals in LDS for its bases, then
+//     a stable scatter).  Tiles are 4096 keys (256 threads x 16 striped rounds, coalesced);
+//     each thread loads all 16 of its keys up front so the loads overlap (v1 loaded per round
+//     and ran a single-block serial scan: ~60 us per pass at 1M).  Stable in-tile ranking uses wave64 "match" masks
+//     built from 8 ballots: each lane's rank among equal digits is popc(peers & lanes_below),
+//     per-wave digit counts are combined in wave order through LDS, so the scatter is stable
+//     (LSD correctness) and contention-free even when every key shares a digit (typical for
+//     probabilities, whose top byte is nearly constant);
+//   * rows are independent segments: histogram/scan/offsets are per row, so a [C, n]
+//     one-vs-rest score matrix is sorted in the same 12 launches.
+#include "tea_common.h"
+#include "tea_kernels.h"
+
+namespace tea {
+
+namespace {
+
+constexpr int kRT = 256;
+constexpr int kRounds = 16;
+constexpr int kRTile = kRT * kRounds;  // 4096
+constexpr int kBins = 256;
+constexpr int kRWaves = kRT / 64;
+
+__device__ __forceinline__ uint32_t f2key_desc(float f) {
+  uint32_t u = __float_as_uint(f);
+  if (f != f) u = 0x7fc00000u;      // canonical +NaN: first in descending order (torch.sort)
+  if (u == 0x80000000u) u = 0u;     // -0 == +0
+  const uint32_t asc = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  return ~asc;
+}
+
+__device__ __forceinline__ float key2f_desc(uint32_t k) {
+  const uint32_t asc = ~k;
+  const uint32_t u = (asc & 0x80000000u) ? (asc & 0x7fffffffu) : ~asc;
+  return __uint_as_float(u);
+}
+
+__device__ __forceinline__ uint32_t load_key(const RadixArgs& a, const uint32_t* keys_in, int pass,
+                                             int64_t row, int64_t i) {
+  if (pass == 0) return f2key_desc(a.in[row * a.in_row_stride + i]);
+  return keys_in[row * a.n + i];
+}
+
+// lanes (among `active`) holding the same 8-bit digit as this lane
+__device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
+  uint64_t peers = active;
+#pragma unroll
+  for (int b = 0; b < 8; ++b) {
+    const uint64_t ones = __ballot((d >> b) & 1u);
+    peers &= ((d >> b) & 1u) ? ones : ~ones;
+  }
+  return peers;
+}
+
+// keys of this thread's 16 striped rounds, loaded up front so the loads overlap
+__device__ __forceinline__ void load_tile(const RadixArgs& a, const uint32_t* keys_in, const uint32_t* vals_in,
+                                          int pass, int64_t row, int tile, uint32_t (&k)[kRounds],
+                                          uint32_t (&v)[kRounds], bool want_vals) {
+  const int64_t t0 = static_cast<int64_t>(tile) * kRTile + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const int64_t i = t0 + j * kRT;
+    k[j] = 0u;
+    v[j] = 0u;
+    if (i < a.n) {
+      k[j] = load_key(a, keys_in, pass, row, i);
+      if (want_vals) v[j] = pass == 0 ? static_cast<uint32_t>(i) : vals_in[row * a.n + i];
+    }
+  }
+}
+
+// hist layout: [row][tile][digit] (each block writes 1 KB contiguously)
+__global__ __launch_bounds__(kRT) void radix_upsweep_kernel(RadixArgs a, const uint32_t* keys_in, int pass) {
+  const int64_t row = blockIdx.y;
+  const int tile = blockIdx.x;
+  const int shift = 8 * pass;
+  __shared__ uint32_t h[kBins];
+  h[threadIdx.x] = 0;
+  uint32_t k[kRounds], v[kRounds];
+  load_tile(a, keys_in, nullptr, pass, row, tile, k, v, false);
+  __syncthreads();
+  const int lane = lane_id();
+  const int64_t t0 = static_cast<int64_t>(tile) * kRTile + threadIdx.x;
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const bool valid = t0 + j * kRT < a.n;
+    const uint64_t active = __ballot(valid);
+    if (active == 0ull) break;
+    const uint32_t d = (k[j] >> shift) & 0xffu;
+    const uint64_t peers = match_digit(d, active);
+    if (valid && (__ffsll(static_cast<long long>(peers)) - 1) == lane)
+      atomicAdd(&h[d], static_cast<uint32_t>(__popcll(peers)));
+  }
+  __syncthreads();
+  a.hist[(row * a.tiles + tile) * kBins + threadIdx.x] = h[threadIdx.x];
+}
+
+// grid (digit, row): exclusive scan of one digit's counts over the row's tiles (in place) and
+// the digit total.  Threads own tiles, so every load is independent (no serial chains).
+__global__ __launch_bounds__(kRT) void radix_scan_kernel(RadixArgs a) {
+  const int d = blockIdx.x;
+  const int64_t row = blockIdx.y;
+  uint32_t* h = a.hist + row * a.tiles * kBins + d;
+  __shared__ uint32_t wsum[kRWaves];
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (int64_t t0 = 0; t0 < a.tiles; t0 += kRT) {
+    const int64_t t = t0 + threadIdx.x;
+    const uint32_t c = t < a.tiles ? h[t * kBins] : 0u;
+    uint32_t inc = c;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = carry, tot = 0;
+#pragma unroll
+    for (int q = 0; q < kRWaves; ++q) {
+      if (q < w) off += wsum[q];
+      tot += wsum[q];
+    }
+    if (t < a.tiles) h[t * kBins] = off + inc - c;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.dtotal[row * kBins + d] = carry;
+}
+
+// Downsweep: wave w owns the contiguous sub-tile [w * 1024, (w + 1) * 1024) of the tile
+// (round j = 64 consecutive keys), so (wave, round, lane) IS the source order and every
+// wave ranks its keys with wave-private digit counters - no block barrier inside the loop.
+// Then: wave-ordered offsets + per-tile digit starts (one barrier), keys/values are placed in
+// LDS in sorted tile order, and written out with consecutive threads writing consecutive
+// addresses of each digit run (coalesced; v1 scattered 4-byte writes straight to HBM).
+__global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const uint32_t* keys_in,
+                                                              const uint32_t* vals_in, uint32_t* keys_out,
+                                                              uint32_t* vals_out, int pass) {
+  const int64_t row = blockIdx.y;
+  const int tile = blockIdx.x;
+  const int shift = 8 * pass;
+  const bool last = pass == 3;
+  constexpr int kSub = kRTile / kRWaves;  // 1024 keys per wave
+  __shared__ uint32_t base[kBins];        // global (row-relative) start of each digit's run
+  __shared__ uint32_t tstart[kBins];      // start of each digit inside the sorted tile
+  __shared__ uint32_t wc[kRWaves][kBins]; // per-wave digit counts -> per-wave offsets
+  __shared__ uint32_t wsum[kRWaves];
+  __shared__ uint32_t sk[kRTile], sv[kRTile];
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const int64_t tbase = static_cast<int64_t>(tile) * kRTile;
+  const int64_t wbase = tbase + static_cast<int64_t>(w) * kSub;
+  uint32_t k[kRounds], v[kRounds], r[kRounds];
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const int64_t i = wbase + j * 64 + lane;
+    k[j] = 0u;
+    v[j] = 0u;
+    if (i < a.n) {
+      k[j] = load_key(a, keys_in, pass, row, i);
+      v[j] = pass == 0 ? static_cast<uint32_t>(i) : vals_in[row * a.n + i];
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < kBins / 64; ++q) wc[w][lane + 64 * q] = 0;
+  {  // digit bases = exclusive scan of the row's digit totals + this tile's prefix in the digit
+    const uint32_t tot = a.dtotal[row * kBins + threadIdx.x];
+    uint32_t inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+#pragma unroll
+    for (int q = 0; q < kRWaves; ++q)
+      if (q < w) off += wsum[q];
+    base[threadIdx.x] = off + inc - tot + a.hist[(row * a.tiles + tile) * kBins + threadIdx.x];
+  }
+  // wave-local stable ranks (wave-private counters; a wave's LDS ops are in program order)
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const bool valid = wbase + j * 64 + lane < a.n;
+    const uint64_t active = __ballot(valid);
+    const uint32_t d = (k[j] >> shift) & 0xffu;
+    const uint64_t peers = match_digit(d, active);
+    r[j] = wc[w][d] + static_cast<uint32_t>(__popcll(peers & below));
+    if (valid && (__ffsll(static_cast<long long>(peers)) - 1) == lane)
+      wc[w][d] += static_cast<uint32_t>(__popcll(peers));
+  }
+  __syncthreads();
+  {  // thread t owns digit t: per-wave exclusive offsets, tile count, tile-start scan
+    const int t = threadIdx.x;
+    uint32_t o = 0;
+#pragma unroll
+    for (int q = 0; q < kRWaves; ++q) {
+      const uint32_t c = wc[q][t];
+      wc[q][t] = o;
+      o += c;
+    }
+    uint32_t inc = o;
+#pragma unroll
+    for (int s2 = 1; s2 < 64; s2 <<= 1) {
+      const uint32_t u = __shfl_up(inc, s2, 64);
+      if (lane >= s2) inc += u;
+    }
+    __syncthreads();  // wsum reuse
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+#pragma unroll
+    for (int q = 0; q < kRWaves; ++q)
+      if (q < w) off += wsum[q];
+    tstart[t] = off + inc - o;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    if (wbase + j * 64 + lane < a.n) {
+      const uint32_t d = (k[j] >> shift) & 0xffu;
+      const uint32_t p = tstart[d] + wc[w][d] + r[j];
+      sk[p] = k[j];
+      sv[p] = v[j];
+    }
+  }
+  __syncthreads();
+  const int64_t tn64 = a.n - tbase;
+  const int tn = static_cast<int>(tn64 < kRTile ? tn64 : kRTile);
+  for (int p = threadIdx.x; p < tn; p += kRT) {
+    const uint32_t key = sk[p];
+    const uint32_t d = (key >> shift) & 0xffu;
+    const int64_t pos = row * a.n + base[d] + (p - tstart[d]);
+    if (last) {
+      a.out_sorted[pos] = key2f_desc(key);
+      a.out_order[pos] = static_cast<int32_t>(sv[p]);
+    } else {
+      keys_out[pos] = key;
+      vals_out[pos] = sv[p];
+    }
+  }
+}
+
+// [n, C] row-major -> [C, n] (LDS-tiled 64 x 64 transpose; coalesced both ways)
+__global__ __launch_bounds__(kRT) void transpose_kernel(const float* in, int64_t n, int64_t c, int64_t ld_in,
+                                                        float* out) {
+  __shared__ float t[64][65];
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * 64, c0 = static_cast<int64_t>(blockIdx.y) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += kRT / 64) {
+    const int64_t i = i0 + r, cc = c0 + tx;
+    t[r][tx] = (i < n && cc < c) ? in[i * ld_in + cc] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += kRT / 64) {
+    const int64_t cc = c0 + r, i = i0 + tx;
+    if (cc < c && i < n) out[cc * n + i] = t[tx][r];
+  }
+}
+
+}  // namespace
+
+int64_t radix_sort_tiles(int64_t n) { return (n + kRTile - 1) / kRTile; }
+
+int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream) {
+  if (n <= 0 || c <= 0) return 0;
+  const dim3 grid(static_cast<unsigned>((n + 63) / 64), static_cast<unsigned>((c + 63) / 64));
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(kRT), 0, stream, in, n, c, ld_in, out);
+  return static_cast<int>(hipGetLastError());
+}
+
+int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
+  if (a.n <= 0 || a.rows <= 0) return 0;
+  const dim3 grid(static_cast<unsigned>(a.tiles), static_cast<unsigned>(a.rows));
+  const uint32_t* kin[4] = {nullptr, a.keys0, a.keys1, a.keys0};
+  const uint32_t* vin[4] = {nullptr, a.vals0, a.vals1, a.vals0};
+  uint32_t* kout[4] = {a.keys0, a.keys1, a.keys0, nullptr};
+  uint32_t* vout[4] = {a.vals0, a.vals1, a.vals0, nullptr};
+  for (int p = 0; p < 4; ++p) {
+    hipLaunchKernelGGL(radix_upsweep_kernel, grid, dim3(kRT), 0, stream, a, kin[p], p);
+    hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins, static_cast<unsigned>(a.rows)), dim3(kRT), 0, stream, a);
+    hipLaunchKernelGGL(radix_downsweep_kernel, grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p);
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace tea

@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
 }
 
 __global__ __launch_bounds__(kB) void moments_finalize_kernel(MomentsArgs a, int P) {
-  constexpr int G = 16, C = kB / G;  // partial groups x columns per block
+  constexpr int G = 32, C = kB / G;  // partial groups x columns per block (<= 8 partials each)
   const int64_t d = a.d;
   const int c = threadIdx.x % C, grp = threadIdx.x / C;
   const int64_t col = static_cast<int64_t>(blockIdx.x) * C + c;
@@ -156,7 +156,8 @@ __global__ __launch_bounds__(kB) void moments_finalize_kernel(MomentsArgs a, int
   const int64_t stride = sl.n * d + 1;
   __shared__ double lds[G][kStats + 1][C];
   double s[kStats + 1] = {0, 0, 0, 0, 0};
-  for (int p = grp; p < P; p += G) {
+#pragma unroll 8
+  for (int p = grp; p < P; p += G) {  // independent loads: the unroll keeps 8 in flight
     const double* ws = a.ws + p * stride;
     if (col < d) {
 #pragma unroll
@@ -255,7 +256,7 @@ int launch_column_moments(const MomentsArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(moments_partial_kernel<4>, dim3(P, ct), dim3(kB), 0, stream, a);
   else
     hipLaunchKernelGGL(moments_partial_kernel<1>, dim3(P, ct), dim3(kB), 0, stream, a);
-  const unsigned fb = static_cast<unsigned>((a.d + 15) / 16);
+  const unsigned fb = static_cast<unsigned>((a.d + 7) / 8);
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(fb), dim3(kB), 0, stream, a, P);
   return static_cast<int>(hipGetLastError());
 }

@@ -25,7 +25,7 @@ namespace tea {
 namespace {
 
 constexpr int kT = 256;              // threads per block
-constexpr int kPer = 16;             // samples per thread
+constexpr int kPer = 4;              // samples per thread (1024-sample tiles: ~1000 blocks at 1M)
 constexpr int kTile = kT * kPer;     // samples per tile
 
 struct alignas(16) D2 {
@@ -90,7 +90,8 @@ __device__ __forceinline__ K key_at(const AucScanArgs& a, int r, int64_t i) {
 }
 
 __device__ __forceinline__ float2 sample_ab(const AucScanArgs& a, int r, int64_t i) {
-  const int64_t src = a.order[r * a.order_stride + i];
+  const int64_t src = a.order32 ? static_cast<int64_t>(a.order32[r * a.order_stride + i])
+                                : a.order[r * a.order_stride + i];
   float t;
   if (a.class_mode) {
     t = load_as_i64(a.target, a.tg_dt, src) == r ? 1.f : 0.f;

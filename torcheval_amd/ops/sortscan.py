@@ -12,8 +12,16 @@ from torcheval_amd.ops import native
 
 
 def _sort_rows(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Descending per-row sort: K3a radix sort for f32 (int32 permutation); torch.sort for f64."""
     if x.dtype not in (torch.float32, torch.float64):
         x = x.float()  # f16/bf16 -> f32 is exact and order preserving
+    if x.dtype == torch.float32 and x.shape[-1] < 2**31:
+        if x.stride(-1) != 1:
+            x = x.contiguous()
+        s = torch.empty(x.shape, dtype=torch.float32, device=x.device)
+        idx = torch.empty(x.shape, dtype=torch.int32, device=x.device)
+        native().sort_desc(x, s, idx)
+        return s, idx
     s, idx = torch.sort(x.contiguous(), dim=-1, descending=True)
     return s, idx
 
@@ -50,7 +58,15 @@ def multiclass_auc(
     pr: bool = False,
 ) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
     """One-vs-rest per-class AUROC / AUPRC (float64 [C]) of ``input`` [n, C] vs labels [n]."""
-    s, idx = _sort_rows(input.t())
+    x = input
+    if x.dtype in (torch.float16, torch.bfloat16):
+        x = x.float()
+    if x.dtype == torch.float32 and x.stride(-1) == 1:
+        xt = torch.empty(x.shape[1], x.shape[0], dtype=torch.float32, device=x.device)
+        native().transpose_f32(x, xt)  # LDS-tiled; torch's strided copy is ~10x slower here
+    else:
+        xt = x.t()
+    s, idx = _sort_rows(xt)
     rows = s.shape[0]
     out_roc = torch.empty(rows, dtype=torch.float64, device=input.device) if roc else None
     out_pr = torch.empty(rows, dtype=torch.float64, device=input.device) if pr else None
