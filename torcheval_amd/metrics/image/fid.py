@@ -4,9 +4,9 @@ MI355X path:
 * update: features from the model, then the K8 FP32-MFMA symmetric rank-k kernel adds
   act^T act (upper-triangle tiles, mirrored) and the column sums straight into the states -
   half the FLOPs of the reference's dense ``act.T @ act`` and no separate ``sum``;
-* compute: tr sqrt(S1 S2) via two symmetric eigendecompositions in FP64,
-  tr sqrt(S1^1/2 S2 S1^1/2), instead of the reference's non-symmetric ``linalg.eigvals``
-  (better conditioned; identical in exact arithmetic);
+* compute: tr sqrt(S1 S2) in FP64 from the symmetric L^T S2 L (S1 = L L^T, Cholesky) with an
+  eigenvalues-only ``eigvalsh``, instead of the reference's non-symmetric ``linalg.eigvals``
+  (better conditioned, identical in exact arithmetic; singular S1 falls back to eigh);
 * sync: every state is ``merge="sum"``, so syncing is one RCCL all-reduce of 2 x D^2 + 2 x D
   floats; the model itself is never pickled or transferred (the reference all-gathers the
   whole pickled metric, Inception-v3 included).
@@ -43,18 +43,33 @@ def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
     cov_sum += torch.matmul(act.T, act)
 
 
+def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
+    """tr sqrt(S1 S2) for symmetric PSD S1, S2 (FP64).
+
+    The eigenvalues of S1 S2 equal those of the symmetric L^T S2 L when S1 = L L^T, so the
+    fast path is one Cholesky, two triangular products and ONE eigenvalues-only ``eigvalsh``
+    (no eigenvectors, no back-transformation).  A singular S1 (fewer samples than features)
+    has no Cholesky factor; then S1^1/2 comes from a full ``eigh`` and the same eigvalsh runs
+    on S1^1/2 S2 S1^1/2."""
+    L, info = torch.linalg.cholesky_ex(s1)
+    if int(info) == 0:
+        m = L.T @ s2 @ L
+    else:
+        lam, vec = torch.linalg.eigh(s1)
+        root = (vec * lam.clamp(min=0).sqrt()) @ vec.T
+        m = root @ s2 @ root
+    ev = torch.linalg.eigvalsh((m + m.T) / 2)
+    return ev.clamp(min=0).sqrt().sum()
+
+
 def frechet_distance(mu1: Tensor, sigma1: Tensor, mu2: Tensor, sigma2: Tensor) -> Tensor:
-    """||mu1 - mu2||^2 + tr S1 + tr S2 - 2 tr sqrt(S1^1/2 S2 S1^1/2)  (FP64 symmetric eigh)."""
+    """||mu1 - mu2||^2 + tr S1 + tr S2 - 2 tr sqrt(S1 S2)  (FP64, symmetric formulation)."""
     mu1, mu2 = mu1.double(), mu2.double()
     s1 = sigma1.double()
     s2 = sigma2.double()
     s1 = (s1 + s1.T) / 2
     s2 = (s2 + s2.T) / 2
-    lam, vec = torch.linalg.eigh(s1)
-    root = (vec * lam.clamp(min=0).sqrt()) @ vec.T
-    m = root @ s2 @ root
-    ev = torch.linalg.eigvalsh((m + m.T) / 2)
-    tr_sqrt = ev.clamp(min=0).sqrt().sum()
+    tr_sqrt = _tr_sqrt_product(s1, s2)
     return (mu1 - mu2).square().sum() + s1.trace() + s2.trace() - 2 * tr_sqrt
 
 
