@@ -27,6 +27,8 @@ from torcheval_amd.metrics import functional as F  # noqa: E402
 
 # BASELINE.md "measured here" reference numbers (8-core CPU), ms per call
 REF_CPU_MS = {
+    "multiclass_accuracy functional bs=8 C=6": 1000 / 42013,
+    "MulticlassAccuracy.update bs=8 C=6": None,
     "MulticlassAccuracy.update micro bs8192 C1000": 1000 / 351,
     "MulticlassAccuracy.update macro bs8192 C1000": 1000 / 423,
     "MulticlassConfusionMatrix(1000).update bs8192": 1000 / 224,
@@ -176,7 +178,29 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
             m.update_activations(torch.randn(4 * D, D, device=dev, generator=g) * (1.0 if real else 1.1), real)
         return m.compute
 
+    def small_functional():
+        x, y = torch.randn(8, 6, device=dev, generator=g), randint(6, 8)
+        return lambda: F.multiclass_accuracy(x, y)
+
+    def small_class():
+        x, y = torch.randn(8, 6, device=dev, generator=g), randint(6, 8)
+        m = M.MulticlassAccuracy(device=dev)
+        return lambda: m.update(x, y)
+
+    def small_graphed():
+        x, y = torch.randn(8, 6, device=dev, generator=g), randint(6, 8)
+        m = M.MulticlassAccuracy(device=dev)
+        if dev.type != "cuda":
+            return lambda: m.update(x, y)
+        from torcheval_amd.utils.graphs import GraphedUpdate
+
+        step = GraphedUpdate(m, x, y)
+        return lambda: step(x, y)
+
     return {
+        "multiclass_accuracy functional bs=8 C=6": small_functional,
+        "MulticlassAccuracy.update bs=8 C=6": small_class,
+        "MulticlassAccuracy.update bs=8 C=6 HIP-graph replay": small_graphed,
         "MulticlassAccuracy.update micro bs8192 C1000": acc("micro"),
         "MulticlassAccuracy.update macro bs8192 C1000": acc("macro"),
         "MulticlassConfusionMatrix(1000).update bs8192": confusion,

@@ -598,4 +598,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
         py::arg("act"), py::arg("cov"), py::arg("colsum"));
   tea_register_runtime(m);
+  tea_register_cpu_metrics(m);
 }

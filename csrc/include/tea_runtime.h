@@ -6,3 +6,4 @@
 #include <pybind11/pybind11.h>
 
 void tea_register_runtime(pybind11::module_& m);
+void tea_register_cpu_metrics(pybind11::module_& m);

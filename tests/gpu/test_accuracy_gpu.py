@@ -107,3 +107,38 @@ def test_k2_class_states_and_bf16():
         X, T = torch.cat(xs), torch.cat(ts)
         torch.testing.assert_close(m.compute().cpu(), multilabel_accuracy(X.bfloat16().float(), T, criteria=crit))
         torch.testing.assert_close(mk.compute().cpu(), topk_multilabel_accuracy(X, T, criteria=crit, k=3))
+
+
+# ----------------------------------------------------------------------------- HIP graphs
+def test_graphed_update_matches_eager():
+    from torcheval_amd.metrics import MulticlassAccuracy, MulticlassConfusionMatrix, MultilabelAccuracy
+    from torcheval_amd.utils.graphs import GraphedUpdate
+
+    g = torch.Generator(device="cuda").manual_seed(0)
+    xs = [torch.randn(64, 10, device="cuda", generator=g) for _ in range(20)]
+    ys = [torch.randint(0, 10, (64,), device="cuda", generator=g) for _ in range(20)]
+    for make in (lambda: MulticlassAccuracy(device="cuda"),
+                 lambda: MulticlassAccuracy(average="macro", num_classes=10, device="cuda"),
+                 lambda: MulticlassConfusionMatrix(10, device="cuda")):
+        eager, graphed = make(), make()
+        step = GraphedUpdate(graphed, xs[0], ys[0])
+        for x, y in zip(xs, ys):
+            eager.update(x, y)
+            step(x, y)
+        torch.testing.assert_close(graphed.compute(), eager.compute())
+    ml_e, ml_g = MultilabelAccuracy(criteria="hamming", device="cuda"), MultilabelAccuracy(criteria="hamming", device="cuda")
+    t = [(torch.rand(64, 10, device="cuda") < 0.5).long() for _ in range(5)]
+    step = GraphedUpdate(ml_g, xs[0].sigmoid(), t[0])
+    for x, tt in zip(xs, t):
+        ml_e.update(x.sigmoid(), tt)
+        step(x.sigmoid(), tt)
+    torch.testing.assert_close(ml_g.compute(), ml_e.compute())
+
+
+def test_graphed_update_rejects_rebinding_metric():
+    from torcheval_amd.metrics import PeakSignalNoiseRatio
+    from torcheval_amd.utils.graphs import GraphedUpdate
+
+    m = PeakSignalNoiseRatio(device="cuda")  # its update rebinds (self.x = self.x + ...)
+    with pytest.raises(RuntimeError, match="rebinds its states"):
+        GraphedUpdate(m, torch.rand(8, device="cuda"), torch.rand(8, device="cuda"))

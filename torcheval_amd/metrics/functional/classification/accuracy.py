@@ -14,7 +14,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops import use_native
+from torcheval_amd.ops import native, native_loaded, use_native
 from torcheval_amd.ops.classification import (
     binary_counts,
     cls_counts,
@@ -40,7 +40,6 @@ def binary_accuracy(
     return _accuracy_compute(num_correct, num_total, "micro")
 
 
-@torch.inference_mode()
 def multiclass_accuracy(
     input: torch.Tensor,
     target: torch.Tensor,
@@ -57,6 +56,46 @@ def multiclass_accuracy(
     sample correct when its target is within the top-k scores.
     Class version: ``torcheval_amd.metrics.MulticlassAccuracy``.
     """
+    if (
+        average == "micro"
+        and type(k) == int
+        and k >= 1
+        and not input.is_cuda
+        and input.numel() <= _CPU_FAST_MAX
+        and _cpu_fast_ok(input, target, k, num_classes)
+    ):
+        # small CPU batches: one fused C++ call instead of six ATen dispatches
+        return native().cpu_micro_accuracy(input, target, k)
+    return _multiclass_accuracy_impl(input, target, average=average, num_classes=num_classes, k=k)
+
+
+_CPU_FAST_MAX = 1 << 16
+
+
+def _cpu_fast_ok(input: torch.Tensor, target: torch.Tensor, k: int, num_classes: Optional[int]) -> bool:
+    if not native_loaded() or target.dim() != 1 or target.dtype != torch.int64 or target.numel() == 0:
+        return False
+    if input.dim() == 2:
+        ok = (
+            input.dtype in (torch.float32, torch.float64)
+            and input.shape[0] == target.shape[0]
+            and input.stride(1) == 1
+            and input.shape[1] > 0
+            and (num_classes is None or input.shape[1] == num_classes)
+        )
+        return ok and (k == 1 or k <= input.shape[1]) and not input.requires_grad
+    return input.dim() == 1 and k == 1 and input.dtype == torch.int64 and input.shape == target.shape
+
+
+@torch.inference_mode()
+def _multiclass_accuracy_impl(
+    input: torch.Tensor,
+    target: torch.Tensor,
+    *,
+    average: Optional[str],
+    num_classes: Optional[int],
+    k: int,
+) -> torch.Tensor:
     _accuracy_param_check(average, num_classes, k)
     num_correct, num_total = _multiclass_accuracy_update(input, target, average, num_classes, k)
     return _accuracy_compute(num_correct, num_total, average)

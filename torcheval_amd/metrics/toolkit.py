@@ -17,7 +17,12 @@ import torch.distributed as dist
 
 from torcheval_amd.metrics.metric import Metric, TComputeReturn
 from torcheval_amd.parallel.distributed import PGWrapper
-from torcheval_amd.parallel.state_sync import sync_metric, sync_metric_collection
+from torcheval_amd.parallel.state_sync import (
+    PendingSync,
+    start_sync_collection,
+    sync_metric,
+    sync_metric_collection,
+)
 
 log: logging.Logger = logging.getLogger(__name__)
 
@@ -40,6 +45,60 @@ def sync_and_compute_collection(
     """Sync a dict of metrics (batched into one exchange) and compute each on all ranks."""
     synced_metrics = get_synced_metric_collection(metrics, process_group)
     return {key: m.compute() for key, m in synced_metrics.items()}
+
+
+class SyncFuture:
+    """Handle of :func:`sync_and_compute_async` / :func:`get_synced_metric_async`.
+
+    ``wait()`` returns the synced metric (or dict of metrics); ``compute()`` returns the
+    synced value(s).  Every rank must call ``wait``/``compute`` (it may run collectives).
+    """
+
+    def __init__(self, pending: Optional[PendingSync], ready: Any, single: bool) -> None:
+        self._pending = pending
+        self._ready = ready
+        self._single = single
+
+    def wait(self) -> Any:
+        if self._ready is None:
+            out = self._pending.finish()
+            self._ready = out["_"] if self._single else out
+            self._pending = None
+        return self._ready
+
+    def compute(self) -> Any:
+        synced = self.wait()
+        if self._single:
+            return synced.compute()
+        return {key: m.compute() for key, m in synced.items()}
+
+
+def get_synced_metric_async(
+    metric: Union[Metric, MutableMapping[str, Metric]],
+    process_group: Optional[dist.ProcessGroup] = None,
+) -> SyncFuture:
+    """Start syncing ``metric`` (or a dict of metrics) and return immediately.
+
+    The states are snapshotted now; the bucketed RCCL all-reduce of additive / extremal states
+    runs on RCCL's stream while the caller keeps calling ``update()`` on the live metric(s).
+    The result reflects the states at the time of this call (same on every rank).
+    """
+    single = isinstance(metric, Metric)
+    world_size = PGWrapper(process_group).get_world_size()
+    _validate_rank_and_world_size(world_size)
+    if world_size == 1:
+        return SyncFuture(None, clone_metric(metric) if single else {k: clone_metric(m) for k, m in metric.items()}, single)
+    coll = {"_": metric} if single else metric
+    pending = start_sync_collection(coll, process_group if process_group else dist.group.WORLD, world_size)
+    return SyncFuture(pending, None, single)
+
+
+def sync_and_compute_async(
+    metric: Union[Metric, MutableMapping[str, Metric]],
+    process_group: Optional[dist.ProcessGroup] = None,
+) -> SyncFuture:
+    """Asynchronous :func:`sync_and_compute`: ``sync_and_compute_async(m).compute()``."""
+    return get_synced_metric_async(metric, process_group)
 
 
 def get_synced_state_dict(

@@ -18,6 +18,8 @@ Here the same result is produced with device-resident RCCL traffic:
   exactly (including order-dependent merges such as window metrics).
 
 The all-reduce buckets are issued before the all-gather, so both are in flight together.
+``start_sync_collection`` / ``PendingSync.finish`` split the exchange so the all-reduce can
+overlap further ``update()`` calls (``toolkit.sync_and_compute_async``).
 """
 
 import copy
@@ -61,12 +63,106 @@ def _shallow_clone(metric: Metric) -> Metric:
     return copy.copy(metric)
 
 
-def sync_metric_collection(
+class PendingSync:
+    """An in-flight metric sync (see :func:`start_sync_collection`).
+
+    At creation every state that will travel has been snapshotted (the all-reduce buckets are
+    packing copies already queued on RCCL's own stream; gathered states are cloned), so the
+    caller may keep calling ``update()`` on the original metrics while the all-reduce runs.
+    ``finish()`` issues the all-gather-v (if any), waits, and assembles the merged metrics.
+    """
+
+    def __init__(self, metrics, group, ws, typed, gather_tree, reduced, reduce_slots, outs) -> None:
+        self._metrics = metrics
+        self._group = group
+        self._ws = ws
+        self._typed = typed
+        self._gather_tree = gather_tree
+        self._reduced = reduced
+        self._reduce_slots = reduce_slots
+        self._outs = outs
+        self._result: Optional[Dict[str, Metric]] = None
+
+    def finish(self) -> Dict[str, Metric]:
+        if self._result is not None:
+            return self._result
+        metrics, ws, gather_tree = self._metrics, self._ws, self._gather_tree
+        gathered = (
+            collectives.packed_all_gather(
+                gather_tree, self._group, ws, default_factory=_ZeroTensor(torch.device("cpu"))
+            )
+            if gather_tree
+            else None
+        )
+        reduced_values = self._reduced.wait()
+
+        result: Dict[str, Metric] = {}
+        # typed metrics: clone + fill reduced / concatenated states
+        for key, m in metrics.items():
+            if not self._typed[key]:
+                continue
+            out = self._outs[key]
+            result[key] = out
+            if gathered is not None and key in gather_tree:
+                for name in gather_tree[key]["states"]:
+                    merged: List[torch.Tensor] = []
+                    for r in range(ws):
+                        merged.extend(t.to(m.device) for t in gathered[r][key]["states"][name])
+                    setattr(out, name, merged)
+        for (key, name), value in zip(self._reduce_slots, reduced_values):
+            setattr(result[key], name, value.to(metrics[key].device))
+
+        # untyped metrics: shadow per rank + the metric's own merge_state (reference semantics)
+        for key, m in metrics.items():
+            if self._typed[key]:
+                continue
+            shadows = []
+            for r in range(ws):
+                sh = _shallow_clone(self._outs[key])
+                entry = gathered[r][key]
+                for attr, v in entry["extras"].items():
+                    setattr(sh, attr, v)
+                for name, v in entry["states"].items():
+                    if isinstance(v, dict):
+                        v = defaultdict(_ZeroTensor(m.device), v)
+                    setattr(sh, name, v)
+                shadows.append(sh)
+            base = shadows[0].to(m.device)
+            # detach base states from the shared receive buffer before in-place merges
+            for name in m._state_name_to_default:
+                v = getattr(base, name)
+                if isinstance(v, torch.Tensor):
+                    setattr(base, name, v.clone())
+                elif isinstance(v, list):
+                    setattr(base, name, [t.clone() for t in v])
+            result[key] = base.merge_state(shadows[1:])
+        self._result = result
+        return result
+
+
+def _snapshot(v: Any) -> Any:
+    if isinstance(v, torch.Tensor):
+        return v.detach().clone()
+    if isinstance(v, list):
+        return [_snapshot(x) for x in v]
+    if isinstance(v, dict):
+        return {k: _snapshot(x) for k, x in v.items()}
+    return v
+
+
+def start_sync_collection(
     metrics: MutableMapping[str, Metric],
     process_group: Optional[dist.ProcessGroup] = None,
     world_size: Optional[int] = None,
-) -> Dict[str, Metric]:
-    """Return a dict of new metrics whose states are merged over every rank of the group."""
+    *,
+    snapshot: bool = True,
+) -> PendingSync:
+    """Snapshot the states of ``metrics`` and issue the bucketed all-reduce asynchronously.
+
+    The all-reduce rides RCCL's internal stream, so it overlaps whatever the caller enqueues
+    next on the compute stream (typically more ``update()`` calls).  With ``snapshot=False``
+    gathered states are referenced instead of cloned (the blocking path, which finishes
+    immediately, uses this to avoid a copy)."""
     group = process_group
     ws = world_size if world_size is not None else dist.get_world_size(group)
 
@@ -78,11 +174,14 @@ def sync_metric_collection(
     reduce_slots: List[tuple] = []  # (key, state_name)
     gather_tree: Dict[str, Any] = {}
     typed: Dict[str, bool] = {}
+    outs: Dict[str, Metric] = {}
+    keep = _snapshot if snapshot else (lambda v: v)
 
     for key, m in metrics.items():
         is_typed = _is_typed(m)
         typed[key] = is_typed
         kinds = m._state_merge_kinds()
+        outs[key] = _shallow_clone(m)
         if is_typed:
             cat_states = {}
             for name, kind in kinds.items():
@@ -92,11 +191,11 @@ def sync_metric_collection(
                     reduce_ops.append(kind)
                     reduce_slots.append((key, name))
                 else:
-                    cat_states[name] = list(value)
+                    cat_states[name] = keep(list(value))
             if cat_states:
                 gather_tree[key] = {"states": cat_states}
         else:
-            states = {name: getattr(m, name) for name in kinds}
+            states = {name: keep(getattr(m, name)) for name in kinds}
             extras = {
                 k: v
                 for k, v in vars(m).items()
@@ -104,59 +203,18 @@ def sync_metric_collection(
             }
             gather_tree[key] = {"states": states, "extras": extras}
 
-    # issue the all-reduce buckets first (async), then the all-gather-v
+    # the packing copies inside snapshot the reduce states; RCCL runs them asynchronously
     reduced = collectives.allreduce_coalesced_async(reduce_tensors, reduce_ops, group)
-    gathered = (
-        collectives.packed_all_gather(
-            gather_tree, group, ws, default_factory=_ZeroTensor(torch.device("cpu"))
-        )
-        if gather_tree
-        else None
-    )
-    reduced_values = reduced.wait()
+    return PendingSync(metrics, group, ws, typed, gather_tree, reduced, reduce_slots, outs)
 
-    result: Dict[str, Metric] = {}
-    # typed metrics: clone + fill reduced / concatenated states
-    for key, m in metrics.items():
-        if not typed[key]:
-            continue
-        out = _shallow_clone(m)
-        result[key] = out
-        if gathered is not None and key in gather_tree:
-            for name in gather_tree[key]["states"]:
-                merged: List[torch.Tensor] = []
-                for r in range(ws):
-                    merged.extend(t.to(m.device) for t in gathered[r][key]["states"][name])
-                setattr(out, name, merged)
-    for (key, name), value in zip(reduce_slots, reduced_values):
-        m = metrics[key]
-        setattr(result[key], name, value.to(m.device))
 
-    # untyped metrics: shadow per rank + the metric's own merge_state (reference semantics)
-    for key, m in metrics.items():
-        if typed[key]:
-            continue
-        shadows = []
-        for r in range(ws):
-            sh = _shallow_clone(m)
-            entry = gathered[r][key]
-            for attr, v in entry["extras"].items():
-                setattr(sh, attr, v)
-            for name, v in entry["states"].items():
-                if isinstance(v, dict):
-                    v = defaultdict(_ZeroTensor(m.device), v)
-                setattr(sh, name, v)
-            shadows.append(sh)
-        base = shadows[0].to(m.device)
-        # detach base states from the shared receive buffer before in-place merges
-        for name in m._state_name_to_default:
-            v = getattr(base, name)
-            if isinstance(v, torch.Tensor):
-                setattr(base, name, v.clone())
-            elif isinstance(v, list):
-                setattr(base, name, [t.clone() for t in v])
-        result[key] = base.merge_state(shadows[1:])
-    return result
+def sync_metric_collection(
+    metrics: MutableMapping[str, Metric],
+    process_group: Optional[dist.ProcessGroup] = None,
+    world_size: Optional[int] = None,
+) -> Dict[str, Metric]:
+    """Return a dict of new metrics whose states are merged over every rank of the group."""
+    return start_sync_collection(metrics, process_group, world_size, snapshot=False).finish()
 
 
 def sync_metric(
