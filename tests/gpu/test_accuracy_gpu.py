@@ -136,9 +136,26 @@ def test_graphed_update_matches_eager():
 
 
 def test_graphed_update_rejects_rebinding_metric():
-    from torcheval_amd.metrics import PeakSignalNoiseRatio
+    from torcheval_amd.metrics import Metric, PeakSignalNoiseRatio
     from torcheval_amd.utils.graphs import GraphedUpdate
 
-    m = PeakSignalNoiseRatio(device="cuda")  # its update rebinds (self.x = self.x + ...)
+    class Rebinding(Metric):
+        def __init__(self):
+            super().__init__(device="cuda")
+            self._add_state("total", torch.zeros((), device="cuda"))
+
+        def update(self, x):
+            self.total = self.total + x.sum()  # new tensor each call: not replayable
+            return self
+
+        def compute(self):
+            return self.total
+
+        def merge_state(self, metrics):
+            return self
+
     with pytest.raises(RuntimeError, match="rebinds its states"):
-        GraphedUpdate(m, torch.rand(8, device="cuda"), torch.rand(8, device="cuda"))
+        GraphedUpdate(Rebinding(), torch.rand(8, device="cuda"))
+    # an update that copies host data to the device cannot be recorded at all
+    with pytest.raises(RuntimeError, match="cannot be captured"):
+        GraphedUpdate(PeakSignalNoiseRatio(device="cuda"), torch.rand(8, device="cuda"), torch.rand(8, device="cuda"))

@@ -60,8 +60,14 @@ class GraphedUpdate:
         torch.cuda.current_stream().wait_stream(stream)
         ptrs = _state_ptrs(metric)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph, stream=stream):
-            metric.update(*self._static)
+        try:
+            with torch.cuda.graph(self.graph, stream=stream):
+                metric.update(*self._static)
+        except Exception as e:  # host syncs / H2D copies / allocations that cannot be recorded
+            torch.cuda.synchronize()
+            raise RuntimeError(
+                f"{type(metric).__name__}.update cannot be captured into a HIP graph: {e}"
+            ) from e
         if _state_ptrs(metric) != ptrs:
             raise RuntimeError(
                 f"{type(metric).__name__}.update rebinds its states; it cannot be replayed from a graph"
