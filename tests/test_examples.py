@@ -25,3 +25,10 @@ def test_distributed_example_gloo() -> None:
     assert out.returncode == 0, out.stderr[-2000:]
     assert "Epoch 4/4, Batch 16/16" in out.stdout
     assert "synced throughput" in out.stdout
+
+
+def test_tour_runs() -> None:
+    sys.path.insert(0, os.path.join(REPO, "examples"))
+    import tour
+
+    tour.main("cpu")

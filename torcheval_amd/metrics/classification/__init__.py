@@ -67,3 +67,4 @@ __all__ = [
     "MultilabelRecallAtFixedPrecision",
     "TopKMultilabelAccuracy",
 ]
+__doc_name__ = "Classification Metrics"

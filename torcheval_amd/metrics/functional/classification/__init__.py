@@ -83,3 +83,4 @@ __all__ = [
     "multilabel_recall_at_fixed_precision",
     "topk_multilabel_accuracy",
 ]
+__doc_name__ = "Classification Metrics"

@@ -15,3 +15,4 @@ __all__ = [
     "ModuleSummary",
     "prune_module_summary",
 ]
+__doc_name__ = "Tools"
