@@ -60,6 +60,48 @@ def _reference_eager_rate(x_pool, y_pool, iters: int) -> float:
     return iters / (time.perf_counter() - t0)
 
 
+def _sync_extras(dev: torch.device, world: int, barrier) -> dict:
+    """BASELINE.json secondary configs at N > 1 (max over ranks, ms per call): RCCL sync of a
+    1000x1000 confusion matrix, of BinaryAUROC's 1M samples per rank (all-gather-v + K3a sort
+    of the union), and of FID's D=2048 states (one all-reduce of 2 x 16 MB + sums)."""
+    from torcheval_amd.metrics import BinaryAUROC, MulticlassConfusionMatrix
+    from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
+    from torcheval_amd.metrics.toolkit import get_synced_metric, sync_and_compute
+
+    out = {}
+    g = torch.Generator(device=dev).manual_seed(7 + dist.get_rank())
+
+    def timed(name, fn, reps):
+        try:
+            fn()
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            torch.cuda.synchronize()
+            barrier()
+            t = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64)
+            if dist.get_backend() == "nccl":
+                t = t.to(dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            out[name] = round(float(t), 3)
+        except Exception as e:  # an extra must never cost the headline number
+            out[name] = f"error: {type(e).__name__}: {e}"[:160]
+
+    cm = MulticlassConfusionMatrix(1000, device=dev)
+    cm.update(torch.randn(8192, 1000, device=dev, generator=g), torch.randint(0, 1000, (8192,), device=dev, generator=g))
+    timed("confusion_matrix_1000_sync_and_compute", lambda: sync_and_compute(cm), 20)
+    auroc = BinaryAUROC(device=dev)
+    auroc.update(torch.rand(1_000_000, device=dev, generator=g), torch.randint(0, 2, (1_000_000,), device=dev, generator=g))
+    timed("binary_auroc_1M_per_rank_sync_and_compute", lambda: sync_and_compute(auroc), 5)
+    fid = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=2048, device=dev)
+    fid.update_activations(torch.randn(1000, 2048, device=dev, generator=g), True)
+    fid.update_activations(torch.randn(1000, 2048, device=dev, generator=g), False)
+    timed("fid_2048_state_sync", lambda: get_synced_metric(fid), 5)
+    return out
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -78,8 +120,12 @@ def main() -> None:
     from torcheval_amd.metrics.toolkit import sync_and_compute
     from torcheval_amd.parallel import init_from_env
 
-    dev = init_from_env(device_type="cuda") if world > 1 else torch.device("cuda", local_rank)
+    # BENCH_BACKEND=gloo lets the multi-rank path be rehearsed with several ranks per GPU
+    backend = os.environ.get("BENCH_BACKEND", "nccl")
+    dev = torch.device("cuda", local_rank % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    if world > 1:
+        init_from_env(device_type="cuda" if backend == "nccl" else "cpu", pg_backend=backend)
 
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -95,7 +141,10 @@ def main() -> None:
 
     def barrier():
         if world > 1:
-            dist.barrier(device_ids=[dev.index])
+            if backend == "nccl":
+                dist.barrier(device_ids=[dev.index])
+            else:
+                dist.barrier()
 
     barrier()
     torch.cuda.synchronize()
@@ -117,6 +166,8 @@ def main() -> None:
         assert total == args.steps * BATCH, (total, args.steps * BATCH)
     acc_v = float(acc)
     assert 0.0 <= acc_v <= 0.01, acc_v  # random logits: ~1/1000
+
+    sync_extras = _sync_extras(dev, world, barrier) if world > 1 else None
 
     ref_rate = None
     if rank == 0 and not args.no_reference:
@@ -149,6 +200,7 @@ def main() -> None:
             "samples_per_s": round(updates_per_s * BATCH, 1),
             "hbm_GBps_per_gpu": round(updates_per_s / world * BATCH * NUM_CLASSES * 4 / 1e9, 1),
             "reference_eager_same_gpu_updates_per_s": None if ref_rate is None else round(ref_rate, 1),
+            "sync_ms": sync_extras,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
