@@ -28,7 +28,6 @@ def test_distributed_example_gloo() -> None:
 
 
 def test_tour_runs() -> None:
-    sys.path.insert(0, os.path.join(REPO, "examples"))
-    import tour
+    from examples import tour  # importable by the gloo worker processes (repo root on sys.path)
 
     tour.main("cpu")

@@ -9,7 +9,7 @@ from typing import List, Optional, Tuple, Union
 
 import torch
 
-from torcheval_amd.metrics.functional.tensor_utils import _create_threshold_tensor
+from torcheval_amd.metrics.functional.tensor_utils import _threshold_check, _create_threshold_tensor
 from torcheval_amd.ops.binned import binned_counts
 
 DEFAULT_NUM_THRESHOLD = 200
@@ -55,10 +55,7 @@ def _binary_binned_auroc_compute(
 def _binary_binned_auroc_param_check(num_tasks: int, threshold: torch.Tensor) -> None:
     if num_tasks < 1:
         raise ValueError("`num_tasks` has to be at least 1.")
-    if (torch.diff(threshold) < 0.0).any():
-        raise ValueError("The `threshold` should be a sorted tensor.")
-    if (threshold < 0.0).any() or (threshold > 1.0).any():
-        raise ValueError("The values in `threshold` should be in the range of [0, 1].")
+    _threshold_check(threshold)
 
 
 def _binary_binned_auroc_update_input_check(
@@ -124,10 +121,7 @@ def _multiclass_binned_auroc_param_check(
         )
     if num_classes < 2:
         raise ValueError("`num_classes` has to be at least 2.")
-    if (torch.diff(threshold) < 0.0).any():
-        raise ValueError("The `threshold` should be a sorted tensor.")
-    if (threshold < 0.0).any() or (threshold > 1.0).any():
-        raise ValueError("The values in `threshold` should be in the range of [0, 1].")
+    _threshold_check(threshold)
 
 
 def _multiclass_binned_auroc_update_input_check(

@@ -1,8 +1,15 @@
 """Small tensor helpers (parity: functional/tensor_utils.py:12-33)."""
 
-from typing import List, Union
+import weakref
+from typing import Dict, List, Tuple, Union
 
 import torch
+
+# Threshold tensors known to be sorted and inside [0, 1]: ints -> cached linspace, validated
+# lists, and user tensors after their first (single-sync) check.  Keyed by id with a weak
+# value so a freed tensor's id can never alias a validated one.
+_VALIDATED: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
+_LINSPACE: Dict[Tuple[int, str], torch.Tensor] = {}
 
 
 def _riemann_integral(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -13,9 +20,43 @@ def _riemann_integral(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
 def _create_threshold_tensor(
     threshold: Union[int, List[float], torch.Tensor], device: torch.device
 ) -> torch.Tensor:
-    """An int n becomes ``linspace(0, 1, n)``; a list becomes a tensor; tensors pass through."""
+    """An int n becomes ``linspace(0, 1, n)``; a list becomes a tensor; tensors pass through.
+
+    Int thresholds are cached per (n, device) - no per-call linspace launch - and, like lists
+    (checked on the host before the copy), are marked valid so ``_threshold_check`` skips the
+    device round trip the reference pays on every call."""
     if isinstance(threshold, int):
-        return torch.linspace(0, 1.0, threshold, device=device)
+        key = (threshold, str(torch.device(device)))
+        t = _LINSPACE.get(key)
+        if t is None:
+            t = torch.linspace(0, 1.0, threshold, device=device)
+            _LINSPACE[key] = t
+            _VALIDATED[id(t)] = t
+        return t
     if isinstance(threshold, list):
-        return torch.tensor(threshold, device=device)
+        _check_host(threshold)
+        t = torch.tensor(threshold, device=device)
+        _VALIDATED[id(t)] = t
+        return t
     return threshold
+
+
+def _check_host(values: List[float]) -> None:
+    if any(b < a for a, b in zip(values, values[1:])):
+        raise ValueError("The `threshold` should be a sorted tensor.")
+    if any(v < 0.0 or v > 1.0 for v in values):
+        raise ValueError("The values in `threshold` should be in the range of [0, 1].")
+
+
+def _threshold_check(threshold: torch.Tensor) -> None:
+    """Sorted and inside [0, 1] (reference messages); one host sync for unseen tensors."""
+    if _VALIDATED.get(id(threshold)) is threshold:
+        return
+    flags = torch.stack(
+        [(torch.diff(threshold) < 0.0).any(), ((threshold < 0.0) | (threshold > 1.0)).any()]
+    ).tolist()
+    if flags[0]:
+        raise ValueError("The `threshold` should be a sorted tensor.")
+    if flags[1]:
+        raise ValueError("The values in `threshold` should be in the range of [0, 1].")
+    _VALIDATED[id(threshold)] = threshold
