@@ -559,6 +559,38 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   check_launch(tea::launch_radix_sort_desc(a, stream_for(x)), "sort_desc");
 }
 
+
+// binned AUROC / AUPRC from [T, rows] float32 counts in one launch
+void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>& fn,
+                     const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc) {
+  check_gpu(tp, "tp");
+  TORCH_CHECK(tp.dim() == 2 && tp.scalar_type() == at::kFloat && fp.sizes() == tp.sizes() &&
+                  fp.strides() == tp.strides() && fp.scalar_type() == at::kFloat,
+              "binned_finalize: tp/fp must be float32 [T, rows] with equal strides");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(tp.device());
+  tea::BinnedFinalizeArgs a;
+  a.tp = tp.data_ptr<float>();
+  a.fp = fp.data_ptr<float>();
+  a.k_stride = tp.stride(0);
+  a.r_stride = tp.stride(1);
+  a.T = static_cast<int>(tp.size(0));
+  a.rows = tp.size(1);
+  if (out_auprc.has_value()) {
+    TORCH_CHECK(fn.has_value() && fn->sizes() == tp.sizes() && fn->strides() == tp.strides() &&
+                    fn->scalar_type() == at::kFloat, "binned_finalize: AUPRC needs fn like tp");
+    TORCH_CHECK(out_auprc->scalar_type() == at::kFloat && out_auprc->is_contiguous() &&
+                    out_auprc->numel() == a.rows, "binned_finalize: out_auprc float32 [rows]");
+    a.fn = fn->data_ptr<float>();
+    a.out_auprc = out_auprc->data_ptr<float>();
+  }
+  if (out_auroc.has_value()) {
+    TORCH_CHECK(out_auroc->scalar_type() == at::kDouble && out_auroc->is_contiguous() &&
+                    out_auroc->numel() == a.rows, "binned_finalize: out_auroc float64 [rows]");
+    a.out_auroc = out_auroc->data_ptr<double>();
+  }
+  check_launch(tea::launch_binned_finalize(a, stream_for(tp)), "binned_finalize");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -595,6 +627,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"));
   m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
         py::arg("x"), py::arg("out_sorted"), py::arg("out_order"));
+  m.def("binned_finalize", &binned_finalize, "binned AUROC / AUPRC from counts", py::arg("tp"),
+        py::arg("fp"), py::arg("fn") = py::none(), py::arg("out_auroc") = py::none(),
+        py::arg("out_auprc") = py::none());
   m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
         py::arg("act"), py::arg("cov"), py::arg("colsum"));
   tea_register_runtime(m);

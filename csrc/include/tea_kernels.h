@@ -114,6 +114,17 @@ struct BinnedArgs {
   int64_t out_c_stride = 0;
 };
 int64_t binned_workspace_words(int T, int64_t c);
+struct BinnedFinalizeArgs {
+  const float* tp = nullptr;  // [T, rows] counts, element (k, r) at k * k_stride + r * r_stride
+  const float* fp = nullptr;
+  const float* fn = nullptr;  // needed for AUPRC
+  int64_t k_stride = 0, r_stride = 0;
+  int T = 0;
+  int64_t rows = 0;
+  double* out_auroc = nullptr;  // [rows] float64 (reference: trapz(...).double())
+  float* out_auprc = nullptr;   // [rows] float32
+};
+int launch_binned_finalize(const BinnedFinalizeArgs& a, hipStream_t stream);
 int launch_binned(const BinnedArgs& a, hipStream_t stream);
 
 }  // namespace tea

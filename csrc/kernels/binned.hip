@@ -168,7 +168,65 @@ __global__ __launch_bounds__(kB) void binned_suffix_kernel(BinnedArgs a, int rep
   }
 }
 
+// one block per row: AUROC (trapezoid over the binned ROC points) and AUPRC (Riemann sum over
+// the binned PR points with the (precision 1, recall 0) end point) from [T, R] counts - the
+// ~20 small ATen ops of the reference compute (binned_auroc.py:111-138,
+// binned_auprc.py:86-112) in one launch.
+__global__ __launch_bounds__(kB) void binned_finalize_kernel(BinnedFinalizeArgs a) {
+  const int64_t r = blockIdx.x;
+  const int T = a.T;
+  auto at = [&](const float* p, int k) -> double { return static_cast<double>(p[k * a.k_stride + r * a.r_stride]); };
+  double area = 0.0, riem = 0.0;
+  bool riem_nan = false;
+  for (int k = threadIdx.x; k < T; k += kB) {
+    const double tp = at(a.tp, k), fp = at(a.fp, k);
+    const double tpn = k + 1 < T ? at(a.tp, k + 1) : 0.0, fpn = k + 1 < T ? at(a.fp, k + 1) : 0.0;
+    area += (fp - fpn) * (tp + tpn) * 0.5;
+    if (a.out_auprc) {
+      const double fn = at(a.fn, k);
+      double prec = tp / (tp + fp);
+      if (prec != prec) prec = 1.0;
+      const double rec = tp / (tp + fn);
+      double recn = 0.0;
+      if (k + 1 < T) recn = at(a.tp, k + 1) / (at(a.tp, k + 1) + at(a.fn, k + 1));
+      const double term = (recn - rec) * prec;
+      if (term != term) riem_nan = true;
+      else riem -= term;
+    }
+  }
+  __shared__ double s[2][kB / 64];
+  __shared__ int s_nan;
+  if (threadIdx.x == 0) s_nan = 0;
+  area = wave_sum(area);
+  riem = wave_sum(riem);
+  __syncthreads();
+  if (riem_nan) s_nan = 1;
+  if (lane_id() == 0) {
+    s[0][threadIdx.x >> 6] = area;
+    s[1][threadIdx.x >> 6] = riem;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ar = 0.0, rm = 0.0;
+    for (int w = 0; w < kB / 64; ++w) {
+      ar += s[0][w];
+      rm += s[1][w];
+    }
+    if (a.out_auroc) {
+      const double factor = at(a.tp, 0) * at(a.fp, 0);
+      a.out_auroc[r] = factor == 0.0 ? 0.5 : ar / factor;
+    }
+    if (a.out_auprc) a.out_auprc[r] = s_nan ? 0.f : static_cast<float>(rm);
+  }
+}
+
 }  // namespace
+
+int launch_binned_finalize(const BinnedFinalizeArgs& a, hipStream_t stream) {
+  if (a.rows <= 0 || a.T <= 0) return 0;
+  hipLaunchKernelGGL(binned_finalize_kernel, dim3(static_cast<unsigned>(a.rows)), dim3(kB), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
 
 int64_t binned_workspace_words(int T, int64_t c) { return static_cast<int64_t>(kReplicas) * (T + 1) * c * 2; }
 

@@ -32,11 +32,15 @@ def _create_threshold_tensor(
             t = torch.linspace(0, 1.0, threshold, device=device)
             _LINSPACE[key] = t
             _VALIDATED[id(t)] = t
+            if threshold >= 2:
+                _ENDPOINTS_OK[id(t)] = t
         return t
     if isinstance(threshold, list):
         _check_host(threshold)
         t = torch.tensor(threshold, device=device)
         _VALIDATED[id(t)] = t
+        if threshold and threshold[0] == 0 and threshold[-1] == 1:
+            _ENDPOINTS_OK[id(t)] = t
         return t
     return threshold
 
@@ -48,15 +52,28 @@ def _check_host(values: List[float]) -> None:
         raise ValueError("The values in `threshold` should be in the range of [0, 1].")
 
 
-def _threshold_check(threshold: torch.Tensor) -> None:
-    """Sorted and inside [0, 1] (reference messages); one host sync for unseen tensors."""
-    if _VALIDATED.get(id(threshold)) is threshold:
+_ENDPOINTS_OK: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
+
+
+def _threshold_check(threshold: torch.Tensor, endpoints: bool = False) -> None:
+    """Sorted and inside [0, 1] (and, with ``endpoints``, starting at 0 and ending at 1), with
+    the reference's messages - one host sync for an unseen tensor instead of up to four."""
+    known = _VALIDATED.get(id(threshold)) is threshold
+    ends = _ENDPOINTS_OK.get(id(threshold)) is threshold
+    if known and (ends or not endpoints):
         return
-    flags = torch.stack(
-        [(torch.diff(threshold) < 0.0).any(), ((threshold < 0.0) | (threshold > 1.0)).any()]
-    ).tolist()
+    checks = [(torch.diff(threshold) < 0.0).any(), ((threshold < 0.0) | (threshold > 1.0)).any()]
+    if endpoints:
+        checks += [threshold[0] != 0, threshold[-1] != 1]
+    flags = torch.stack(checks).tolist()
     if flags[0]:
         raise ValueError("The `threshold` should be a sorted tensor.")
     if flags[1]:
         raise ValueError("The values in `threshold` should be in the range of [0, 1].")
+    if endpoints and flags[2]:
+        raise ValueError("First value in `threshold` should be 0.")
+    if endpoints and flags[3]:
+        raise ValueError("Last value in `threshold` should be 1.")
     _VALIDATED[id(threshold)] = threshold
+    if endpoints:
+        _ENDPOINTS_OK[id(threshold)] = threshold

@@ -56,3 +56,23 @@ def _binned_counts_aten(
     fp = suffix[1:, :, 0]
     fn = hist[:, :, 1].sum(0)[None, :] - tp
     return tp.float(), fp.float(), fn.float()
+
+
+def binned_finalize_supported(*counts: torch.Tensor) -> bool:
+    return all(
+        use_native(c) and c.dtype == torch.float32 and c.dim() == 2 and c.shape == counts[0].shape
+        for c in counts
+    )
+
+
+def binned_finalize(
+    tp: torch.Tensor, fp: torch.Tensor, fn: Optional[torch.Tensor] = None, *, auroc: bool = True, auprc: bool = False
+) -> Tuple[Optional[torch.Tensor], Optional[torch.Tensor]]:
+    """One launch: float64 [R] binned AUROC and/or float32 [R] binned AUPRC from [T, R] counts."""
+    tp, fp = tp.contiguous(), fp.contiguous()
+    fn = fn.contiguous() if fn is not None else None
+    rows = tp.shape[1]
+    out_roc = torch.empty(rows, dtype=torch.float64, device=tp.device) if auroc else None
+    out_pr = torch.empty(rows, dtype=torch.float32, device=tp.device) if auprc else None
+    native().binned_finalize(tp, fp, fn, out_roc, out_pr)
+    return out_roc, out_pr
