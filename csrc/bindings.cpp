@@ -381,7 +381,7 @@ void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
 
 // x, t: [rows, n] (rows contiguous); w optional [rows, n]; out float64 [rows, 3] accumulated.
 void ne_sums(const Tensor& x, const Tensor& t, const optional<Tensor>& w, bool from_logits,
-             const Tensor& out, const optional<Tensor>& err) {
+             const Tensor& out, const optional<Tensor>& err, bool deterministic) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && t.sizes() == x.sizes(), "ne_sums: x/t must be [rows, n]");
   TORCH_CHECK(x.stride(1) == 1 && t.stride(1) == 1, "ne_sums: rows must be contiguous");
@@ -409,13 +409,18 @@ void ne_sums(const Tensor& x, const Tensor& t, const optional<Tensor>& w, bool f
     TORCH_CHECK(err->scalar_type() == at::kInt, "ne_sums: err must be int32");
     a.err = err->data_ptr<int>();
   }
+  Tensor ws;
+  if (deterministic && a.rows > 0) {
+    ws = at::empty({a.rows * 3 * tea::ne_sums_blocks(a.n)}, out.options());
+    a.ordered_ws = ws.data_ptr<double>();
+  }
   check_launch(tea::launch_ne_sums(a, stream_for(x)), "ne_sums");
 }
 
 // ---------------------------------------------------------------- K7 perplexity
 // input: [rows, v] logits (unit column stride); target: [rows]; out float64 [2] accumulated.
 void perplexity_sums(const Tensor& input, const Tensor& target, optional<int64_t> ignore_index,
-                     const Tensor& out, const optional<Tensor>& err) {
+                     const Tensor& out, const optional<Tensor>& err, bool deterministic) {
   check_gpu(input, "input");
   TORCH_CHECK(input.dim() == 2 && input.stride(1) == 1, "perplexity: input must be [rows, v]");
   TORCH_CHECK(target.dim() == 1 && target.size(0) == input.size(0), "perplexity: target must be [rows]");
@@ -437,6 +442,11 @@ void perplexity_sums(const Tensor& input, const Tensor& target, optional<int64_t
   }
   a.out = out.data_ptr<double>();
   if (err.has_value()) a.err = err->data_ptr<int>();
+  Tensor ws;
+  if (deterministic && a.rows > 0) {
+    ws = at::empty({2 * tea::perplexity_blocks(a.rows)}, out.options());
+    a.ordered_ws = ws.data_ptr<double>();
+  }
   const int rc = tea::launch_perplexity(a, stream_for(input));
   TORCH_CHECK(rc != -1, "perplexity: unsupported logits dtype ", input.scalar_type());
   check_launch(rc, "perplexity");
@@ -617,9 +627,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),
         py::arg("sw"));
   m.def("ne_sums", &ne_sums, "K6 normalized-entropy row sums", py::arg("x"), py::arg("t"),
-        py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"));
+        py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"),
+        py::arg("deterministic") = false);
   m.def("perplexity_sums", &perplexity_sums, "K7 fused log-softmax gather", py::arg("input"),
-        py::arg("target"), py::arg("ignore_index"), py::arg("out"), py::arg("err"));
+        py::arg("target"), py::arg("ignore_index"), py::arg("out"), py::arg("err"),
+        py::arg("deterministic") = false);
   m.def("multilabel_counts", &multilabel_counts, "K2 multilabel accuracy counts", py::arg("input"),
         py::arg("target"), py::arg("threshold"), py::arg("k"), py::arg("criteria"),
         py::arg("num_correct"), py::arg("num_total") = py::none(), py::arg("total") = 0.0);

@@ -170,8 +170,13 @@ struct NeArgs {
   int from_logits = 0;
   double* out = nullptr;  // [rows, 3]: sum w*bce, sum w*t, sum w (accumulated)
   int* err = nullptr;
+  double* ordered_ws = nullptr;  // deterministic mode: [rows * 3, ne_sums_blocks] partials
 };
+int ne_sums_blocks(int64_t n);
 int launch_ne_sums(const NeArgs& a, hipStream_t stream);
+
+// deterministic fold: out[v] += sum_{p < parts} ws[v * parts + p], summed in index order
+int launch_ordered_sum(const double* ws, int64_t nvals, int64_t parts, double* out, hipStream_t stream);
 
 }  // namespace tea
 
@@ -189,7 +194,9 @@ struct PerplexityArgs {
   int64_t ignore_index = 0;
   double* out = nullptr;  // [2]: sum of -log p(target), token count (accumulated)
   int* err = nullptr;
+  double* ordered_ws = nullptr;  // deterministic mode: [2, perplexity_blocks] partials
 };
+int perplexity_blocks(int64_t rows);
 int launch_perplexity(const PerplexityArgs& a, hipStream_t stream);
 
 }  // namespace tea

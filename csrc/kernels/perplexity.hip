@@ -127,7 +127,10 @@ __global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
     double tot = 0.0;
 #pragma unroll
     for (int w = 0; w < kWpb; ++w) tot += lds[threadIdx.x][w];
-    if (tot != 0.0) atomicAdd(a.out + threadIdx.x, tot);
+    if (a.ordered_ws)  // deterministic: per-block partial, folded in block order afterwards
+      a.ordered_ws[threadIdx.x * gridDim.x + blockIdx.x] = tot;
+    else if (tot != 0.0)
+      atomicAdd(a.out + threadIdx.x, tot);
   }
 }
 
@@ -141,10 +144,16 @@ void launch_kind(const PerplexityArgs& a, int grid, bool vec, hipStream_t s) {
 
 }  // namespace
 
+int perplexity_blocks(int64_t rows) {
+  int64_t grid = (rows + kWpb - 1) / kWpb;
+  if (grid > 512) grid = 512;
+  if (grid < 1) grid = 1;
+  return static_cast<int>(grid);
+}
+
 int launch_perplexity(const PerplexityArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
-  int64_t grid = (a.rows + kWpb - 1) / kWpb;
-  if (grid > 512) grid = 512;
+  const int64_t grid = perplexity_blocks(a.rows);
   const uintptr_t base = reinterpret_cast<uintptr_t>(a.input);
   const int vw = a.in_dt == DType::f32 ? 4 : 8;
   const bool vec = a.v % 16 == 0 && a.row_stride % vw == 0 && base % 16 == 0;
@@ -154,6 +163,7 @@ int launch_perplexity(const PerplexityArgs& a, hipStream_t stream) {
     case DType::f16: launch_kind<2>(a, static_cast<int>(grid), vec, stream); break;
     default: return -1;
   }
+  if (a.ordered_ws) return launch_ordered_sum(a.ordered_ws, 2, grid, a.out, stream);
   return static_cast<int>(hipGetLastError());
 }
 

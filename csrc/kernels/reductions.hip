@@ -226,8 +226,20 @@ __global__ __launch_bounds__(kB) void ne_sums_kernel(NeArgs a) {
   if (threadIdx.x < 3) {
     double tot = 0;
     for (int k = 0; k < kB / 64; ++k) tot += lds[threadIdx.x][k];
-    atomicAdd(a.out + r * 3 + threadIdx.x, tot);
+    if (a.ordered_ws)  // deterministic: partial per block, folded in block order afterwards
+      a.ordered_ws[(static_cast<int64_t>(r) * 3 + threadIdx.x) * gridDim.x + blockIdx.x] = tot;
+    else
+      atomicAdd(a.out + r * 3 + threadIdx.x, tot);
   }
+}
+
+__global__ __launch_bounds__(kB) void ordered_sum_kernel(const double* ws, int64_t nvals, int64_t parts,
+                                                         double* out) {
+  const int64_t v = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x;
+  if (v >= nvals) return;
+  double s = 0.0;
+  for (int64_t p = 0; p < parts; ++p) s += ws[v * parts + p];
+  out[v] += s;
 }
 
 }  // namespace
@@ -261,13 +273,26 @@ int launch_column_moments(const MomentsArgs& a, hipStream_t stream) {
   return static_cast<int>(hipGetLastError());
 }
 
-int launch_ne_sums(const NeArgs& a, hipStream_t stream) {
-  if (a.rows <= 0) return 0;
-  int64_t blocks = (a.n + kB * 16 - 1) / (kB * 16);
+int ne_sums_blocks(int64_t n) {
+  int64_t blocks = (n + kB * 16 - 1) / (kB * 16);
   if (blocks > 64) blocks = 64;
   if (blocks < 1) blocks = 1;
+  return static_cast<int>(blocks);
+}
+
+int launch_ne_sums(const NeArgs& a, hipStream_t stream) {
+  if (a.rows <= 0) return 0;
+  const int blocks = ne_sums_blocks(a.n);
   hipLaunchKernelGGL(ne_sums_kernel, dim3(static_cast<unsigned>(blocks), static_cast<unsigned>(a.rows)),
                      dim3(kB), 0, stream, a);
+  if (a.ordered_ws) return launch_ordered_sum(a.ordered_ws, a.rows * 3, blocks, a.out, stream);
+  return static_cast<int>(hipGetLastError());
+}
+
+int launch_ordered_sum(const double* ws, int64_t nvals, int64_t parts, double* out, hipStream_t stream) {
+  if (nvals <= 0) return 0;
+  hipLaunchKernelGGL(ordered_sum_kernel, dim3(static_cast<unsigned>((nvals + kB - 1) / kB)), dim3(kB), 0,
+                     stream, ws, nvals, parts, out);
   return static_cast<int>(hipGetLastError());
 }
 

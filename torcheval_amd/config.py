@@ -1,0 +1,83 @@
+"""Runtime flags: read once from the environment, settable at runtime.
+
+=============================  ========================================================
+``TORCHEVAL_AMD_DISABLE_HIP``  1: run the ATen path even for ROCm tensors (debug / A-B)
+``TORCHEVAL_AMD_VALIDATE``     1: raise input-validation errors at the ``update()`` that
+                               caused them (one host sync per update), like the reference;
+                               0 (default): kernels record violations in a device flag
+                               that ``compute()`` raises (no per-update sync)
+``TORCHEVAL_AMD_DETERMINISTIC``  1: reductions whose float accumulation order depends on
+                               block scheduling (K6 entropy sums, K7 perplexity sums) use
+                               an ordered two-pass fold - bit-identical run to run
+``TORCHEVAL_AMD_TRACE``        1: ``torch.profiler.record_function`` ranges around every
+                               metric ``update`` / ``compute`` / ``merge_state`` and the
+                               toolkit syncs (visible in torch.profiler and rocprofv3 -r)
+=============================  ========================================================
+
+Use ``torcheval_amd.config.flags(validate=True)`` as a context manager for a scoped change.
+"""
+
+import contextlib
+import os
+from typing import Iterator
+
+
+def _env(name: str) -> bool:
+    return os.environ.get(name, "0") not in ("", "0", "false", "False")
+
+
+class _Config:
+    __slots__ = ("validate", "deterministic", "trace")
+
+    def __init__(self) -> None:
+        self.validate = _env("TORCHEVAL_AMD_VALIDATE")
+        self.deterministic = _env("TORCHEVAL_AMD_DETERMINISTIC")
+        self.trace = _env("TORCHEVAL_AMD_TRACE")
+
+    @property
+    def disable_hip(self) -> bool:
+        from torcheval_amd import ops
+
+        return ops.DISABLE_HIP
+
+    @disable_hip.setter
+    def disable_hip(self, value: bool) -> None:
+        from torcheval_amd import ops
+
+        ops.DISABLE_HIP = bool(value)
+
+    def __repr__(self) -> str:
+        return (
+            f"config(disable_hip={self.disable_hip}, validate={self.validate}, "
+            f"deterministic={self.deterministic}, trace={self.trace})"
+        )
+
+
+config = _Config()
+
+
+@contextlib.contextmanager
+def flags(**kwargs: bool) -> Iterator[_Config]:
+    """Temporarily set flags: ``with flags(validate=True, deterministic=True): ...``."""
+    old = {k: getattr(config, k) for k in kwargs}
+    try:
+        for k, v in kwargs.items():
+            if not hasattr(type(config), k) and k not in _Config.__slots__:
+                raise AttributeError(f"unknown flag {k!r}")
+            setattr(config, k, v)
+        yield config
+    finally:
+        for k, v in old.items():
+            setattr(config, k, v)
+
+
+def trace_range(name: str):
+    """``record_function(name)`` when tracing is on, else a no-op context."""
+    if config.trace:
+        import torch
+
+        return torch.profiler.record_function(name)
+    return contextlib.nullcontext()
+
+
+__all__ = ["config", "flags", "trace_range"]

@@ -133,10 +133,13 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
             self.num_total += num_total
         return self
 
+    def _check_device_errors(self) -> None:
+        _raise_on_device_error(self._err)
+
     @torch.inference_mode()
     def compute(self: TAccuracy) -> torch.Tensor:
         """Return the accuracy (NaN if ``update()`` was never called)."""
-        _raise_on_device_error(self._err)
+        self._check_device_errors()
         return _accuracy_compute(self.num_correct, self.num_total, self.average)
 
     @torch.inference_mode()

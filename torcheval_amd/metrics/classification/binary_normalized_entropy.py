@@ -71,12 +71,15 @@ class BinaryNormalizedEntropy(Metric[torch.Tensor]):
         self.num_positive += num_positive
         return self
 
-    @torch.inference_mode()
-    def compute(self: TNormalizedEntropy) -> torch.Tensor:
-        """Normalized entropy per task; empty tensor if some task has no examples."""
+    def _check_device_errors(self) -> None:
         if self._err is not None and int(self._err.item()) != 0:
             self._err.zero_()
             _ne_range_check(torch.tensor([2.0]), self.from_logits)
+
+    @torch.inference_mode()
+    def compute(self: TNormalizedEntropy) -> torch.Tensor:
+        """Normalized entropy per task; empty tensor if some task has no examples."""
+        self._check_device_errors()
         if torch.any(self.num_examples == 0.0):
             return torch.empty(0)
         baseline_entropy = _baseline_update(self.num_positive, self.num_examples)

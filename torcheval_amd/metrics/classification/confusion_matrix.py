@@ -68,7 +68,7 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
             self.confusion_matrix += _confusion_matrix_update(input, target, self.num_classes)
         return self
 
-    def _check_device_err(self) -> None:
+    def _check_device_errors(self) -> None:
         if self._err is not None and int(self._err.item()) != 0:
             err = self._err.clone()
             self._err.zero_()
@@ -76,14 +76,14 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self: TMulticlassConfusionMatrix) -> torch.Tensor:
-        self._check_device_err()
+        self._check_device_errors()
         return _confusion_matrix_compute(self.confusion_matrix, normalize=self.normalize)
 
     @torch.inference_mode()
     def normalized(self: TMulticlassConfusionMatrix, normalize: Optional[str] = None) -> torch.Tensor:
         """The confusion matrix normalised with ``normalize`` (ignores the constructor's)."""
         _confusion_matrix_param_check(self.num_classes, normalize)
-        self._check_device_err()
+        self._check_device_errors()
         return _confusion_matrix_compute(self.confusion_matrix, normalize)
 
     @torch.inference_mode()

@@ -63,11 +63,14 @@ class MulticlassF1Score(Metric[torch.Tensor]):
             self.num_prediction += num_prediction
         return self
 
-    @torch.inference_mode()
-    def compute(self: TF1Score) -> torch.Tensor:
+    def _check_device_errors(self) -> None:
         from torcheval_amd.metrics.classification.accuracy import _raise_on_device_error
 
         _raise_on_device_error(self._err)
+
+    @torch.inference_mode()
+    def compute(self: TF1Score) -> torch.Tensor:
+        self._check_device_errors()
         return _f1_score_compute(self.num_tp, self.num_label, self.num_prediction, self.average)
 
     @torch.inference_mode()

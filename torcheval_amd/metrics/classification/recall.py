@@ -104,11 +104,14 @@ class MulticlassRecall(Metric[torch.Tensor]):
             self.num_predictions += num_predictions
         return self
 
-    @torch.inference_mode()
-    def compute(self: TRecall) -> torch.Tensor:
+    def _check_device_errors(self) -> None:
         from torcheval_amd.metrics.classification.accuracy import _raise_on_device_error
 
         _raise_on_device_error(self._err)
+
+    @torch.inference_mode()
+    def compute(self: TRecall) -> torch.Tensor:
+        self._check_device_errors()
         return _recall_compute(self.num_tp, self.num_labels, self.num_predictions, self.average)
 
     @torch.inference_mode()

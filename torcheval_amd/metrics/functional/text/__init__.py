@@ -271,7 +271,9 @@ def _perplexity_update(
             logits = logits.contiguous()
         out = torch.zeros(2, dtype=torch.float64, device=input.device)
         flag = err if err is not None else torch.zeros(1, dtype=torch.int32, device=input.device)
-        native().perplexity_sums(logits, tgt, ignore_index, out, flag)
+        from torcheval_amd.config import config
+
+        native().perplexity_sums(logits, tgt, ignore_index, out, flag, config.deterministic)
         if err is None and int(flag.item()) != 0:
             _perplexity_label_check(input, target, ignore_index)
         return out[0], out[1]

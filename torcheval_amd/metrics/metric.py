@@ -19,12 +19,15 @@ MI355X-first differences (documented decisions):
   picklable (the reference's lambda-defaultdict metrics are not).
 """
 
+import functools
 from abc import ABC, abstractmethod
 from collections import defaultdict
 from copy import deepcopy
-from typing import Any, Dict, Generic, Iterable, List, Optional, TypeVar, Union
+from typing import Any, Callable, Dict, Generic, Iterable, List, Optional, TypeVar, Union
 
 import torch
+
+from torcheval_amd.config import config as _cfg
 
 TSelf = TypeVar("TSelf", bound="Metric")
 TComputeReturn = TypeVar("TComputeReturn")
@@ -54,6 +57,28 @@ def _as_device(device: Optional[Union[str, torch.device]]) -> torch.device:
     return torch.device(device) if not isinstance(device, torch.device) else device
 
 
+def _instrument(fn: Callable, label: str, check_after: bool) -> Callable:
+    """Wrap a metric method: ``record_function`` range when tracing; after ``update`` in
+    validate mode, raise any device-recorded input error immediately."""
+    if getattr(fn, "__tea_instrumented__", False):
+        return fn
+
+    @functools.wraps(fn)
+    def wrapper(self, *args, **kwargs):
+        if _cfg.trace:
+            with torch.profiler.record_function(f"{type(self).__name__}.{label}"):
+                out = fn(self, *args, **kwargs)
+        else:
+            out = fn(self, *args, **kwargs)
+        if check_after and _cfg.validate:
+            with torch.inference_mode():  # error flags are created inside inference-mode updates
+                self._check_device_errors()
+        return out
+
+    wrapper.__tea_instrumented__ = True  # type: ignore[attr-defined]
+    return wrapper
+
+
 class Metric(Generic[TComputeReturn], ABC):
     """
     Base class for all metrics present in the Metrics API.
@@ -61,6 +86,20 @@ class Metric(Generic[TComputeReturn], ABC):
     Implement ``__init__()``, ``update()``, ``compute()`` and ``merge_state()`` to implement
     your own metric (reference: torcheval/metrics/metric.py:21-47).
     """
+
+    def __init_subclass__(cls, **kwargs: Any) -> None:
+        super().__init_subclass__(**kwargs)
+        for label in ("update", "compute", "merge_state"):
+            fn = cls.__dict__.get(label)
+            if fn is not None and callable(fn):
+                setattr(cls, label, _instrument(fn, label, check_after=label == "update"))
+
+    def _check_device_errors(self) -> None:
+        """Raise input-validation errors that native kernels recorded on the device.
+
+        Metrics whose GPU update validates inputs asynchronously (a device error flag instead
+        of a host sync) override this; ``compute()`` calls it, and so does every ``update()``
+        when ``torcheval_amd.config.validate`` is set."""
 
     def __init__(self: TSelf, *, device: Optional[torch.device] = None) -> None:
         torch._C._log_api_usage_once(f"torcheval_amd.metrics.{self.__class__.__name__}")

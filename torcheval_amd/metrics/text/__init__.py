@@ -96,14 +96,17 @@ class Perplexity(_SumStates):
         self.num_total += n
         return self
 
-    @torch.inference_mode()
-    def compute(self) -> torch.Tensor:
+    def _check_device_errors(self) -> None:
         if self._err is not None and int(self._err.item()) != 0:
             self._err.zero_()
             raise ValueError(
                 "Class labels in `target` tensor cannot be larger than vocab_size minus one "
                 "(detected on device in an earlier update())."
             )
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        self._check_device_errors()
         if self.num_total == 0.0:
             return torch.empty(0)
         return _perplexity_compute(self.sum_log_probs, self.num_total)

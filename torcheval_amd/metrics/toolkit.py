@@ -15,6 +15,7 @@ from typing import Any, Dict, Iterable, List, MutableMapping, Optional, TypeVar,
 import torch
 import torch.distributed as dist
 
+from torcheval_amd.config import trace_range
 from torcheval_amd.metrics.metric import Metric, TComputeReturn
 from torcheval_amd.parallel.distributed import PGWrapper
 from torcheval_amd.parallel.state_sync import (
@@ -89,7 +90,8 @@ def get_synced_metric_async(
     if world_size == 1:
         return SyncFuture(None, clone_metric(metric) if single else {k: clone_metric(m) for k, m in metric.items()}, single)
     coll = {"_": metric} if single else metric
-    pending = start_sync_collection(coll, process_group if process_group else dist.group.WORLD, world_size)
+    with trace_range("torcheval_amd.start_sync"):
+        pending = start_sync_collection(coll, process_group if process_group else dist.group.WORLD, world_size)
     return SyncFuture(pending, None, single)
 
 
@@ -142,9 +144,8 @@ def get_synced_metric(
     _validate_rank_and_world_size(world_size)
     if world_size == 1:
         return metric
-    return sync_metric(
-        metric, process_group if process_group else dist.group.WORLD, world_size
-    )
+    with trace_range("torcheval_amd.sync_metric"):
+        return sync_metric(metric, process_group if process_group else dist.group.WORLD, world_size)
 
 
 def get_synced_metric_collection(
@@ -156,9 +157,10 @@ def get_synced_metric_collection(
     _validate_rank_and_world_size(world_size)
     if world_size == 1:
         return metric_collection
-    return sync_metric_collection(
-        metric_collection, process_group if process_group else dist.group.WORLD, world_size
-    )
+    with trace_range("torcheval_amd.sync_metric_collection"):
+        return sync_metric_collection(
+            metric_collection, process_group if process_group else dist.group.WORLD, world_size
+        )
 
 
 def _validate_rank_and_world_size(world_size: int) -> None:

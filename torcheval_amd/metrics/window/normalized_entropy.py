@@ -62,11 +62,14 @@ class WindowedBinaryNormalizedEntropy(_WindowedSums):
         self._push((ce, ex, pos))
         return self
 
-    @torch.inference_mode()
-    def compute(self) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
+    def _check_device_errors(self) -> None:
         if self._err is not None and int(self._err.item()) != 0:
             self._err.zero_()
             _ne_range_check(torch.tensor([2.0]), self.from_logits)
+
+    @torch.inference_mode()
+    def compute(self) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
+        self._check_device_errors()
         if self.total_updates == 0:
             return self._empty_result()
         ce, ex, pos = self._window_totals()

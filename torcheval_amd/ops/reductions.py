@@ -53,5 +53,7 @@ def ne_sums(
         w = w.contiguous()
     out = torch.zeros(x.shape[0], 3, dtype=torch.float64, device=x.device)
     flag = err if err is not None else torch.zeros(1, dtype=torch.int32, device=x.device)
-    native().ne_sums(x, t, w, bool(from_logits), out, flag)
+    from torcheval_amd.config import config
+
+    native().ne_sums(x, t, w, bool(from_logits), out, flag, config.deterministic)
     return out, flag
