@@ -17,6 +17,9 @@ import torch.distributed as dist
 
 from torcheval_amd.config import trace_range
 from torcheval_amd.metrics.metric import Metric, TComputeReturn
+from datetime import timedelta
+
+from torcheval_amd.parallel.collectives import sync_timeout
 from torcheval_amd.parallel.distributed import PGWrapper
 from torcheval_amd.parallel.state_sync import (
     PendingSync,
@@ -33,18 +36,23 @@ _TMetrics = TypeVar("_TMetrics", bound=Iterable[Metric])
 def sync_and_compute(
     metric: Metric[TComputeReturn],
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> TComputeReturn:
-    """Sync metric states and return ``metric.compute()`` of the synced metric on all ranks."""
-    synced_metric = get_synced_metric(metric, process_group)
+    """Sync metric states and return ``metric.compute()`` of the synced metric on all ranks.
+    ``timeout`` bounds the sync's collectives (``TimeoutError`` instead of a hang)."""
+    synced_metric = get_synced_metric(metric, process_group, timeout=timeout)
     return synced_metric.compute()
 
 
 def sync_and_compute_collection(
     metrics: MutableMapping[str, Metric],
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> Dict[str, Any]:
     """Sync a dict of metrics (batched into one exchange) and compute each on all ranks."""
-    synced_metrics = get_synced_metric_collection(metrics, process_group)
+    synced_metrics = get_synced_metric_collection(metrics, process_group, timeout=timeout)
     return {key: m.compute() for key, m in synced_metrics.items()}
 
 
@@ -55,14 +63,18 @@ class SyncFuture:
     synced value(s).  Every rank must call ``wait``/``compute`` (it may run collectives).
     """
 
-    def __init__(self, pending: Optional[PendingSync], ready: Any, single: bool) -> None:
+    def __init__(
+        self, pending: Optional[PendingSync], ready: Any, single: bool, timeout: Optional[timedelta] = None
+    ) -> None:
         self._pending = pending
         self._ready = ready
         self._single = single
+        self._timeout = timeout
 
     def wait(self) -> Any:
         if self._ready is None:
-            out = self._pending.finish()
+            with sync_timeout(self._timeout):
+                out = self._pending.finish()
             self._ready = out["_"] if self._single else out
             self._pending = None
         return self._ready
@@ -77,6 +89,8 @@ class SyncFuture:
 def get_synced_metric_async(
     metric: Union[Metric, MutableMapping[str, Metric]],
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> SyncFuture:
     """Start syncing ``metric`` (or a dict of metrics) and return immediately.
 
@@ -90,34 +104,40 @@ def get_synced_metric_async(
     if world_size == 1:
         return SyncFuture(None, clone_metric(metric) if single else {k: clone_metric(m) for k, m in metric.items()}, single)
     coll = {"_": metric} if single else metric
-    with trace_range("torcheval_amd.start_sync"):
+    with trace_range("torcheval_amd.start_sync"), sync_timeout(timeout):
         pending = start_sync_collection(coll, process_group if process_group else dist.group.WORLD, world_size)
-    return SyncFuture(pending, None, single)
+    return SyncFuture(pending, None, single, timeout)
 
 
 def sync_and_compute_async(
     metric: Union[Metric, MutableMapping[str, Metric]],
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> SyncFuture:
     """Asynchronous :func:`sync_and_compute`: ``sync_and_compute_async(m).compute()``."""
-    return get_synced_metric_async(metric, process_group)
+    return get_synced_metric_async(metric, process_group, timeout=timeout)
 
 
 def get_synced_state_dict(
     metric: Metric,
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> Dict[str, Any]:
     """Return the state dict of a metric after syncing on all ranks."""
-    synced_metric = get_synced_metric(metric, process_group)
+    synced_metric = get_synced_metric(metric, process_group, timeout=timeout)
     return synced_metric.state_dict() if synced_metric else {}
 
 
 def get_synced_state_dict_collection(
     metric_collection: MutableMapping[str, Metric],
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> Dict[str, Dict[str, Any]]:
     """Return the state dicts of a collection of metrics after syncing on all ranks."""
-    synced_metrics = get_synced_metric_collection(metric_collection, process_group)
+    synced_metrics = get_synced_metric_collection(metric_collection, process_group, timeout=timeout)
     return {key: metric.state_dict() for key, metric in synced_metrics.items()}
 
 
@@ -134,6 +154,8 @@ def clone_metrics(metrics: _TMetrics) -> List[Metric]:
 def get_synced_metric(
     metric: Metric,
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> Metric:
     """
     Return a metric object on all ranks whose state variables are merged across the ranks of
@@ -144,20 +166,22 @@ def get_synced_metric(
     _validate_rank_and_world_size(world_size)
     if world_size == 1:
         return metric
-    with trace_range("torcheval_amd.sync_metric"):
+    with trace_range("torcheval_amd.sync_metric"), sync_timeout(timeout):
         return sync_metric(metric, process_group if process_group else dist.group.WORLD, world_size)
 
 
 def get_synced_metric_collection(
     metric_collection: MutableMapping[str, Metric],
     process_group: Optional[dist.ProcessGroup] = None,
+    *,
+    timeout: Optional[timedelta] = None,
 ) -> Union[Dict[str, Metric], MutableMapping[str, Metric]]:
     """Return a dict of metrics whose states are synced across the ranks (one batched exchange)."""
     world_size = PGWrapper(process_group).get_world_size()
     _validate_rank_and_world_size(world_size)
     if world_size == 1:
         return metric_collection
-    with trace_range("torcheval_amd.sync_metric_collection"):
+    with trace_range("torcheval_amd.sync_metric_collection"), sync_timeout(timeout):
         return sync_metric_collection(
             metric_collection, process_group if process_group else dist.group.WORLD, world_size
         )

@@ -17,7 +17,10 @@ Replaces the reference's object-level sync (``dist.all_gather_object`` of whole 
   never leave HBM under RCCL; received tensors are zero-copy views into the gathered buffer.
 """
 
+import contextlib
+import contextvars
 import pickle
+from datetime import timedelta
 from collections import defaultdict
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -37,6 +40,40 @@ _REDUCE_OPS = {
 
 
 # ---------------------------------------------------------------------------- all-reduce
+
+# Per-call deadline for the metric-sync collectives; None = the process
+# group's own timeout.  Set through ``sync_timeout`` / the toolkit's ``timeout=`` argument.
+_SYNC_TIMEOUT: "contextvars.ContextVar[Optional[timedelta]]" = contextvars.ContextVar(
+    "torcheval_amd_sync_timeout", default=None
+)
+
+
+@contextlib.contextmanager
+def sync_timeout(timeout: Optional[timedelta]):
+    """Bound every metric-sync collective issued inside the block by ``timeout``."""
+    token = _SYNC_TIMEOUT.set(timeout)
+    try:
+        yield
+    finally:
+        _SYNC_TIMEOUT.reset(token)
+
+
+def current_sync_timeout() -> Optional[timedelta]:
+    return _SYNC_TIMEOUT.get()
+
+
+def _wait(work, timeout: Optional[timedelta] = None) -> None:
+    t = timeout if timeout is not None else _SYNC_TIMEOUT.get()
+    if t is None:
+        work.wait()
+        return
+    try:
+        ok = work.wait(t)
+    except RuntimeError as e:
+        raise TimeoutError(f"metric-state sync did not complete within {t}: {e}") from e
+    if ok is False:
+        raise TimeoutError(f"metric-state sync did not complete within {t}")
+
 class AllReduceHandle:
     """In-flight bucketed all-reduce; ``wait()`` returns the reduced tensors in input order."""
 
@@ -44,13 +81,14 @@ class AllReduceHandle:
         self._pending = pending
         self._n = n
         self._out: Optional[List[torch.Tensor]] = None
+        self._timeout = _SYNC_TIMEOUT.get()  # deadline captured at issue time
 
     def wait(self) -> List[torch.Tensor]:
         if self._out is not None:
             return self._out
         out: List[Optional[torch.Tensor]] = [None] * self._n
         for work, flat, is_bool, layout in self._pending:
-            work.wait()
+            _wait(work, self._timeout)
             if is_bool:
                 flat = flat.to(torch.bool)
             off = 0
@@ -264,10 +302,10 @@ def _all_gather_fixed(t: torch.Tensor, group, ws: int) -> torch.Tensor:
     """All-gather equal-size 1-D tensors into one flat [ws * n] tensor."""
     if backend_of(group) == "nccl":
         out = torch.empty(ws * t.numel(), dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(out, t, group=group)
+        _wait(dist.all_gather_into_tensor(out, t, group=group, async_op=True))
         return out
     outs = [torch.empty_like(t) for _ in range(ws)]
-    dist.all_gather(outs, t, group=group)
+    _wait(dist.all_gather(outs, t, group=group, async_op=True))
     return torch.cat(outs)
 
 
