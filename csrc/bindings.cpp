@@ -206,7 +206,8 @@ void binary_counts(const Tensor& input, const Tensor& target, const optional<Ten
 // targets or (class_mode) [n] labels; weight: optional [rows, n]; outputs float64 [rows].
 void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
               const optional<Tensor>& weight, bool class_mode, const optional<Tensor>& out_auroc,
-              const optional<Tensor>& out_auprc) {
+              const optional<Tensor>& out_auprc, const optional<Tensor>& init,
+              const optional<Tensor>& out_raw) {
   check_gpu(sorted, "sorted");
   TORCH_CHECK(sorted.dim() == 2 && order.dim() == 2 && sorted.sizes() == order.sizes(),
               "auc_scan: sorted/order must be [rows, n]");
@@ -257,6 +258,16 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
   };
   a.out_auroc = f64_out(out_auroc, "out_auroc");
   a.out_auprc = f64_out(out_auprc, "out_auprc");
+  if (init.has_value()) {
+    TORCH_CHECK(init->scalar_type() == at::kDouble && init->is_contiguous() && init->numel() == 2 * rows,
+                "auc_scan: init must be contiguous float64 [rows, 2]");
+    a.init = init->data_ptr<double>();
+  }
+  if (out_raw.has_value()) {
+    TORCH_CHECK(out_raw->scalar_type() == at::kDouble && out_raw->is_contiguous() && out_raw->numel() == 4 * rows,
+                "auc_scan: out_raw must be contiguous float64 [rows, 4]");
+    a.out_raw = out_raw->data_ptr<double>();
+  }
   Tensor ws = at::empty({tea::auc_scan_workspace_bytes(rows, n)},
                         at::TensorOptions().dtype(at::kByte).device(sorted.device()));
   check_launch(tea::launch_auc_scan(a, ws.data_ptr(), stream_for(sorted)), "auc_scan");
@@ -619,7 +630,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("tn2") = py::none(), py::arg("fn2") = py::none());
   m.def("auc_scan", &auc_scan, "K3 tie-aware scan -> AUROC / AUPRC per row", py::arg("sorted"),
         py::arg("order"), py::arg("target"), py::arg("weight"), py::arg("class_mode"),
-        py::arg("out_auroc"), py::arg("out_auprc"));
+        py::arg("out_auroc"), py::arg("out_auprc"), py::arg("init") = py::none(),
+        py::arg("out_raw") = py::none());
   m.def("binned_counts", &binned_counts, "K4 binned TP/FP/FN per (threshold, class)",
         py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("mode"), py::arg("tp"),
         py::arg("fp"), py::arg("fn"));

@@ -77,6 +77,11 @@ struct AucScanArgs {
   int64_t n = 0;
   double* out_auroc = nullptr;  // [rows]
   double* out_auprc = nullptr;  // [rows]
+  // sample-sharded (distributed) mode: per-row (TP, FP) that precede this shard in the global
+  // descending order, and raw sums [rows, 4] = (roc sum, pr sum, local P, local N) instead of
+  // the normalised areas (the caller all-reduces them and normalises by the global P, N)
+  const double* init = nullptr;  // [rows, 2]
+  double* out_raw = nullptr;     // [rows, 4]
   // workspace carve-up (set by the launcher)
   void* ab = nullptr;
   void* tsum = nullptr;

@@ -138,7 +138,8 @@ __global__ __launch_bounds__(kT) void tile_scan_kernel(AucScanArgs a, int ntiles
   D2* ts = reinterpret_cast<D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
   D2* st = reinterpret_cast<D2*>(a.tstart) + static_cast<int64_t>(r) * ntiles;
   __shared__ D2 lds[kT / 64];
-  D2 carry{0.0, 0.0};
+  const D2 init = a.init ? D2{a.init[2 * r], a.init[2 * r + 1]} : D2{0.0, 0.0};
+  D2 carry = init;
   for (int b = 0; b < ntiles; b += kT) {
     const int t = b + threadIdx.x;
     const D2 v = t < ntiles ? ts[t] : D2{0.0, 0.0};
@@ -147,7 +148,8 @@ __global__ __launch_bounds__(kT) void tile_scan_kernel(AucScanArgs a, int ntiles
     if (t < ntiles) st[t] = d2add(carry, ex);
     carry = d2add(carry, tot);
   }
-  if (threadIdx.x == 0) reinterpret_cast<D2*>(a.totals)[r] = carry;
+  // totals are this shard's own P, N (the init offsets are excluded)
+  if (threadIdx.x == 0) reinterpret_cast<D2*>(a.totals)[r] = D2{carry.x - init.x, carry.y - init.y};
 }
 
 // sum of a/b over [lo, hi] (inclusive, hi may be < lo -> empty) of row r, block-cooperative
@@ -355,6 +357,12 @@ __global__ __launch_bounds__(kT) void finalize_kernel(AucScanArgs a, int ntiles)
   block_excl_scan(D2{roc, pr}, lds, tot);
   if (threadIdx.x == 0) {
     const D2 pn = reinterpret_cast<const D2*>(a.totals)[r];
+    if (a.out_raw) {
+      a.out_raw[4 * r] = tot.x;
+      a.out_raw[4 * r + 1] = tot.y;
+      a.out_raw[4 * r + 2] = pn.x;
+      a.out_raw[4 * r + 3] = pn.y;
+    }
     const double factor = pn.x * pn.y;
     if (a.out_auroc) a.out_auroc[r] = factor == 0.0 ? 0.5 : tot.x / factor;
     if (a.out_auprc) a.out_auprc[r] = pn.x == 0.0 ? 0.0 : tot.y / pn.x;

@@ -197,3 +197,20 @@ def test_tiled_transpose(n, c):
     out = torch.empty(c, n, device=DEV)
     native().transpose_f32(x, out)
     assert torch.equal(out, x.t().contiguous())
+
+
+@pytest.mark.parametrize("n,levels,weighted", [(5000, 0, False), (70_000, 37, True), (3000, 3, False)])
+def test_k3_shard_offsets_match_cpu(n, levels, weighted):
+    """K3 with (TP0, FP0) shard offsets + raw sums (the sample-sharded AUROC path) vs ATen."""
+    from torcheval_amd.metrics.functional.classification._curve import raw_area_sums
+
+    g = torch.Generator().manual_seed(n)
+    x = torch.rand(n, generator=g)
+    if levels:
+        x = (x * levels).floor() / levels
+    t = torch.randint(0, 2, (n,), generator=g)
+    w = torch.rand(n, generator=g, dtype=torch.float64) if weighted else None
+    for tp0, fp0 in [(0.0, 0.0), (123.0, 456.5)]:
+        want = raw_area_sums(x, t.float(), w, tp0, fp0)
+        got = raw_area_sums(x.cuda(), t.float().cuda(), None if w is None else w.cuda(), tp0, fp0)
+        torch.testing.assert_close(got.cpu(), want, rtol=1e-9, atol=1e-6)

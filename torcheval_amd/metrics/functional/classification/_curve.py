@@ -47,6 +47,34 @@ def _areas_from_points(tp: torch.Tensor, fp: torch.Tensor) -> Tuple[torch.Tensor
     return auroc, auprc
 
 
+def raw_area_sums(
+    x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor], tp0: float, fp0: float
+) -> torch.Tensor:
+    """Un-normalised sums of one 1-D shard whose samples all rank below (TP0, FP0) worth of
+    higher-scored samples held elsewhere: float64 [4] = (roc sum, pr sum, local P, local N)
+    with roc = sum_i b_i (TPs + TPe) / 2 and pr = sum_i a_i TPe / (TPe + FPe) in GLOBAL counts.
+    Summed over shards and divided by the global P * N (roc) or P (pr) they give AUROC / AUPRC.
+    ROCm tensors run K3 with shard offsets; CPU tensors the ATen form."""
+    if use_native(x) and t.is_cuda and x.numel() > 0:
+        from torcheval_amd.ops.sortscan import binary_auc_raw
+
+        return binary_auc_raw(x, t, w, tp0, fp0)
+    dev = x.device
+    if x.numel() == 0:
+        return torch.zeros(4, dtype=torch.float64, device=dev)
+    s, a, b = _sorted_ab(x.double() if x.dtype in (torch.float16, torch.bfloat16) else x, t, w)
+    ends = _group_ends(s)
+    tp = a.cumsum(-1)[ends] + tp0
+    fp = b.cumsum(-1)[ends] + fp0
+    tp_prev = torch.cat([tp.new_full((1,), tp0), tp[:-1]])
+    fp_prev = torch.cat([fp.new_full((1,), fp0), fp[:-1]])
+    roc = ((fp - fp_prev) * (tp + tp_prev)).sum() / 2
+    den = tp + fp
+    prec = torch.where(den > 0, tp / torch.where(den > 0, den, torch.ones_like(den)), torch.zeros_like(den))
+    pr = ((tp - tp_prev) * prec).sum()
+    return torch.stack([roc, pr, a.sum(), b.sum()]).to(torch.float64)
+
+
 def _sorted_ab(
     x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor]
 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:

@@ -72,3 +72,20 @@ def multiclass_auc(
     out_pr = torch.empty(rows, dtype=torch.float64, device=input.device) if pr else None
     native().auc_scan(s, idx, target, None, True, out_roc, out_pr)
     return out_roc, out_pr
+
+
+def binary_auc_raw(
+    input: torch.Tensor, target: torch.Tensor, weight: Optional[torch.Tensor], tp0: float, fp0: float
+) -> torch.Tensor:
+    """K3 over one 1-D shard with global (TP, FP) offsets: float64 [4] = (roc sum, pr sum,
+    local P, local N) - see ``_curve.raw_area_sums``."""
+    x = input.reshape(1, -1)
+    t = target.reshape(1, -1)
+    if t.dtype == torch.bool:
+        t = t.to(torch.uint8)
+    w = None if weight is None else weight.reshape(1, -1)
+    s, idx = _sort_rows(x)
+    init = torch.tensor([[tp0, fp0]], dtype=torch.float64, device=x.device)
+    raw = torch.empty(1, 4, dtype=torch.float64, device=x.device)
+    native().auc_scan(s, idx, t, w, False, None, None, init, raw)
+    return raw[0]

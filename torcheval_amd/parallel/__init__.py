@@ -3,6 +3,7 @@
 * ``distributed`` — process-group helpers (PGWrapper, init_from_env, transport device).
 * ``collectives`` — bucketed all-reduce and packed all-gather-v of metric states.
 * ``state_sync`` — typed metric-state sync engine used by ``metrics.toolkit``.
+* ``dist_auc`` — sample-sharded exact AUROC / AUPRC (splitter all-to-all + K3 shard offsets).
 """
 
 from torcheval_amd.parallel.collectives import (
@@ -31,4 +32,18 @@ __all__ = [
     "init_from_env",
     "packed_all_gather",
     "transport_device",
+    "distributed_binary_auroc",
+    "distributed_binary_auprc",
+    "distributed_binary_areas",
+    "sharded_compute",
 ]
+
+_LAZY = {"distributed_binary_auroc", "distributed_binary_auprc", "distributed_binary_areas", "sharded_compute"}
+
+
+def __getattr__(name):  # dist_auc imports the metric layer, which imports this package
+    if name in _LAZY:
+        from torcheval_amd.parallel import dist_auc
+
+        return getattr(dist_auc, name)
+    raise AttributeError(name)
