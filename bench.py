@@ -18,6 +18,7 @@ Rank 0 prints ONE JSON line.
 """
 
 import argparse
+from datetime import timedelta
 import json
 import os
 import time
@@ -99,6 +100,20 @@ def _sync_extras(dev: torch.device, world: int, barrier) -> dict:
     fid.update_activations(torch.randn(1000, 2048, device=dev, generator=g), True)
     fid.update_activations(torch.randn(1000, 2048, device=dev, generator=g), False)
     timed("fid_2048_state_sync", lambda: get_synced_metric(fid), 5)
+
+    # sharded alternatives (torcheval_amd.parallel): same results, no full replication
+    from torcheval_amd.metrics import MulticlassBinnedAUPRC
+    from torcheval_amd.parallel import class_sharded_compute, sharded_compute, sharded_confusion_matrix
+    from torcheval_amd.parallel.collectives import sync_timeout
+
+    with sync_timeout(timedelta(seconds=120)):
+        timed("binary_auroc_1M_per_rank_sample_sharded", lambda: sharded_compute(auroc), 5)
+        timed("confusion_matrix_1000_row_sharded", lambda: sharded_confusion_matrix(cm), 20)
+        ap = MulticlassBinnedAUPRC(num_classes=20000, threshold=200, average="macro", device=dev)
+        for s_ in (ap.num_tp, ap.num_fp, ap.num_fn):
+            s_.copy_(torch.randint(0, 1000, s_.shape, device=dev, generator=g).float())
+        timed("binned_auprc_C20000_T200_sync_and_compute", lambda: sync_and_compute(ap), 5)
+        timed("binned_auprc_C20000_T200_class_sharded", lambda: class_sharded_compute(ap), 5)
     return out
 
 

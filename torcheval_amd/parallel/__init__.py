@@ -3,6 +3,7 @@
 * ``distributed`` — process-group helpers (PGWrapper, init_from_env, transport device).
 * ``collectives`` — bucketed all-reduce and packed all-gather-v of metric states.
 * ``state_sync`` — typed metric-state sync engine used by ``metrics.toolkit``.
+* ``class_shard`` — class-dimension reduce-scatter sync (row-sharded confusion matrix, binned AUPRC).
 * ``dist_auc`` — sample-sharded exact AUROC / AUPRC (splitter all-to-all + K3 shard offsets).
 """
 
@@ -36,14 +37,25 @@ __all__ = [
     "distributed_binary_auprc",
     "distributed_binary_areas",
     "sharded_compute",
+    "class_sharded_compute",
+    "reduce_scatter_classes",
+    "sharded_confusion_matrix",
 ]
 
-_LAZY = {"distributed_binary_auroc", "distributed_binary_auprc", "distributed_binary_areas", "sharded_compute"}
+_LAZY = {
+    "distributed_binary_auroc": "dist_auc",
+    "distributed_binary_auprc": "dist_auc",
+    "distributed_binary_areas": "dist_auc",
+    "sharded_compute": "dist_auc",
+    "class_sharded_compute": "class_shard",
+    "reduce_scatter_classes": "class_shard",
+    "sharded_confusion_matrix": "class_shard",
+}
 
 
-def __getattr__(name):  # dist_auc imports the metric layer, which imports this package
+def __getattr__(name):  # these modules import the metric layer, which imports this package
     if name in _LAZY:
-        from torcheval_amd.parallel import dist_auc
+        import importlib
 
-        return getattr(dist_auc, name)
+        return getattr(importlib.import_module(f"torcheval_amd.parallel.{_LAZY[name]}"), name)
     raise AttributeError(name)

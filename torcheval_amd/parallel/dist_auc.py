@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from torcheval_amd.metrics.functional.classification._curve import raw_area_sums
+from torcheval_amd.parallel.collectives import _wait
 from torcheval_amd.parallel.distributed import transport_device
 
 __all__ = ["distributed_binary_auroc", "distributed_binary_auprc", "distributed_binary_areas"]
@@ -85,14 +86,15 @@ def distributed_binary_areas(
     order = torch.argsort(dest, stable=True)
     send_counts = torch.bincount(dest, minlength=ws)
     recv_counts = torch.empty_like(send_counts, device=tdev)
-    dist.all_to_all_single(recv_counts, send_counts.to(tdev), group=group)
+    _wait(dist.all_to_all_single(recv_counts, send_counts.to(tdev), group=group, async_op=True))
     send_splits = send_counts.tolist()
     recv_splits = recv_counts.cpu().tolist()
     total_recv = int(sum(recv_splits))
 
     def exchange(v: torch.Tensor) -> torch.Tensor:
         out = torch.empty(total_recv, dtype=v.dtype, device=tdev)
-        dist.all_to_all_single(out, v[order].contiguous().to(tdev), recv_splits, send_splits, group=group)
+        _wait(dist.all_to_all_single(out, v[order].contiguous().to(tdev), recv_splits, send_splits,
+                                     group=group, async_op=True))
         return out.to(dev)
 
     x_loc = exchange(input.to(torch.float32) if input.dtype in (torch.float16, torch.bfloat16) else input)
@@ -106,7 +108,7 @@ def distributed_binary_areas(
     tp0, fp0 = (float(v) for v in all_pn[:rank].sum(0)) if rank > 0 else (0.0, 0.0)
     raw = raw_area_sums(x_loc, t_loc, w_loc, tp0, fp0).to(tdev)
     sums = raw[:2].clone()
-    dist.all_reduce(sums, group=group)
+    _wait(dist.all_reduce(sums, group=group, async_op=True))
     P, N = all_pn.sum(0).tolist()
     roc, pr = sums.to(dev).unbind(0)
     return _normalise(roc, pr, torch.tensor(P, dtype=torch.float64, device=dev),
@@ -116,9 +118,9 @@ def distributed_binary_areas(
 def _all_gather_flat(v: torch.Tensor, ws: int, group) -> torch.Tensor:
     out = torch.empty(ws * v.numel(), dtype=v.dtype, device=v.device)
     if v.is_cuda:
-        dist.all_gather_into_tensor(out, v, group=group)  # one RCCL all-gather into a flat buffer
+        _wait(dist.all_gather_into_tensor(out, v, group=group, async_op=True))  # one flat RCCL all-gather
     else:
-        dist.all_gather(list(out.view(ws, -1).unbind(0)), v, group=group)
+        _wait(dist.all_gather(list(out.view(ws, -1).unbind(0)), v, group=group, async_op=True))
     return out
 
 
