@@ -148,6 +148,21 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         x, y = rand(B, C), randint(2, B, C)
         return lambda: F.topk_multilabel_accuracy(x, y, k=2)
 
+    def rr():
+        x, y = rand(B, C), randint(C, B)
+        return lambda: F.reciprocal_rank(x, y, k=10)
+
+    def hr():
+        x, y = rand(B, C), randint(C, B)
+        m = M.HitRate(k=10, device=dev)
+
+        def step():
+            m.update(x, y)
+            if len(m.scores) > 256:  # bound the sample list over long timing loops
+                m.scores.clear()
+
+        return step
+
     def ppl():
         V = 32000 if s >= 1 else 50
         x, y = torch.randn(4, n(1024), V, device=dev, generator=g), randint(V, 4, n(1024))
@@ -214,6 +229,8 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "MulticlassBinnedAUPRC(C=100,T=100).update N=100k": mc_binned_auprc_cls,
         "MultilabelAccuracy(hamming).update 8192x1000": ml_hamming,
         "topk_multilabel_accuracy 8192x1000": topk_ml,
+        "reciprocal_rank 8192x1000 k=10 (K10)": rr,
+        "HitRate(k=10).update 8192x1000 (K10)": hr,
         "perplexity (4,1024,32000)": ppl,
         "mean_squared_error 8192x1000": mse,
         "r2_score 8192x1000": r2,

@@ -161,6 +161,41 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
   check_launch(rc, "cls_counts");
 }
 
+// ---------------------------------------------------------------- K10 rank-of-target scores
+Tensor rank_scores(const Tensor& input, const Tensor& target, int64_t mode, int64_t k,
+                   const optional<Tensor>& err) {
+  check_gpu(input, "input");
+  check_gpu(target, "target");
+  TORCH_CHECK(input.dim() == 2 && target.dim() == 1 && input.size(0) == target.size(0),
+              "rank_scores: input [n, c] and target [n] expected");
+  TORCH_CHECK(mode == 0 || mode == 1, "rank_scores: mode must be 0 (hit) or 1 (reciprocal)");
+  TORCH_CHECK(input.size(1) < (int64_t(1) << 31), "rank_scores: too many columns");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(input.device());
+  Tensor in = input.stride(1) == 1 ? input : input.contiguous();
+  Tensor tg = target.contiguous();
+  tea::RankArgs a;
+  a.input = in.data_ptr();
+  a.in_dt = dt_of(in);
+  a.n = in.size(0);
+  a.c = in.size(1);
+  a.row_stride = in.stride(0);
+  a.target = tg.data_ptr();
+  a.tg_dt = dt_of(tg);
+  a.mode = static_cast<int>(mode);
+  a.k = static_cast<int>(k);
+  Tensor out = at::empty({a.n}, input.options().dtype(at::kFloat));
+  a.out = out.data_ptr<float>();
+  if (err.has_value()) {
+    TORCH_CHECK(err->scalar_type() == at::kInt && err->numel() >= 1 && err->device() == input.device(),
+                "rank_scores: err must be an int32 tensor on the input device");
+    a.err = err->data_ptr<int>();
+  }
+  const int rc = tea::launch_rank_scores(a, stream_for(input));
+  TORCH_CHECK(rc != -1, "rank_scores: unsupported input dtype ", input.scalar_type());
+  check_launch(rc, "rank_scores");
+  return out;
+}
+
 void binary_counts(const Tensor& input, const Tensor& target, const optional<Tensor>& weight,
                    double threshold, const optional<Tensor>& tp, const optional<Tensor>& fp,
                    const optional<Tensor>& tn, const optional<Tensor>& fn,
@@ -617,6 +652,8 @@ void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>&
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "torcheval_amd native ops: hand-written HIP/CDNA4 kernels for MI355X (gfx950)";
   m.attr("ARCH") = "gfx950";
+  m.def("rank_scores", &rank_scores, "K10 rank-of-target scores (hit rate / reciprocal rank)",
+        py::arg("input"), py::arg("target"), py::arg("mode"), py::arg("k"), py::arg("err") = py::none());
   m.def("cls_counts", &cls_counts, "K1 fused classification counts", py::arg("input"),
         py::arg("target"), py::arg("k"), py::arg("num_classes"), py::arg("micro_correct"),
         py::arg("micro_total"), py::arg("cls_correct"), py::arg("cls_label"),

@@ -54,6 +54,22 @@ struct BinaryCountsArgs {
 };
 int launch_binary_counts(const BinaryCountsArgs& a, hipStream_t stream);
 
+// ------------------------------------------------------------------ K10 rank-of-target scores
+struct RankArgs {
+  const void* input = nullptr;  // [n, c] scores, unit column stride
+  DType in_dt = DType::f32;
+  int64_t n = 0;
+  int64_t c = 0;
+  int64_t row_stride = 0;
+  const void* target = nullptr;  // [n] integer class index
+  DType tg_dt = DType::i64;
+  int mode = 0;  // 0: hit rate (rank < k), 1: reciprocal rank (0 beyond k when k > 0)
+  int k = 0;
+  float* out = nullptr;  // [n] float32 scores
+  int* err = nullptr;    // bit 0: target out of range (row scored NaN)
+};
+int launch_rank_scores(const RankArgs& a, hipStream_t stream);
+
 }  // namespace tea
 
 namespace tea {

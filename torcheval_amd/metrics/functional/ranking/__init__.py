@@ -101,21 +101,52 @@ def _rank_input_check(input: torch.Tensor, target: torch.Tensor) -> None:
         )
 
 
+def _native_rank_scores(input, target, mode: int, k: Optional[int], err: Optional[torch.Tensor]):
+    """K10 (one streaming pass, no [N, C] temporaries) when the tensors are on a ROCm device.
+    Out-of-range targets are recorded in ``err`` (class path: raised at ``compute()``) or, for
+    the functional call without ``err``, raised here when ``config.validate`` is on; otherwise
+    their rows score NaN."""
+    from torcheval_amd.config import config
+    from torcheval_amd.ops.ranking import native_rank, rank_scores
+
+    if not native_rank(input, target):
+        return None
+    own = err is None and config.validate
+    if own:
+        err = torch.zeros(1, dtype=torch.int32, device=input.device)
+    out = rank_scores(input, target, mode, k, err)
+    if own:
+        from torcheval_amd.metrics.classification.accuracy import _raise_on_device_error
+
+        _raise_on_device_error(err)
+    return out
+
+
 @torch.inference_mode()
-def hit_rate(input: torch.Tensor, target: torch.Tensor, *, k: Optional[int] = None) -> torch.Tensor:
+def hit_rate(
+    input: torch.Tensor, target: torch.Tensor, *, k: Optional[int] = None, _err: Optional[torch.Tensor] = None
+) -> torch.Tensor:
     """Per-sample 1.0 if the target is within the top-k scores.  Class: ``HitRate``."""
     _rank_input_check(input, target)
     if k is not None and k <= 0:
         raise ValueError(f"k should be None or positive, got {k}.")
     if k is None or k >= input.size(dim=-1):
         return input.new_ones(target.size())
+    out = _native_rank_scores(input, target, 0, k, _err)
+    if out is not None:
+        return out
     return (_rank_of_target(input, target) < k).float()
 
 
 @torch.inference_mode()
-def reciprocal_rank(input: torch.Tensor, target: torch.Tensor, *, k: Optional[int] = None) -> torch.Tensor:
+def reciprocal_rank(
+    input: torch.Tensor, target: torch.Tensor, *, k: Optional[int] = None, _err: Optional[torch.Tensor] = None
+) -> torch.Tensor:
     """Per-sample 1 / (rank of target + 1), 0 beyond top-k.  Class: ``ReciprocalRank``."""
     _rank_input_check(input, target)
+    out = _native_rank_scores(input, target, 1, k, _err)
+    if out is not None:
+        return out
     rank = _rank_of_target(input, target)
     score = torch.reciprocal(rank + 1.0)
     if k is not None:

@@ -79,21 +79,44 @@ class _ScoreList(Metric[torch.Tensor]):
             self.scores = [torch.cat(self.scores)]
 
 
-class HitRate(_ScoreList):
+class _RankScoreList(_ScoreList):
+    """ROCm inputs run K10; out-of-range targets land in a device flag raised at ``compute()``."""
+
+    _err: Optional[torch.Tensor] = None
+
+    def _err_for(self, input: torch.Tensor) -> Optional[torch.Tensor]:
+        if not input.is_cuda:
+            return None
+        if self._err is None or self._err.device != input.device:
+            self._err = torch.zeros(1, dtype=torch.int32, device=input.device)
+        return self._err
+
+    def _check_device_errors(self) -> None:
+        from torcheval_amd.metrics.classification.accuracy import _raise_on_device_error
+
+        _raise_on_device_error(self._err)
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        self._check_device_errors()
+        return super().compute()
+
+
+class HitRate(_RankScoreList):
     """Per-sample hit (target within top-k) scores, concatenated over updates."""
 
     @torch.inference_mode()
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "HitRate":
-        self.scores.append(hit_rate(input, target, k=self.k))
+        self.scores.append(hit_rate(input, target, k=self.k, _err=self._err_for(input)))
         return self
 
 
-class ReciprocalRank(_ScoreList):
+class ReciprocalRank(_RankScoreList):
     """Per-sample reciprocal rank scores, concatenated over updates."""
 
     @torch.inference_mode()
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "ReciprocalRank":
-        self.scores.append(reciprocal_rank(input, target, k=self.k))
+        self.scores.append(reciprocal_rank(input, target, k=self.k, _err=self._err_for(input)))
         return self
 
 
