@@ -242,7 +242,7 @@ void binary_counts(const Tensor& input, const Tensor& target, const optional<Ten
 void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
               const optional<Tensor>& weight, bool class_mode, const optional<Tensor>& out_auroc,
               const optional<Tensor>& out_auprc, const optional<Tensor>& init,
-              const optional<Tensor>& out_raw) {
+              const optional<Tensor>& out_raw, int64_t payload_kind) {
   check_gpu(sorted, "sorted");
   TORCH_CHECK(sorted.dim() == 2 && order.dim() == 2 && sorted.sizes() == order.sizes(),
               "auc_scan: sorted/order must be [rows, n]");
@@ -282,6 +282,9 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
     a.weight_stride = w.stride(0);
   }
   a.class_mode = class_mode ? 1 : 0;
+  TORCH_CHECK(payload_kind == 0 || (order.scalar_type() == at::kInt && !weight.has_value()),
+              "auc_scan: a payload order must be int32 and unweighted");
+  a.payload_kind = static_cast<int>(payload_kind);
   a.rows = rows;
   a.n = n;
   auto f64_out = [&](const optional<Tensor>& t, const char* name) -> double* {
@@ -584,7 +587,8 @@ void transpose_f32(const Tensor& x, const Tensor& out) {
 }
 
 // K3a: segmented descending radix sort of f32 rows -> (sorted scores, int32 permutation)
-void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_order) {
+void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_order,
+               const optional<Tensor>& payload, int64_t payload_kind) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kFloat && x.stride(1) == 1,
               "sort_desc: x must be float32 [rows, n] with contiguous rows");
@@ -612,6 +616,30 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   a.dtotal = a.hist + a.rows * 256 * a.tiles;
   a.out_sorted = out_sorted.data_ptr<float>();
   a.out_order = out_order.data_ptr<int32_t>();
+  Tensor pl;
+  if (payload.has_value() && payload_kind != 0) {
+    TORCH_CHECK(payload_kind == 1 || payload_kind == 2, "sort_desc: payload_kind must be 0, 1 or 2");
+    pl = *payload;
+    TORCH_CHECK(pl.device() == x.device(), "sort_desc: payload on another device");
+    // [n] (shared by every row) or [rows, n], unit stride along samples
+    if (pl.dim() == 1) {
+      TORCH_CHECK(pl.size(0) == a.n, "sort_desc: payload must have n samples");
+      if (!pl.is_contiguous()) pl = pl.contiguous();
+      a.payload_row_stride = 0;
+    } else {
+      TORCH_CHECK(pl.dim() == 2 && pl.size(0) == a.rows && pl.size(1) == a.n, "sort_desc: payload must be [rows, n]");
+      if (pl.stride(1) != 1) pl = pl.contiguous();
+      a.payload_row_stride = pl.stride(0);
+    }
+    const auto st = pl.scalar_type();
+    TORCH_CHECK(payload_kind == 1 ? (st == at::kFloat || st == at::kLong || st == at::kInt || st == at::kByte ||
+                                     st == at::kBool)
+                                  : (st == at::kLong || st == at::kInt),
+                "sort_desc: unsupported payload dtype ", st);
+    a.payload_kind = static_cast<int>(payload_kind);
+    a.payload = pl.data_ptr();
+    a.payload_dt = dt_of(pl);
+  }
   check_launch(tea::launch_radix_sort_desc(a, stream_for(x)), "sort_desc");
 }
 
@@ -668,7 +696,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("auc_scan", &auc_scan, "K3 tie-aware scan -> AUROC / AUPRC per row", py::arg("sorted"),
         py::arg("order"), py::arg("target"), py::arg("weight"), py::arg("class_mode"),
         py::arg("out_auroc"), py::arg("out_auprc"), py::arg("init") = py::none(),
-        py::arg("out_raw") = py::none());
+        py::arg("out_raw") = py::none(), py::arg("payload_kind") = 0);
   m.def("binned_counts", &binned_counts, "K4 binned TP/FP/FN per (threshold, class)",
         py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("mode"), py::arg("tp"),
         py::arg("fp"), py::arg("fn"));
@@ -687,7 +715,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("transpose_f32", &transpose_f32, "LDS-tiled [n, c] -> [c, n] float32 transpose", py::arg("x"),
         py::arg("out"));
   m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
-        py::arg("x"), py::arg("out_sorted"), py::arg("out_order"));
+        py::arg("x"), py::arg("out_sorted"), py::arg("out_order"), py::arg("payload") = py::none(),
+        py::arg("payload_kind") = 0);
   m.def("binned_finalize", &binned_finalize, "binned AUROC / AUPRC from counts", py::arg("tp"),
         py::arg("fp"), py::arg("fn") = py::none(), py::arg("out_auroc") = py::none(),
         py::arg("out_auprc") = py::none());

@@ -76,6 +76,7 @@ namespace tea {
 
 // ------------------------------------------------------------------ K3 sort-scan (AUROC/AUPRC)
 struct AucScanArgs {
+  int payload_kind = 0;  // 0: order = source index (gather); 1: order32 = f32 target bits; 2: order32 = class label
   const void* sorted = nullptr;  // [rows, n] scores sorted descending (f32 or f64)
   DType key_dt = DType::f32;
   int64_t key_stride = 0;
@@ -271,7 +272,14 @@ struct RadixArgs {
   uint32_t* hist = nullptr;   // [rows, tiles, 256]
   uint32_t* dtotal = nullptr; // [rows, 256]
   float* out_sorted = nullptr;  // [rows, n] descending
-  int32_t* out_order = nullptr; // [rows, n] source index within the row
+  int32_t* out_order = nullptr; // [rows, n] source index within the row (or the payload)
+  // optional payload carried instead of the source index (pass 0 reads it, coalesced):
+  //   1: f32 bits of payload[row * payload_row_stride + i]  (binary targets)
+  //   2: int32 of payload[row * payload_row_stride + i]     (class labels; row stride 0 = shared)
+  int payload_kind = 0;
+  const void* payload = nullptr;
+  DType payload_dt = DType::f32;
+  int64_t payload_row_stride = 0;
 };
 int64_t radix_sort_tiles(int64_t n);
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream);

@@ -65,6 +65,23 @@ __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
   return peers;
 }
 
+// pass-0 payload carried instead of the source index, converted per element from the
+// caller's dtype PT (compile-time, so the 16 up-front loads stay batched): KIND 1 -> f32 bits of
+// the value (binary targets), KIND 2 -> int32 of the value (class labels)
+template <typename PT, int KIND>
+__device__ __forceinline__ uint32_t first_payload(const RadixArgs& a, int64_t row, int64_t i) {
+  if constexpr (sizeof(PT) == 8) {
+    // int64 targets / labels: only the low dword is loaded (one VGPR per element, no 64-bit
+    // convert); binary targets and class labels both fit in int32
+    const int32_t lo = static_cast<const int32_t*>(a.payload)[2 * (row * a.payload_row_stride + i)];
+    if constexpr (KIND == 1) return __float_as_uint(static_cast<float>(lo));
+    return static_cast<uint32_t>(lo);
+  }
+  const PT x = static_cast<const PT*>(a.payload)[row * a.payload_row_stride + i];
+  if constexpr (KIND == 1) return __float_as_uint(static_cast<float>(x));
+  return static_cast<uint32_t>(static_cast<int32_t>(x));
+}
+
 // keys of this thread's 16 striped rounds, loaded up front so the loads overlap
 __device__ __forceinline__ void load_tile(const RadixArgs& a, const uint32_t* keys_in, const uint32_t* vals_in,
                                           int pass, int64_t row, int tile, uint32_t (&k)[kRounds],
@@ -77,7 +94,7 @@ __device__ __forceinline__ void load_tile(const RadixArgs& a, const uint32_t* ke
     v[j] = 0u;
     if (i < a.n) {
       k[j] = load_key(a, keys_in, pass, row, i);
-      if (want_vals) v[j] = pass == 0 ? static_cast<uint32_t>(i) : vals_in[row * a.n + i];
+      if (want_vals) v[j] = vals_in[row * a.n + i];
     }
   }
 }
@@ -148,6 +165,9 @@ __global__ __launch_bounds__(kRT) void radix_scan_kernel(RadixArgs a) {
 // Then: wave-ordered offsets + per-tile digit starts (one barrier), keys/values are placed in
 // LDS in sorted tile order, and written out with consecutive threads writing consecutive
 // addresses of each digit run (coalesced; v1 scattered 4-byte writes straight to HBM).
+// VMODE: 0 = values from the previous pass, 1 = source index (pass 0), 2 = caller payload of
+// dtype PT (pass 0); separate instantiations keep the payload conversion out of passes 1-3
+template <int VMODE, typename PT = uint32_t, int KIND = 0>
 __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const uint32_t* keys_in,
                                                               const uint32_t* vals_in, uint32_t* keys_out,
                                                               uint32_t* vals_out, int pass) {
@@ -173,7 +193,9 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     v[j] = 0u;
     if (i < a.n) {
       k[j] = load_key(a, keys_in, pass, row, i);
-      v[j] = pass == 0 ? static_cast<uint32_t>(i) : vals_in[row * a.n + i];
+      if constexpr (VMODE == 0) v[j] = vals_in[row * a.n + i];
+      else if constexpr (VMODE == 1) v[j] = static_cast<uint32_t>(i);
+      else v[j] = first_payload<PT, KIND>(a, row, i);
     }
   }
 #pragma unroll
@@ -296,7 +318,28 @@ int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
   for (int p = 0; p < 4; ++p) {
     hipLaunchKernelGGL(radix_upsweep_kernel, grid, dim3(kRT), 0, stream, a, kin[p], p);
     hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins, static_cast<unsigned>(a.rows)), dim3(kRT), 0, stream, a);
-    hipLaunchKernelGGL(radix_downsweep_kernel, grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p);
+#define TEA_DOWNSWEEP(...) \
+  hipLaunchKernelGGL((radix_downsweep_kernel<__VA_ARGS__>), grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p)
+    if (p > 0) {
+      TEA_DOWNSWEEP(0);
+    } else if (a.payload_kind == 0) {
+      TEA_DOWNSWEEP(1);
+    } else if (a.payload_kind == 1) {
+      switch (a.payload_dt) {
+        case DType::f32: TEA_DOWNSWEEP(2, float, 1); break;
+        case DType::i64: TEA_DOWNSWEEP(2, int64_t, 1); break;
+        case DType::i32: TEA_DOWNSWEEP(2, int32_t, 1); break;
+        case DType::u8: case DType::b8: TEA_DOWNSWEEP(2, uint8_t, 1); break;
+        default: return -2;
+      }
+    } else {
+      switch (a.payload_dt) {
+        case DType::i64: TEA_DOWNSWEEP(2, int64_t, 2); break;
+        case DType::i32: TEA_DOWNSWEEP(2, int32_t, 2); break;
+        default: return -2;
+      }
+    }
+#undef TEA_DOWNSWEEP
   }
   return static_cast<int>(hipGetLastError());
 }

@@ -90,6 +90,14 @@ __device__ __forceinline__ K key_at(const AucScanArgs& a, int r, int64_t i) {
 }
 
 __device__ __forceinline__ float2 sample_ab(const AucScanArgs& a, int r, int64_t i) {
+  if (a.payload_kind == 1) {  // unweighted binary: the sort carried the target itself
+    const float t = __uint_as_float(static_cast<uint32_t>(a.order32[r * a.order_stride + i]));
+    return make_float2(t, 1.f - t);
+  }
+  if (a.payload_kind == 2) {  // one-vs-rest: the sort carried the class label
+    const float t = a.order32[r * a.order_stride + i] == r ? 1.f : 0.f;
+    return make_float2(t, 1.f - t);
+  }
   const int64_t src = a.order32 ? static_cast<int64_t>(a.order32[r * a.order_stride + i])
                                 : a.order[r * a.order_stride + i];
   float t;

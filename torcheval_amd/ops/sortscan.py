@@ -11,8 +11,20 @@ import torch
 from torcheval_amd.ops import native
 
 
-def _sort_rows(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
-    """Descending per-row sort: K3a radix sort for f32 (int32 permutation); torch.sort for f64."""
+PAYLOAD_TARGET, PAYLOAD_LABEL = 1, 2
+_TARGET_PAYLOAD = (torch.float32, torch.int64, torch.int32, torch.uint8, torch.bool)
+
+
+def _sort_rows(
+    x: torch.Tensor, payload: Optional[torch.Tensor] = None, payload_kind: int = 0
+) -> Tuple[torch.Tensor, torch.Tensor, int]:
+    """Descending per-row sort -> (sorted, order, kind).
+
+    f32 runs the K3a radix sort.  With ``payload`` it carries the per-sample target
+    (``PAYLOAD_TARGET``: f32 value) or class label (``PAYLOAD_LABEL``: int32; a 1-D payload is
+    shared by every row) through the sort instead of the source index, so K3 reads targets in
+    sorted order without a random gather (``kind`` echoes what ``order`` holds).  f64 keys go
+    through torch.sort (int64 permutation, kind 0)."""
     if x.dtype not in (torch.float32, torch.float64):
         x = x.float()  # f16/bf16 -> f32 is exact and order preserving
     if x.dtype == torch.float32 and x.shape[-1] < 2**31:
@@ -20,10 +32,15 @@ def _sort_rows(x: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
             x = x.contiguous()
         s = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         idx = torch.empty(x.shape, dtype=torch.int32, device=x.device)
-        native().sort_desc(x, s, idx)
-        return s, idx
+        kind = payload_kind if payload is not None else 0
+        if kind == PAYLOAD_TARGET and payload.dtype not in _TARGET_PAYLOAD:
+            payload = payload.float()
+        elif kind == PAYLOAD_LABEL and payload.dtype not in (torch.int64, torch.int32):
+            payload = payload.long()
+        native().sort_desc(x, s, idx, payload, kind)
+        return s, idx, kind
     s, idx = torch.sort(x.contiguous(), dim=-1, descending=True)
-    return s, idx
+    return s, idx, 0
 
 
 def binary_auc(
@@ -42,11 +59,11 @@ def binary_auc(
         w = weight if weight.dim() == 2 else weight.unsqueeze(0)
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
-    s, idx = _sort_rows(x)
+    s, idx, kind = _sort_rows(x, t if w is None else None, PAYLOAD_TARGET)
     rows = s.shape[0]
     out_roc = torch.empty(rows, dtype=torch.float64, device=x.device) if roc else None
     out_pr = torch.empty(rows, dtype=torch.float64, device=x.device) if pr else None
-    native().auc_scan(s, idx, t, w, False, out_roc, out_pr)
+    native().auc_scan(s, idx, t, w, False, out_roc, out_pr, None, None, kind)
     return out_roc, out_pr
 
 
@@ -66,11 +83,11 @@ def multiclass_auc(
         native().transpose_f32(x, xt)  # LDS-tiled; torch's strided copy is ~10x slower here
     else:
         xt = x.t()
-    s, idx = _sort_rows(xt)
+    s, idx, kind = _sort_rows(xt, target, PAYLOAD_LABEL)
     rows = s.shape[0]
     out_roc = torch.empty(rows, dtype=torch.float64, device=input.device) if roc else None
     out_pr = torch.empty(rows, dtype=torch.float64, device=input.device) if pr else None
-    native().auc_scan(s, idx, target, None, True, out_roc, out_pr)
+    native().auc_scan(s, idx, target, None, True, out_roc, out_pr, None, None, kind)
     return out_roc, out_pr
 
 
@@ -84,8 +101,8 @@ def binary_auc_raw(
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
     w = None if weight is None else weight.reshape(1, -1)
-    s, idx = _sort_rows(x)
+    s, idx, kind = _sort_rows(x, t if w is None else None, PAYLOAD_TARGET)
     init = torch.tensor([[tp0, fp0]], dtype=torch.float64, device=x.device)
     raw = torch.empty(1, 4, dtype=torch.float64, device=x.device)
-    native().auc_scan(s, idx, t, w, False, None, None, init, raw)
+    native().auc_scan(s, idx, t, w, False, None, None, init, raw, kind)
     return raw[0]
