@@ -312,7 +312,7 @@ class TestBinned(MetricClassTester):
         thr = torch.cat([torch.zeros(1), x.flatten().unique(), torch.ones(1)]).unique()
         exact = binary_auroc(x.flatten(), t.flatten())
         auc, th = binary_binned_auroc(x.flatten(), t.flatten(), threshold=thr)
-        torch.testing.assert_close(auc.double(), exact, atol=1e-6, rtol=1e-6)
+        torch.testing.assert_close(auc.double(), exact.reshape(1), atol=1e-6, rtol=1e-6)
         self.run_class_implementation_tests(
             metric=BinaryBinnedAUROC(threshold=thr),
             state_names={"inputs", "targets"},

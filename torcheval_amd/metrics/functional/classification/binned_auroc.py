@@ -51,7 +51,8 @@ def _binary_binned_auroc_compute(
     t = target if target.ndim == 2 else target.unsqueeze(0)
     tp, fp, _ = binned_counts(x.t(), t.t(), threshold, 0)
     auroc = _binned_trapz(tp, fp)
-    return (auroc[0] if input.ndim == 1 else auroc), threshold
+    # the reference keeps the task dim even for 1-D input: shape [1] (binned_auroc.py:111-138)
+    return auroc, threshold
 
 
 def _binary_binned_auroc_param_check(num_tasks: int, threshold: torch.Tensor) -> None:
@@ -79,7 +80,7 @@ def _binary_binned_auroc_update_input_check(
             )
     elif len(input.shape) == 1 or input.shape[0] != num_tasks:
         raise ValueError(
-            f"`num_tasks = {num_tasks}`, `input`'s shape is expected to be ({num_tasks}, num_samples), but got shape {input.shape}."
+            f"`num_tasks = {num_tasks}`, `input`'s shape is expected to be ({num_tasks}, num_samples), but got shape ({input.shape})."
         )
 
 

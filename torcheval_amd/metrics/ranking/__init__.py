@@ -190,7 +190,7 @@ class RetrievalPrecision(Metric[torch.Tensor]):
                 elif self.empty_target_action == "skip":
                     rp.append(torch.tensor([torch.nan]))
                 elif self.empty_target_action == "err":
-                    raise ValueError(f"no positive value found in target={tgt}.")
+                    raise ValueError(f"no positive value found in target={tgt.float()}.")
             else:
                 rp.append(
                     retrieval_precision(self.topk[i], tgt, self.k, self.limit_k_to_size).reshape(-1).cpu()
