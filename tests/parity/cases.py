@@ -431,8 +431,11 @@ for mo in ("uniform_average", "raw_values"):
     _ccase(f"MeanSquaredError_{mo}", "MeanSquaredError", lambda mo=mo: {"multioutput": mo},
            lambda s: ((_randn(_g(s), B, 3), _randn(_g(s + 1), B, 3)), {"sample_weight": _rand(_g(s + 2), B)}))
     _ccase(f"WindowedMeanSquaredError_{mo}", "WindowedMeanSquaredError",
-           lambda mo=mo: {"multioutput": mo, "max_num_updates": 2},
-           lambda s: ((_randn(_g(s), B, 3), _randn(_g(s + 1), B, 3)), {}))
+           lambda mo=mo: {"multioutput": mo, "max_num_updates": 2, "num_tasks": 3},
+           lambda s: ((_randn(_g(s), B, 3), _randn(_g(s + 1), B, 3)), {"sample_weight": _rand(_g(s + 2), B)}))
+    _ccase(f"WindowedMeanSquaredError_1d_{mo}", "WindowedMeanSquaredError",
+           lambda mo=mo: {"multioutput": mo, "max_num_updates": 3},
+           lambda s: ((_randn(_g(s), B), _randn(_g(s + 1), B)), {}))
 for mo in ("uniform_average", "raw_values", "variance_weighted"):
     _ccase(f"R2Score_{mo}", "R2Score", lambda mo=mo: {"multioutput": mo, "num_regressors": 2},
            lambda s: ((_randn(_g(s), B, 3), _randn(_g(s + 1), B, 3)), {}))
@@ -447,6 +450,20 @@ _ccase("PeakSignalNoiseRatio_fixed", "PeakSignalNoiseRatio", lambda: {"data_rang
 # ranking
 _ccase("ClickThroughRate", "ClickThroughRate", lambda: {"num_tasks": T},
        lambda s: ((_randint(_g(s), 0, 2, T, B).float(), _rand(_g(s + 1), T, B)), {}))
+_ccase("WindowedClickThroughRate_no_lifetime", "WindowedClickThroughRate",
+       lambda: {"num_tasks": T, "max_num_updates": 3, "enable_lifetime": False},
+       lambda s: ((_randint(_g(s), 0, 2, T, B).float(), _rand(_g(s + 1), T, B)), {}))
+_ccase("WindowedWeightedCalibration_no_lifetime", "WindowedWeightedCalibration",
+       lambda: {"num_tasks": T, "max_num_updates": 3, "enable_lifetime": False},
+       lambda s: ((_rand(_g(s), T, B), _randint(_g(s + 1), 0, 2, T, B)), {}))
+_ccase("WindowedBinaryNormalizedEntropy_no_lifetime", "WindowedBinaryNormalizedEntropy",
+       lambda: {"max_num_updates": 2, "enable_lifetime": False},
+       lambda s: ((_rand(_g(s), B) * 0.9 + 0.05, _randint(_g(s + 1), 0, 2, B).float()), {}))
+_ccase("WindowedMeanSquaredError_no_lifetime", "WindowedMeanSquaredError",
+       lambda: {"max_num_updates": 5, "enable_lifetime": False},
+       lambda s: ((_randn(_g(s), B), _randn(_g(s + 1), B)), {}))
+_ccase("WindowedBinaryAUROC_small_window", "WindowedBinaryAUROC", lambda: {"max_num_samples": 30},
+       lambda s: ((_rand(_g(s), 20), _randint(_g(s + 1), 0, 2, 20)), {"weight": _rand(_g(s + 2), 20)}))
 _ccase("WindowedClickThroughRate", "WindowedClickThroughRate", lambda: {"num_tasks": T, "max_num_updates": 3},
        lambda s: ((_randint(_g(s), 0, 2, T, B).float(), _rand(_g(s + 1), T, B)), {}))
 _ccase("WeightedCalibration", "WeightedCalibration", lambda: {"num_tasks": T},

@@ -27,7 +27,7 @@ def binary_confusion_matrix(
     ``normalize`` in None | "none" | "true" | "pred" | "all".  Class: ``BinaryConfusionMatrix``."""
     _confusion_matrix_param_check(2, normalize)
     matrix = _binary_confusion_matrix_update(input, target, threshold)
-    return _confusion_matrix_compute(matrix, normalize)
+    return _functional_result(matrix, normalize)
 
 
 @torch.inference_mode()
@@ -42,6 +42,14 @@ def multiclass_confusion_matrix(
     Class version: ``MulticlassConfusionMatrix``."""
     _confusion_matrix_param_check(num_classes, normalize)
     cm = _confusion_matrix_update(input, target, num_classes)
+    return _functional_result(cm, normalize)
+
+
+def _functional_result(cm: torch.Tensor, normalize: Optional[str]) -> torch.Tensor:
+    """Un-normalised functional results are int64 counts as in the reference (its bincount /
+    sparse path); the K1 kernel accumulates exact integer-valued f32 counts."""
+    if normalize in (None, "none") and cm.is_floating_point():
+        return cm.long()
     return _confusion_matrix_compute(cm, normalize=normalize)
 
 

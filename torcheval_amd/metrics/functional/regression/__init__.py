@@ -125,9 +125,11 @@ def _r2_score_update(
         buf = torch.zeros(3 * d + 1, dtype=torch.float32, device=input.device)
         column_moments(input, target, None, stt=buf[:d], st=buf[d : 2 * d], sse=buf[2 * d : 3 * d],
                        sw=buf[3 * d :])
+        # the count is known on the host: a CPU int64 scalar as in the reference (r2_score.py:109)
+        n = torch.tensor(target.size(0))
         if input.ndim == 2:
-            return buf[:d], buf[d : 2 * d], buf[2 * d : 3 * d], buf[3 * d]
-        return buf[0], buf[1], buf[2], buf[3]
+            return buf[:d], buf[d : 2 * d], buf[2 * d : 3 * d], n
+        return buf[0], buf[1], buf[2], n
     return (
         torch.sum(torch.square(target), dim=0),
         torch.sum(target, dim=0),
