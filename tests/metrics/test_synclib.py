@@ -29,3 +29,66 @@ def test_sync_states_all_kinds():
             for t in out[r]["m1"]["l"]:
                 torch.testing.assert_close(t, torch.full((r + 1, 2), float(r)))
             torch.testing.assert_close(out[r]["m1"]["d"]["a"], torch.tensor(float(r)))
+
+
+def _sync_dtypes_shapes(rank, ws):
+    dtypes = [torch.int64, torch.bool, torch.float16, torch.bfloat16, torch.float64, torch.int32]
+    states = {
+        "m": {
+            # a different shape on every rank, every dtype
+            "t_%d" % i: (torch.arange((rank + 1) * 3) % 2).to(dt).reshape(rank + 1, 3)
+            for i, dt in enumerate(dtypes)
+        }
+    }
+    states["m"]["scalar"] = torch.tensor(rank, dtype=torch.int16)
+    order = metrics_traversal_order(states)
+    return sync_states(states, {"m": torch.device("cpu")}, order)
+
+
+def test_sync_mixed_dtypes_and_rank_dependent_shapes():
+    res = run_distributed(_sync_dtypes_shapes, 3)
+    dtypes = [torch.int64, torch.bool, torch.float16, torch.bfloat16, torch.float64, torch.int32]
+    for out in res:
+        for r in range(3):
+            for i, dt in enumerate(dtypes):
+                t = out[r]["m"]["t_%d" % i]
+                assert t.dtype == dt and t.shape == (r + 1, 3)
+                assert torch.equal(t, (torch.arange((r + 1) * 3) % 2).to(dt).reshape(r + 1, 3))
+            assert out[r]["m"]["scalar"].dtype == torch.int16 and int(out[r]["m"]["scalar"]) == r
+
+
+def _sync_all_empty(rank, ws):
+    states = {"m": {"l": [], "d": {}, "x": torch.empty(0)}}
+    return sync_states(states, {"m": torch.device("cpu")}, metrics_traversal_order(states))
+
+
+def test_sync_every_rank_empty():
+    for out in run_distributed(_sync_all_empty, 2):
+        for r in range(2):
+            assert out[r]["m"]["l"] == [] and dict(out[r]["m"]["d"]) == {}
+            assert out[r]["m"]["x"].numel() == 0
+
+
+def _sync_subgroup(rank, ws):
+    import torch.distributed as dist
+
+    group = dist.new_group([0, 1])  # every rank must take part in new_group
+    if rank > 1:
+        return None
+    states = {"m": {"t": torch.tensor([float(rank)])}}
+    return sync_states(states, {"m": torch.device("cpu")}, metrics_traversal_order(states), group)
+
+
+def test_sync_world_size_taken_from_process_group():
+    """Reference synclib.py:237 sizes the gather with the default group; here the group's."""
+    res = run_distributed(_sync_subgroup, 4)
+    for out in res[:2]:
+        assert len(out) == 2
+        for r in range(2):
+            torch.testing.assert_close(out[r]["m"]["t"], torch.tensor([float(r)]))
+    assert res[2] is None and res[3] is None
+
+
+def test_traversal_order_is_sorted_and_stable():
+    states = {"b": {"z": 1, "a": 2}, "a": {"y": 3}}
+    assert metrics_traversal_order(states) == [("a", "y"), ("b", "a"), ("b", "z")]
