@@ -2,6 +2,8 @@
 20 dispatches each (after warm-up), so per-kernel counter rows are easy to aggregate.
 
     rocprofv3 --pmc SQ_WAVE_CYCLES ... --kernel-trace --output-format csv -d DIR -- python3 benchmarks/pmc_targets.py
+
+``PMC_ONLY=<substring>`` restricts the run to matching workloads.
 """
 
 import os
@@ -45,6 +47,13 @@ def main() -> None:
     act = torch.randn(1000, 2048, device=dev, generator=g)
     fid = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=2048, device=dev)
     work.append(("K8 fid cov 1000x2048", lambda: fid.update_activations(act, True)))
+    xm = torch.rand(100_000, 100, device=dev, generator=g)
+    ym = torch.randint(0, 100, (100_000,), device=dev, generator=g)
+    mb = M.MulticlassBinnedAUPRC(num_classes=100, threshold=100, device=dev)
+    work.append(("K4 dense multiclass 100k x 100 T=100", lambda: mb.update(xm, ym)))
+    only = os.environ.get("PMC_ONLY")
+    if only:
+        work = [w for w in work if only in w[0]]
     for name, fn in work:
         for _ in range(3):
             fn()

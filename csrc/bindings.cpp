@@ -316,7 +316,7 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
 // thr: float32 [T] sorted; tp/fp/fn: float32 [T, c] views sharing strides (accumulated).
 void binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr, int64_t mode,
                    const optional<Tensor>& tp, const optional<Tensor>& fp,
-                   const optional<Tensor>& fn) {
+                   const optional<Tensor>& fn, int64_t uniform) {
   check_gpu(input, "input");
   TORCH_CHECK(input.dim() == 2, "binned_counts: input must be a 2-D view [n, c]");
   TORCH_CHECK(thr.dim() == 1 && thr.scalar_type() == at::kFloat && thr.is_contiguous(),
@@ -343,6 +343,7 @@ void binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr,
   a.tg_dt = dt_of(target);
   a.thr = thr.data_ptr<float>();
   a.T = static_cast<int>(thr.numel());
+  a.uniform = uniform != 0 && a.T >= 2;
   int64_t ks = -1, cs = -1;
   auto out = [&](const optional<Tensor>& t, const char* name) -> float* {
     if (!t.has_value()) return nullptr;
@@ -362,6 +363,8 @@ void binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr,
   a.out_c_stride = cs;
   a.ws = reinterpret_cast<unsigned*>(
       zeroed_workspace(input, stream_for(input), tea::binned_workspace_words(a.T, a.c) * 4, 1));
+  if (const int64_t sw = tea::binned_slab_words(a.T, a.c))
+    a.slab = reinterpret_cast<unsigned*>(zeroed_workspace(input, stream_for(input), sw * 4, 2));
   const int rc = tea::launch_binned(a, stream_for(input));
   TORCH_CHECK(rc != -1, "binned_counts: too many thresholds (", a.T, ") for the LDS histogram");
   check_launch(rc, "binned_counts");
@@ -646,7 +649,8 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
 
 // binned AUROC / AUPRC from [T, rows] float32 counts in one launch
 void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>& fn,
-                     const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc) {
+                     const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc,
+                     const optional<Tensor>& out_prec, const optional<Tensor>& out_rec) {
   check_gpu(tp, "tp");
   TORCH_CHECK(tp.dim() == 2 && tp.scalar_type() == at::kFloat && fp.sizes() == tp.sizes() &&
                   fp.strides() == tp.strides() && fp.scalar_type() == at::kFloat,
@@ -671,6 +675,19 @@ void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>&
     TORCH_CHECK(out_auroc->scalar_type() == at::kDouble && out_auroc->is_contiguous() &&
                     out_auroc->numel() == a.rows, "binned_finalize: out_auroc float64 [rows]");
     a.out_auroc = out_auroc->data_ptr<double>();
+  }
+  if (out_prec.has_value() || out_rec.has_value()) {
+    TORCH_CHECK(out_prec.has_value() && out_rec.has_value() && fn.has_value() &&
+                    fn->sizes() == tp.sizes() && fn->strides() == tp.strides() &&
+                    fn->scalar_type() == at::kFloat,
+                "binned_finalize: a curve needs fn like tp and both out_prec / out_rec");
+    for (const Tensor* o : {&*out_prec, &*out_rec})
+      TORCH_CHECK(o->scalar_type() == at::kFloat && o->is_contiguous() &&
+                      o->numel() == a.rows * (a.T + 1) && o->device() == tp.device(),
+                  "binned_finalize: curve outputs must be contiguous float32 [rows, T + 1]");
+    a.fn = fn->data_ptr<float>();
+    a.out_prec = out_prec->data_ptr<float>();
+    a.out_rec = out_rec->data_ptr<float>();
   }
   check_launch(tea::launch_binned_finalize(a, stream_for(tp)), "binned_finalize");
 }
@@ -699,7 +716,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_raw") = py::none(), py::arg("payload_kind") = 0);
   m.def("binned_counts", &binned_counts, "K4 binned TP/FP/FN per (threshold, class)",
         py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("mode"), py::arg("tp"),
-        py::arg("fp"), py::arg("fn"));
+        py::arg("fp"), py::arg("fn"), py::arg("uniform") = 0);
   m.def("column_moments", &column_moments, "K5 weighted column moments", py::arg("x"),
         py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),
         py::arg("sw"));
@@ -717,9 +734,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
         py::arg("x"), py::arg("out_sorted"), py::arg("out_order"), py::arg("payload") = py::none(),
         py::arg("payload_kind") = 0);
-  m.def("binned_finalize", &binned_finalize, "binned AUROC / AUPRC from counts", py::arg("tp"),
-        py::arg("fp"), py::arg("fn") = py::none(), py::arg("out_auroc") = py::none(),
-        py::arg("out_auprc") = py::none());
+  m.def("binned_finalize", &binned_finalize, "binned AUROC / AUPRC / PR-curve points from counts",
+        py::arg("tp"), py::arg("fp"), py::arg("fn") = py::none(), py::arg("out_auroc") = py::none(),
+        py::arg("out_auprc") = py::none(), py::arg("out_prec") = py::none(),
+        py::arg("out_rec") = py::none());
   m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
         py::arg("act"), py::arg("cov"), py::arg("colsum"));
   tea_register_runtime(m);

@@ -128,7 +128,9 @@ struct BinnedArgs {
   int64_t tg_col_stride = 0;
   const float* thr = nullptr;  // [T] sorted ascending
   int T = 0;
+  int uniform = 0;             // thr is exactly torch.linspace(0, 1, T) (host-known)
   unsigned* ws = nullptr;      // [16 replicas, T + 1, c, 2] u32, zero on entry, left zeroed
+  unsigned* slab = nullptr;    // dense path scratch [G, (T + 1) * c] u32, no zero contract
   float* tp = nullptr;         // outputs (accumulated): index k * out_k_stride + j * out_c_stride
   float* fp = nullptr;
   float* fn = nullptr;
@@ -136,6 +138,7 @@ struct BinnedArgs {
   int64_t out_c_stride = 0;
 };
 int64_t binned_workspace_words(int T, int64_t c);
+int64_t binned_slab_words(int T, int64_t c);  // 0 when the dense path is not used
 struct BinnedFinalizeArgs {
   const float* tp = nullptr;  // [T, rows] counts, element (k, r) at k * k_stride + r * r_stride
   const float* fp = nullptr;
@@ -145,6 +148,8 @@ struct BinnedFinalizeArgs {
   int64_t rows = 0;
   double* out_auroc = nullptr;  // [rows] float64 (reference: trapz(...).double())
   float* out_auprc = nullptr;   // [rows] float32
+  float* out_prec = nullptr;    // [rows, T + 1] float32 binned PR curve (precision, then 1)
+  float* out_rec = nullptr;     // [rows, T + 1] float32 (recall, then 0)
 };
 int launch_binned_finalize(const BinnedFinalizeArgs& a, hipStream_t stream);
 int launch_binned(const BinnedArgs& a, hipStream_t stream);

@@ -108,6 +108,63 @@ def test_k4_binned_counts(T, mode):
         torch.testing.assert_close(a.cpu(), b)
 
 
+@pytest.mark.parametrize("case", ["uniform_f32", "bf16_bool", "float_target", "edge_values", "slabs"])
+def test_k4_dense_path(case):
+    """[T+1] x C histograms that fit one block's LDS take the dense path (packed 16-bit
+    counters, slab flush + reduce); rows beyond 512 x 65535 elements split into row slabs."""
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    n, C, T, mode = 20000, 50, 101, 1
+    if case == "slabs":
+        n, C = 700_000, 50  # 35M elements -> 2 row slabs
+    x = torch.rand(n, C, generator=g)
+    thr = torch.linspace(0, 1, T)
+    if case == "edge_values":
+        x[:100] = float("nan")
+        x[100:200] = -0.5
+        x[200:300] = 1.5
+        x[300:400] = thr[37]  # exactly on a threshold
+        thr = torch.cat([torch.tensor([0.0]), torch.rand(T - 2, generator=g).sort().values, torch.tensor([1.0])])
+    t = torch.randint(0, C, (n,), generator=g)
+    if case in ("bf16_bool", "float_target"):
+        mode = 0
+        t = torch.randint(0, 2, (n, C), generator=g)
+        if case == "bf16_bool":
+            x = x.bfloat16()
+            t = t.bool()
+        else:
+            t = t.float()
+    exp = _binned_counts_aten(x.float() if x.dtype == torch.bfloat16 else x, t.long() if t.dtype == torch.bool else t,
+                              thr, mode)
+    got = binned_counts(x.to(DEV), t.to(DEV), thr.to(DEV), mode)
+    for a, b in zip(got, exp):
+        torch.testing.assert_close(a.cpu(), b)
+
+
+@pytest.mark.parametrize("T", [2, 3, 100, 201, 2000])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_k4_uniform_threshold_boundaries(T, mode):
+    """Int thresholds are the cached linspace: the kernels bin arithmetically and only verify
+    near a threshold.  Feed exact thresholds, their float neighbours and out-of-range / NaN
+    values, for both the dense and the (binary, small-T) sparse kernels."""
+    from torcheval_amd.metrics.functional.tensor_utils import _create_threshold_tensor
+
+    thr = _create_threshold_tensor(T, torch.device(DEV))
+    tc = thr.cpu()
+    vals = torch.cat([tc, torch.nextafter(tc, torch.tensor(2.0)), torch.nextafter(tc, torch.tensor(-1.0)),
+                      torch.tensor([0.0, 1.0, -0.0, -1e-30, 1e-30, 1.5, -3.0, float("nan"), float("inf")])])
+    g = torch.Generator().manual_seed(T + mode)
+    for C in (1, 3, 64):
+        n = vals.numel() * 4
+        x = vals[torch.randint(0, vals.numel(), (n, C), generator=g)]
+        t = torch.randint(0, C, (n,), generator=g) if mode == 1 else torch.randint(0, 2, (n, C), generator=g)
+        if mode == 1 and C == 1:
+            continue
+        exp = _binned_counts_aten(x, t, tc, mode)
+        got = binned_counts(x.to(DEV), t.to(DEV), thr, mode)
+        for a, b in zip(got, exp):
+            torch.testing.assert_close(a.cpu(), b)
+
+
 def test_binned_metrics_gpu_vs_cpu():
     g = torch.Generator().manual_seed(11)
     x = torch.rand(4, 3000, generator=g)

@@ -10,6 +10,13 @@ import torch
 # value so a freed tensor's id can never alias a validated one.
 _VALIDATED: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
 _LINSPACE: Dict[Tuple[int, str], torch.Tensor] = {}
+# the cached linspace(0, 1, n) tensors themselves: the K4 kernels may bin them arithmetically
+_UNIFORM: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDictionary()
+
+
+def _is_uniform_linspace(t: torch.Tensor) -> bool:
+    """True iff ``t`` is (the very tensor) ``linspace(0, 1, n)`` made from an int threshold."""
+    return _UNIFORM.get(id(t)) is t
 
 
 def _riemann_integral(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
@@ -34,6 +41,7 @@ def _create_threshold_tensor(
             _VALIDATED[id(t)] = t
             if threshold >= 2:
                 _ENDPOINTS_OK[id(t)] = t
+                _UNIFORM[id(t)] = t
         return t
     if isinstance(threshold, list):
         _check_host(threshold)

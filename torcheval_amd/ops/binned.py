@@ -21,7 +21,10 @@ def binned_counts(
     out: Optional[Tuple[torch.Tensor, torch.Tensor, torch.Tensor]] = None,
 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Accumulate into ``out`` ([T, C] float32 views) or return fresh counts."""
+    from torcheval_amd.metrics.functional.tensor_utils import _is_uniform_linspace
+
     T, C = thr.numel(), scores.shape[1]
+    uniform = _is_uniform_linspace(thr) and thr.dtype == torch.float32 and thr.device == scores.device
     thr = thr.to(device=scores.device)
     if out is None:
         buf = torch.zeros(3, T, C, dtype=torch.float32, device=scores.device)
@@ -30,7 +33,7 @@ def binned_counts(
         t = target
         if t.dtype == torch.bool:
             t = t.to(torch.uint8)
-        native().binned_counts(scores, t, thr.to(torch.float32).contiguous(), int(mode), *out)
+        native().binned_counts(scores, t, thr.to(torch.float32).contiguous(), int(mode), *out, uniform=int(uniform))
         return out
     tp, fp, fn = _binned_counts_aten(scores, target, thr, mode)
     out[0].add_(tp)
@@ -76,3 +79,13 @@ def binned_finalize(
     out_pr = torch.empty(rows, dtype=torch.float32, device=tp.device) if auprc else None
     native().binned_finalize(tp, fp, fn, out_roc, out_pr)
     return out_roc, out_pr
+
+
+def binned_curve(tp: torch.Tensor, fp: torch.Tensor, fn: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """One launch: float32 [R, T+1] precision (NaN -> 1, closed by 1) and recall (closed by 0)
+    from [T, R] counts - the binned PR-curve compute chain."""
+    T, rows = tp.shape
+    prec = torch.empty(rows, T + 1, dtype=torch.float32, device=tp.device)
+    rec = torch.empty(rows, T + 1, dtype=torch.float32, device=tp.device)
+    native().binned_finalize(tp, fp, fn, None, None, prec, rec)
+    return prec, rec
