@@ -28,9 +28,12 @@ namespace tea {
 
 namespace {
 
+#ifndef TEA_RADIX_ROUNDS
+#define TEA_RADIX_ROUNDS 8
+#endif
 constexpr int kRT = 256;
-constexpr int kRounds = 16;
-constexpr int kRTile = kRT * kRounds;  // 4096
+constexpr int kRounds = TEA_RADIX_ROUNDS;
+constexpr int kRTile = kRT * kRounds;  // 2048 keys per tile (8 rounds: 115 vs 132 us for a 1M binary_auroc over 16)
 constexpr int kBins = 256;
 constexpr int kRWaves = kRT / 64;
 
