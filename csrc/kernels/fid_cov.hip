@@ -29,7 +29,7 @@ namespace tea {
 namespace {
 
 constexpr int kTile = 64;
-constexpr int kBK = 32;
+constexpr int kBK = 32;  // rows per stage (64: 104 vs 78 us, 64 KB of LDS halves residency; hoisting the stage's LDS reads ahead of its MFMAs: 87 us)
 constexpr int kThreads = 256;
 constexpr int kPad = kTile + 1;
 constexpr int kStage = kBK * kTile;  // floats per operand per stage
