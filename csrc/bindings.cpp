@@ -376,7 +376,8 @@ void binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr,
 void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
                     const optional<Tensor>& w, const optional<Tensor>& sse,
                     const optional<Tensor>& st, const optional<Tensor>& stt,
-                    const optional<Tensor>& sx, const optional<Tensor>& sw) {
+                    const optional<Tensor>& sx, const optional<Tensor>& sw, int64_t overwrite,
+                    int64_t mse_mode, const optional<Tensor>& mse_out) {
   const Tensor& ref = x.has_value() ? *x : *t;
   check_gpu(ref, "x/t");
   TORCH_CHECK(ref.dim() == 2, "column_moments: inputs must be [n, d] views");
@@ -422,6 +423,20 @@ void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
   if (sw.has_value()) {
     TORCH_CHECK(sw->scalar_type() == at::kFloat && sw->numel() == 1, "column_moments: sw scalar f32");
     a.sw = sw->data_ptr<float>();
+  }
+  a.overwrite = overwrite != 0;
+  a.mse_mode = static_cast<int>(mse_mode);
+  Tensor raw_scratch;
+  if (a.mse_mode) {
+    TORCH_CHECK(a.overwrite && a.sse && mse_out.has_value() && mse_out->scalar_type() == at::kFloat &&
+                    mse_out->is_contiguous() && mse_out->device() == ref.device() &&
+                    mse_out->numel() == (a.mse_mode == 1 ? a.d : 1),
+                "column_moments: fused MSE needs overwrite, sse and a float32 mse_out of d (raw) or 1 elements");
+    a.mse_out = mse_out->data_ptr<float>();
+    if (a.mse_mode == 2) {
+      raw_scratch = at::empty({a.d}, ref.options().dtype(at::kFloat));
+      a.mse_part_f = raw_scratch.data_ptr<float>();
+    }
   }
   if (a.n == 0 || a.d == 0) return;
   a.ws_blocks = tea::column_moments_blocks(a.n, a.d);
@@ -717,9 +732,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("binned_counts", &binned_counts, "K4 binned TP/FP/FN per (threshold, class)",
         py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("mode"), py::arg("tp"),
         py::arg("fp"), py::arg("fn"), py::arg("uniform") = 0);
-  m.def("column_moments", &column_moments, "K5 weighted column moments", py::arg("x"),
-        py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),
-        py::arg("sw"));
+  m.def("column_moments", &column_moments, "K5 weighted column moments (+ fused MSE compute)",
+        py::arg("x"), py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"),
+        py::arg("sx"), py::arg("sw"), py::arg("overwrite") = 0, py::arg("mse_mode") = 0,
+        py::arg("mse_out") = py::none());
   m.def("ne_sums", &ne_sums, "K6 normalized-entropy row sums", py::arg("x"), py::arg("t"),
         py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"),
         py::arg("deterministic") = false);

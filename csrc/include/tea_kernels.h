@@ -178,6 +178,12 @@ struct MomentsArgs {
   int64_t out_stride = 1;
   double* ws = nullptr;  // [ws_blocks, n_requested_stats * d + 1] FP64 partials (caller-allocated)
   int ws_blocks = 0;
+  int overwrite = 0;     // 1: outputs are written (=), not accumulated (fresh functional buffers)
+  // fused mean_squared_error compute (functional path): 1 -> mse_out[d] raw values,
+  // 2 -> mse_out scalar uniform average; needs sse and sw
+  int mse_mode = 0;
+  float* mse_out = nullptr;
+  float* mse_part_f = nullptr;  // [d] raw values scratch (mode 2)
 };
 int column_moments_blocks(int64_t n, int64_t d);
 int launch_column_moments(const MomentsArgs& a, hipStream_t stream);

@@ -147,42 +147,84 @@ __global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
   }
 }
 
+// B) G partial groups x C columns per block: each thread sums P/G partials (independent loads,
+// unrolled), the groups fold through an LDS tree (v1 summed the 32 groups of all 5 stats in
+// ONE thread per column: a ~4 us serial tail), then one thread per column writes.  Every block
+// also folds the weight total, so the functional MSE compute (divide by the clamped signed
+// weight total, then the column mean via a deterministic last-block-done fold) happens here
+// instead of as ~6 ATen launches (the column mean is one more single-block launch: a
+// last-block-done fold would need an agent-scope release fence per block, which
+// tea_fold.h measured at +47 us for a 2048-block grid).
+constexpr int kFG = 32, kFC = kB / kFG;
+
+// mean of the d raw MSE values in a fixed order (per-thread strided sums + LDS tree)
+__global__ __launch_bounds__(kB) void mse_mean_kernel(const float* raw, int64_t d, float* out) {
+  __shared__ double lds[kB];
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < d; j += kB) s += raw[j];
+  lds[threadIdx.x] = s;
+  __syncthreads();
+  for (int h = kB / 2; h >= 1; h >>= 1) {
+    if (threadIdx.x < h) lds[threadIdx.x] += lds[threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = static_cast<float>(lds[0] / static_cast<double>(d));
+}
+
 __global__ __launch_bounds__(kB) void moments_finalize_kernel(MomentsArgs a, int P) {
-  constexpr int G = 32, C = kB / G;  // partial groups x columns per block (<= 8 partials each)
   const int64_t d = a.d;
-  const int c = threadIdx.x % C, grp = threadIdx.x / C;
-  const int64_t col = static_cast<int64_t>(blockIdx.x) * C + c;
+  const int c = threadIdx.x % kFC, grp = threadIdx.x / kFC;
+  const int64_t col = static_cast<int64_t>(blockIdx.x) * kFC + c;
   const Slots sl = slots_of(a);
   const int64_t stride = sl.n * d + 1;
-  __shared__ double lds[G][kStats + 1][C];
+  __shared__ double lds[kFG][kStats + 1][kFC];
   double s[kStats + 1] = {0, 0, 0, 0, 0};
 #pragma unroll 8
-  for (int p = grp; p < P; p += G) {  // independent loads: the unroll keeps 8 in flight
+  for (int p = grp; p < P; p += kFG) {  // independent loads: the unroll keeps 8 in flight
     const double* ws = a.ws + p * stride;
     if (col < d) {
 #pragma unroll
       for (int k = 0; k < kStats; ++k)
         if (sl.s[k] >= 0) s[k] += ws[sl.s[k] * d + col];
     }
-    if (blockIdx.x == 0 && c == 0) s[kStats] += ws[sl.n * d];
+    if (c == 0) s[kStats] += ws[sl.n * d];
   }
 #pragma unroll
   for (int k = 0; k <= kStats; ++k) lds[grp][k][c] = s[k];
   __syncthreads();
-  if (grp == 0) {
-    double t[kStats + 1];
 #pragma unroll
-    for (int k = 0; k <= kStats; ++k) {
-      t[k] = 0.0;
-      for (int g = 0; g < G; ++g) t[k] += lds[g][k][c];
+  for (int h = kFG / 2; h >= 1; h >>= 1) {  // fixed-order tree: deterministic
+    if (grp < h) {
+#pragma unroll
+      for (int k = 0; k <= kStats; ++k)
+        if (k == kStats ? c == 0 : sl.s[k] >= 0) lds[grp][k][c] += lds[grp + h][k][c];
     }
+    __syncthreads();
+  }
+  if (grp == 0) {
+    const double w_tot = lds[0][kStats][0];
     if (col < d) {
       float* outs[kStats] = {a.sse, a.st, a.stt, a.sx};
 #pragma unroll
-      for (int k = 0; k < kStats; ++k)
-        if (outs[k]) outs[k][col * a.out_stride] += static_cast<float>(t[k]);
+      for (int k = 0; k < kStats; ++k) {
+        if (!outs[k]) continue;
+        float& o = outs[k][col * a.out_stride];
+        o = a.overwrite ? static_cast<float>(lds[0][k][c]) : o + static_cast<float>(lds[0][k][c]);
+      }
+      if (a.mse_mode) {
+        // reference mean_squared_error.py:100-111 in float32: sse / (clamp(|sw|, eps) * sign(sw))
+        const float sse = a.sse[col * a.out_stride];
+        const float sw = a.sw ? (a.overwrite ? static_cast<float>(w_tot) : *a.sw + static_cast<float>(w_tot))
+                              : static_cast<float>(w_tot);
+        const float eps = 2.220446049250313e-16f;
+        const float sgn = sw > 0.f ? 1.f : (sw < 0.f ? -1.f : 0.f);
+        const float raw = sse / (fmaxf(fabsf(sw), eps) * sgn);
+        (a.mse_mode == 1 ? a.mse_out : a.mse_part_f)[col] = raw;
+      }
     }
-    if (blockIdx.x == 0 && c == 0 && a.sw) *a.sw += static_cast<float>(t[kStats]);
+    if (blockIdx.x == 0 && c == 0 && a.sw) {
+      *a.sw = a.overwrite ? static_cast<float>(w_tot) : *a.sw + static_cast<float>(w_tot);
+    }
   }
 }
 
@@ -254,6 +296,8 @@ int column_moments_blocks(int64_t n, int64_t d) {
   return static_cast<int>(p);
 }
 
+int column_moments_finalize_blocks(int64_t d) { return static_cast<int>((d + kFC - 1) / kFC); }
+
 int launch_column_moments(const MomentsArgs& a, hipStream_t stream) {
   if (a.n <= 0 || a.d <= 0) return 0;
   const int P = a.ws_blocks;
@@ -268,8 +312,10 @@ int launch_column_moments(const MomentsArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(moments_partial_kernel<4>, dim3(P, ct), dim3(kB), 0, stream, a);
   else
     hipLaunchKernelGGL(moments_partial_kernel<1>, dim3(P, ct), dim3(kB), 0, stream, a);
-  const unsigned fb = static_cast<unsigned>((a.d + 7) / 8);
+  const unsigned fb = static_cast<unsigned>(column_moments_finalize_blocks(a.d));
+  if (a.mse_mode && (!a.overwrite || !a.sse || (a.mse_mode == 2 && !a.mse_part_f))) return -2;
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(fb), dim3(kB), 0, stream, a, P);
+  if (a.mse_mode == 2) hipLaunchKernelGGL(mse_mean_kernel, dim3(1), dim3(kB), 0, stream, a.mse_part_f, a.d, a.mse_out);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -32,6 +32,11 @@ def mean_squared_error(
     """Mean squared error of ``[n]`` or ``[n, d]`` predictions (optionally sample-weighted);
     ``multioutput`` in uniform_average | raw_values.  Class: ``MeanSquaredError``."""
     _mean_squared_error_param_check(multioutput)
+    if _native(input, target, sample_weight):
+        _mean_squared_error_update_input_check(input, target, sample_weight)
+        from torcheval_amd.ops.reductions import mse_fused
+
+        return mse_fused(input, target, sample_weight, multioutput == "raw_values")
     sse, sum_weight = _mean_squared_error_update(input, target, sample_weight)
     return _mean_squared_error_compute(sse, multioutput, sum_weight)
 

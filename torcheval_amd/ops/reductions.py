@@ -24,15 +24,35 @@ def column_moments(
     stt: Optional[torch.Tensor] = None,
     sx: Optional[torch.Tensor] = None,
     sw: Optional[torch.Tensor] = None,
+    overwrite: bool = False,
 ) -> None:
-    """Accumulate weighted column moments of [n, d] (or [n]) x / t into float32 outputs."""
+    """Accumulate (or, with ``overwrite``, write) weighted column moments of [n, d] (or [n])
+    x / t into float32 outputs."""
     if x is not None and x.dim() == 1:
         x = x[:, None]
     if t is not None and t.dim() == 1:
         t = t[:, None]
     if t is not None and t.dtype == torch.bool:
         t = t.to(torch.uint8)
-    native().column_moments(x, t, w, sse, st, stt, sx, sw)
+    native().column_moments(x, t, w, sse, st, stt, sx, sw, int(overwrite))
+
+
+def mse_fused(
+    x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor], raw_values: bool
+) -> torch.Tensor:
+    """Functional mean_squared_error in two launches (+1 for the column mean): K5 partials,
+    then a finalize that also divides by the clamped signed weight total."""
+    d = x.shape[1] if x.dim() == 2 else 1
+    x2 = x[:, None] if x.dim() == 1 else x
+    t2 = t[:, None] if t.dim() == 1 else t
+    if t2.dtype == torch.bool:
+        t2 = t2.to(torch.uint8)
+    buf = torch.empty(d + 1, dtype=torch.float32, device=x.device)
+    out = torch.empty(d if raw_values else (), dtype=torch.float32, device=x.device)
+    native().column_moments(x2, t2, w, buf[:d], None, None, None, buf[d:], 1, 1 if raw_values else 2, out)
+    if raw_values and x.dim() == 1:
+        return out[0]  # [1] -> scalar, as sse.sum(dim=0) of a 1-D error is 0-d
+    return out
 
 
 def ne_sums(
