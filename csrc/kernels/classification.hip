@@ -159,7 +159,12 @@ __device__ __noinline__ int row_argmax_exact(const void* rp, int C, int lane) {
   return bi;
 }
 
-template <int KIND, int VEC, bool TOPK>
+// PRED = false: the caller needs only "was the prediction correct" (micro / macro accuracy:
+// no predicted-label histograms) and the row fits one chunk (C <= 1024 f32 / 2048 16-bit).
+// Then the wave compares the row max with the target's own score first: a row whose target is
+// not the max is incorrect without locating the argmax (the v2 index pass + min-reduce is only
+// run when they are equal, to apply torch.argmax's first-index rule to ties).
+template <int KIND, int VEC, bool TOPK, bool PRED = true>
 __global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
   const int lane = lane_id();
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
@@ -176,7 +181,44 @@ __global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
     const int64_t t = load_target(a.target, a.tg_dt, row);
     bool correct;
     int64_t pred = -1;
-    if constexpr (!TOPK) {
+    if constexpr (!TOPK && !PRED) {
+      const bool t_ok = t >= 0 && t < C;
+      float v[kChunkLoads][VEC];
+#pragma unroll
+      for (int u = 0; u < kChunkLoads; ++u) {
+        const int col = u * STEP + lane * VEC;
+        if (col < C) {
+          load_vec<KIND, VEC>(rp, col, v[u]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) v[u][e] = -__builtin_huge_valf();
+        }
+      }
+      const float xt = t_ok ? load_one<KIND>(rp, t) : 0.f;
+      float m = v[0][0];
+#pragma unroll
+      for (int u = 0; u < kChunkLoads; ++u)
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) m = fmaximum(m, v[u][e]);
+      float wm = m;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wm = fmaximum(wm, __shfl_xor(wm, o, kWave));
+      if (__builtin_expect(wm != wm, 0)) {  // NaN in the row: exact torch.argmax semantics
+        correct = row_argmax_exact<KIND>(rp, C, lane) == t;
+      } else if (!t_ok || xt != wm) {
+        correct = false;
+      } else {  // the target holds the max: correct iff no earlier column ties it
+        int idx = 0x7fffffff;
+#pragma unroll
+        for (int u = kChunkLoads - 1; u >= 0; --u)
+#pragma unroll
+          for (int e = VEC - 1; e >= 0; --e)
+            idx = (v[u][e] == wm) ? (u * STEP + lane * VEC + e) : idx;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) idx = min(idx, __shfl_xor(idx, o, kWave));
+        correct = idx == t;
+      }
+    } else if constexpr (!TOPK) {
       float bv = -__builtin_huge_valf();
       int bi = 0x7fffffff;
       bool saw_nan = false;
@@ -373,8 +415,13 @@ __global__ __launch_bounds__(kBlock) void binary_counts_kernel(BinaryCountsArgs 
 
 template <int KIND, int VEC>
 void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
+  constexpr int kChunkCols = kWave * VEC * kChunkLoads;
+  const bool pred_free = a.cls_pred == nullptr && a.cls_fp == nullptr && a.confusion == nullptr &&
+                         a.c <= kChunkCols;
   if (a.k > 1)
     hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, true>), dim3(grid), dim3(kBlock), 0, s, a);
+  else if (pred_free)
+    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, false, false>), dim3(grid), dim3(kBlock), 0, s, a);
   else
     hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, false>), dim3(grid), dim3(kBlock), 0, s, a);
 }

@@ -135,3 +135,40 @@ def test_micro_fold_accumulates_exactly(n, c):
     torch.cuda.synchronize()
     assert out[0].item() == 25 * exp
     assert out[1].item() == 25 * n
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("c", [33, 1000, 1024, 1025, 2048])
+def test_pred_free_accuracy_path(dtype, c):
+    """micro / macro accuracy need no predicted label: the kernel first compares the row max
+    with the target's score and only locates the argmax on a tie with it.  Rows here are ~85%
+    correct, with exact ties before / after the target, NaN, +-inf and -0 / +0."""
+    g = torch.Generator().manual_seed(c)
+    n = 6000
+    x = torch.randn(n, c, generator=g)
+    y = torch.randint(0, c, (n,), generator=g)
+    hit = torch.rand(n, generator=g) < 0.85
+    x[hit, y[hit]] = 10.0  # target is the max
+    r = torch.arange(n)
+    tie_before = r % 7 == 0
+    x[tie_before & (y > 0), 0] = x[tie_before & (y > 0), y[tie_before & (y > 0)]]  # earlier tie -> wrong
+    tie_after = r % 11 == 0
+    last = torch.full((n,), c - 1)
+    x[tie_after, last[tie_after]] = x[tie_after, y[tie_after]]  # later tie -> still right
+    x[r % 13 == 0, c // 2] = float("nan")
+    x[r % 17 == 0, 1] = float("inf")
+    z = r % 19 == 0
+    x[z] = 0.0
+    x[z, 0] = -0.0  # -0 and +0 tie: first index wins
+    x = x.to(dtype)
+    pred = _ref_argmax(x)
+    correct = pred == y
+    out = torch.zeros(2, device=DEV)
+    cc = torch.zeros(c, device=DEV)
+    cl = torch.zeros(c, device=DEV)
+    cls_counts(x.to(DEV), y.to(DEV), k=1, num_classes=c, micro_correct=out[0:1], micro_total=out[1:2],
+               cls_correct=cc, cls_label=cl)
+    torch.cuda.synchronize()
+    assert out[0].item() == correct.sum().item()
+    torch.testing.assert_close(cc.cpu(), torch.zeros(c).index_add_(0, y, correct.float()))
+    torch.testing.assert_close(cl.cpu(), torch.bincount(y, minlength=c).float())
