@@ -166,11 +166,15 @@ __global__ __launch_bounds__(kB) void ml_topk_kernel(MultilabelArgs a) {
   uint32_t mine = 0;
   for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWpb + wave_id(); row < a.n; row += nw) {
     const int64_t xo = row * a.x_row_stride, to = row * a.t_row_stride;
+    // scores AND targets are loaded up front, so the target loads overlap the score loads and
+    // the top-k selection (v1 loaded targets after the selection: their latency was exposed)
     uint32_t key[R];
+    float tv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t j = lane + static_cast<int64_t>(kWave) * r;
       key[r] = j < a.c ? order_key(ld_x<KIND>(a.x, xo + j)) : 0u;
+      tv[r] = j < a.c ? ld_t<TK>(a.t, to + j) : 0.f;
     }
     uint32_t sel = 0;
     for (int it = 0; it < a.k; ++it) {
@@ -191,8 +195,68 @@ __global__ __launch_bounds__(kB) void ml_topk_kernel(MultilabelArgs a) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int64_t j = lane + static_cast<int64_t>(kWave) * r;
-      if (j < a.c) f.add(((sel >> r) & 1u) ? 1.f : 0.f, ld_t<TK>(a.t, to + j));
+      if (j < a.c) f.add(((sel >> r) & 1u) ? 1.f : 0.f, tv[r]);
     }
+    const uint32_t res = row_correct(f, a.criteria);
+    if (lane == 0) mine += res;
+  }
+  block_fold(a, mine);
+}
+
+// vectorised top-k: a lane owns 4 consecutive columns per 256-column round (16-B score
+// loads, 2 x 16-B int64 target loads): 4x fewer memory instructions than the scalar layout,
+// which ran at 33 us for 8192 x 1000 against 17 us for the (vectorised) threshold mode
+template <int KIND, int TK, int RV>
+__global__ __launch_bounds__(kB) void ml_topk_vec_kernel(MultilabelArgs a) {
+  const int lane = lane_id();
+  const int64_t nw = static_cast<int64_t>(gridDim.x) * kWpb;
+  uint32_t mine = 0;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWpb + wave_id(); row < a.n; row += nw) {
+    const int64_t xo = row * a.x_row_stride, to = row * a.t_row_stride;
+    uint32_t key[RV][4];
+    float tv[RV][4];
+#pragma unroll
+    for (int r = 0; r < RV; ++r) {
+      const int64_t j = static_cast<int64_t>(r) * kWave * 4 + lane * 4;
+      if (j < a.c) {
+        float xv[4];
+        ld_x4<KIND>(a.x, xo + j, xv);
+        ld_t4<TK>(a.t, to + j, tv[r]);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) key[r][e] = order_key(xv[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          key[r][e] = 0u;
+          tv[r][e] = 0.f;
+        }
+      }
+    }
+    uint32_t sel = 0;
+    for (int it = 0; it < a.k; ++it) {
+      unsigned long long best = 0ull;
+#pragma unroll
+      for (int r = 0; r < RV; ++r)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const uint32_t j = static_cast<uint32_t>(r * kWave * 4 + lane * 4 + e);
+          if (!((sel >> (r * 4 + e)) & 1u) && j < a.c) {
+            const unsigned long long cand = (static_cast<unsigned long long>(key[r][e]) << 32) | (~j);
+            best = cand > best ? cand : best;
+          }
+        }
+      best = wave_max_u64(best);
+      const uint32_t win = ~static_cast<uint32_t>(best & 0xffffffffull);
+      if (static_cast<int>((win % (kWave * 4)) / 4) == lane) sel |= 1u << ((win / (kWave * 4)) * 4 + win % 4);
+    }
+    RowFlags f;
+#pragma unroll
+    for (int r = 0; r < RV; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int64_t j = static_cast<int64_t>(r) * kWave * 4 + lane * 4 + e;
+        if (j < a.c) f.add(((sel >> (r * 4 + e)) & 1u) ? 1.f : 0.f, tv[r][e]);
+      }
     const uint32_t res = row_correct(f, a.criteria);
     if (lane == 0) mine += res;
   }
@@ -201,6 +265,19 @@ __global__ __launch_bounds__(kB) void ml_topk_kernel(MultilabelArgs a) {
 
 template <int KIND, int TK>
 int launch_kinds(const MultilabelArgs& a, int grid, hipStream_t s) {
+  const int xes = KIND == 0 ? 4 : 2;
+  const int tes = TK == 0 ? 4 : TK == 1 ? 8 : TK == 2 ? 4 : 1;
+  const bool vec = a.c % 4 == 0 && a.x_row_stride % 4 == 0 && a.t_row_stride % 4 == 0 &&
+                   reinterpret_cast<uintptr_t>(a.x) % (4 * xes) == 0 &&
+                   reinterpret_cast<uintptr_t>(a.t) % (4 * tes < 16 ? 4 * tes : 16) == 0;
+  if (a.k > 0 && vec && a.c <= 8 * kWave * 4) {
+    const int64_t RV = (a.c + kWave * 4 - 1) / (kWave * 4);
+    if (RV <= 1) hipLaunchKernelGGL((ml_topk_vec_kernel<KIND, TK, 1>), dim3(grid), dim3(kB), 0, s, a);
+    else if (RV <= 2) hipLaunchKernelGGL((ml_topk_vec_kernel<KIND, TK, 2>), dim3(grid), dim3(kB), 0, s, a);
+    else if (RV <= 4) hipLaunchKernelGGL((ml_topk_vec_kernel<KIND, TK, 4>), dim3(grid), dim3(kB), 0, s, a);
+    else hipLaunchKernelGGL((ml_topk_vec_kernel<KIND, TK, 8>), dim3(grid), dim3(kB), 0, s, a);
+    return 0;
+  }
   if (a.k > 0) {
     const int64_t R = (a.c + kWave - 1) / kWave;
     if (R <= 4) hipLaunchKernelGGL((ml_topk_kernel<KIND, TK, 4>), dim3(grid), dim3(kB), 0, s, a);
@@ -210,11 +287,6 @@ int launch_kinds(const MultilabelArgs& a, int grid, hipStream_t s) {
     else return -2;
     return 0;
   }
-  const int xes = KIND == 0 ? 4 : 2;
-  const int tes = TK == 0 ? 4 : TK == 1 ? 8 : TK == 2 ? 4 : 1;
-  const bool vec = a.c % 4 == 0 && a.x_row_stride % 4 == 0 && a.t_row_stride % 4 == 0 &&
-                   reinterpret_cast<uintptr_t>(a.x) % (4 * xes) == 0 &&
-                   reinterpret_cast<uintptr_t>(a.t) % (4 * tes < 16 ? 4 * tes : 16) == 0;
   if (vec) hipLaunchKernelGGL((ml_threshold_kernel<KIND, TK, true>), dim3(grid), dim3(kB), 0, s, a);
   else hipLaunchKernelGGL((ml_threshold_kernel<KIND, TK, false>), dim3(grid), dim3(kB), 0, s, a);
   return 0;
