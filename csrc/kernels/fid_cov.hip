@@ -21,6 +21,10 @@
 //  * epilogue stages the tile in LDS (64 x 65, conflict-free for the transposed read) and
 //    read-modify-writes C[I, J] and the mirrored C[J, I] with coalesced rows; one block owns
 //    each output tile, so there are no atomics and the result is deterministic.
+//  * measured and rejected (MI355X, 1000 x 2048): in-block split-K with every wave computing
+//    the whole tile as 4 MFMA chains (2 x 2 register blocking, half the LDS operand reads):
+//    118 us - 176 VGPRs, and the waves still wait ~41% of their cycles on the per-stage
+//    operand fetch (SQ_WAIT_INST_ANY), so fewer LDS reads did not help; BK = 64: 104 us.
 #include "tea_common.h"
 #include "tea_kernels.h"
 
