@@ -24,7 +24,8 @@
 //  * measured and rejected (MI355X, 1000 x 2048): in-block split-K with every wave computing
 //    the whole tile as 4 MFMA chains (2 x 2 register blocking, half the LDS operand reads):
 //    118 us - 176 VGPRs, and the waves still wait ~41% of their cycles on the per-stage
-//    operand fetch (SQ_WAIT_INST_ANY), so fewer LDS reads did not help; BK = 64: 104 us.
+//    operand fetch (SQ_WAIT_INST_ANY), so fewer LDS reads did not help; BK = 64: 104 us;
+//    8 x 8 super-tile enumeration (per-XCD runs needing ~16 instead of ~34 panels): 86 us.
 #include "tea_common.h"
 #include "tea_kernels.h"
 
