@@ -377,7 +377,7 @@ void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
                     const optional<Tensor>& w, const optional<Tensor>& sse,
                     const optional<Tensor>& st, const optional<Tensor>& stt,
                     const optional<Tensor>& sx, const optional<Tensor>& sw, int64_t overwrite,
-                    int64_t mse_mode, const optional<Tensor>& mse_out) {
+                    int64_t mse_mode, const optional<Tensor>& mse_out, int64_t num_regressors) {
   const Tensor& ref = x.has_value() ? *x : *t;
   check_gpu(ref, "x/t");
   TORCH_CHECK(ref.dim() == 2, "column_moments: inputs must be [n, d] views");
@@ -428,13 +428,17 @@ void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
   a.mse_mode = static_cast<int>(mse_mode);
   Tensor raw_scratch;
   if (a.mse_mode) {
-    TORCH_CHECK(a.overwrite && a.sse && mse_out.has_value() && mse_out->scalar_type() == at::kFloat &&
-                    mse_out->is_contiguous() && mse_out->device() == ref.device() &&
-                    mse_out->numel() == (a.mse_mode == 1 ? a.d : 1),
-                "column_moments: fused MSE needs overwrite, sse and a float32 mse_out of d (raw) or 1 elements");
+    const bool raw = a.mse_mode == 1 || a.mse_mode == 3;
+    TORCH_CHECK(a.mse_mode >= 1 && a.mse_mode <= 5 && a.overwrite && a.sse && mse_out.has_value() &&
+                    mse_out->scalar_type() == at::kFloat && mse_out->is_contiguous() &&
+                    mse_out->device() == ref.device() && mse_out->numel() == (raw ? a.d : 1),
+                "column_moments: fused compute needs overwrite, sse and a float32 output of d (raw) or 1 elements");
+    TORCH_CHECK(a.mse_mode < 3 || (a.st && a.stt), "column_moments: fused R2 needs st and stt");
     a.mse_out = mse_out->data_ptr<float>();
-    if (a.mse_mode == 2) {
-      raw_scratch = at::empty({a.d}, ref.options().dtype(at::kFloat));
+    a.num_obs = a.n;
+    a.num_regressors = static_cast<int>(num_regressors);
+    if (!raw) {
+      raw_scratch = at::empty({2 * a.d}, ref.options().dtype(at::kFloat));
       a.mse_part_f = raw_scratch.data_ptr<float>();
     }
   }
@@ -735,7 +739,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("column_moments", &column_moments, "K5 weighted column moments (+ fused MSE compute)",
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"),
         py::arg("sx"), py::arg("sw"), py::arg("overwrite") = 0, py::arg("mse_mode") = 0,
-        py::arg("mse_out") = py::none());
+        py::arg("mse_out") = py::none(), py::arg("num_regressors") = 0);
   m.def("ne_sums", &ne_sums, "K6 normalized-entropy row sums", py::arg("x"), py::arg("t"),
         py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"),
         py::arg("deterministic") = false);

@@ -179,11 +179,15 @@ struct MomentsArgs {
   double* ws = nullptr;  // [ws_blocks, n_requested_stats * d + 1] FP64 partials (caller-allocated)
   int ws_blocks = 0;
   int overwrite = 0;     // 1: outputs are written (=), not accumulated (fresh functional buffers)
-  // fused mean_squared_error compute (functional path): 1 -> mse_out[d] raw values,
-  // 2 -> mse_out scalar uniform average; needs sse and sw
+  // fused functional compute (post-processing of the column sums inside the finalize):
+  //   1 MSE raw_values -> mse_out[d]       2 MSE uniform_average -> mse_out scalar (needs sse, sw)
+  //   3 R2 raw_values  -> mse_out[d]       4 R2 uniform_average, 5 R2 variance_weighted -> scalar
+  //   (R2 needs sse = RSS, st, stt; num_obs / num_regressors give tss and the adjusted score)
   int mse_mode = 0;
   float* mse_out = nullptr;
-  float* mse_part_f = nullptr;  // [d] raw values scratch (mode 2)
+  float* mse_part_f = nullptr;  // [2 d] scratch: per-column values (+ tss) for the scalar modes
+  int64_t num_obs = 0;
+  int num_regressors = 0;
 };
 int column_moments_blocks(int64_t n, int64_t d);
 int launch_column_moments(const MomentsArgs& a, hipStream_t stream);

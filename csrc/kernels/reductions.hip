@@ -155,20 +155,43 @@ __global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
 // instead of as ~6 ATen launches (the column mean is one more single-block launch: a
 // last-block-done fold would need an agent-scope release fence per block, which
 // tea_fold.h measured at +47 us for a 2048-block grid).
-constexpr int kFG = 32, kFC = kB / kFG;
+constexpr int kFG = 64, kFC = kB / kFG;  // 4 columns x 64 partial groups: 250 blocks at d = 1000 (32 x 8: 125)
 
-// mean of the d raw MSE values in a fixed order (per-thread strided sums + LDS tree)
-__global__ __launch_bounds__(kB) void mse_mean_kernel(const float* raw, int64_t d, float* out) {
-  __shared__ double lds[kB];
-  double s = 0.0;
-  for (int64_t j = threadIdx.x; j < d; j += kB) s += raw[j];
-  lds[threadIdx.x] = s;
+// final scalar of the fused functional computes, in a fixed order (per-thread strided sums +
+// LDS tree): MSE / R2 uniform mean (modes 2, 4), R2 variance-weighted sum (mode 5); then the
+// adjusted-R2 correction when num_regressors != 0
+__device__ __forceinline__ float adjust_r2(float r2, int64_t n, int k) {
+  // reference r2_score.py:_compute: 1 - (1 - r2) * (n - 1) / (n - k - 1) in float32
+  return 1.f - (1.f - r2) * static_cast<float>(n - 1) / static_cast<float>(n - k - 1);
+}
+
+__global__ __launch_bounds__(kB) void post_reduce_kernel(const float* vals, const float* tss, int64_t d, int mode,
+                                                          int64_t n, int k, float* out) {
+  __shared__ double lds[2][kB];
+  double s = 0.0, st = 0.0;
+  for (int64_t j = threadIdx.x; j < d; j += kB) {
+    if (mode == 5) {
+      s += static_cast<double>(vals[j]) * tss[j];
+      st += tss[j];
+    } else {
+      s += vals[j];
+    }
+  }
+  lds[0][threadIdx.x] = s;
+  lds[1][threadIdx.x] = st;
   __syncthreads();
   for (int h = kB / 2; h >= 1; h >>= 1) {
-    if (threadIdx.x < h) lds[threadIdx.x] += lds[threadIdx.x + h];
+    if (threadIdx.x < h) {
+      lds[0][threadIdx.x] += lds[0][threadIdx.x + h];
+      lds[1][threadIdx.x] += lds[1][threadIdx.x + h];
+    }
     __syncthreads();
   }
-  if (threadIdx.x == 0) *out = static_cast<float>(lds[0] / static_cast<double>(d));
+  if (threadIdx.x == 0) {
+    float r = mode == 5 ? static_cast<float>(lds[0][0] / lds[1][0]) : static_cast<float>(lds[0][0] / static_cast<double>(d));
+    if (mode >= 3 && k != 0) r = adjust_r2(r, n, k);
+    *out = r;
+  }
 }
 
 __global__ __launch_bounds__(kB) void moments_finalize_kernel(MomentsArgs a, int P) {
@@ -211,7 +234,7 @@ __global__ __launch_bounds__(kB) void moments_finalize_kernel(MomentsArgs a, int
         float& o = outs[k][col * a.out_stride];
         o = a.overwrite ? static_cast<float>(lds[0][k][c]) : o + static_cast<float>(lds[0][k][c]);
       }
-      if (a.mse_mode) {
+      if (a.mse_mode == 1 || a.mse_mode == 2) {
         // reference mean_squared_error.py:100-111 in float32: sse / (clamp(|sw|, eps) * sign(sw))
         const float sse = a.sse[col * a.out_stride];
         const float sw = a.sw ? (a.overwrite ? static_cast<float>(w_tot) : *a.sw + static_cast<float>(w_tot))
@@ -220,6 +243,18 @@ __global__ __launch_bounds__(kB) void moments_finalize_kernel(MomentsArgs a, int
         const float sgn = sw > 0.f ? 1.f : (sw < 0.f ? -1.f : 0.f);
         const float raw = sse / (fmaxf(fabsf(sw), eps) * sgn);
         (a.mse_mode == 1 ? a.mse_out : a.mse_part_f)[col] = raw;
+      } else if (a.mse_mode >= 3) {
+        // reference r2_score.py:_compute in float32: tss = stt - st^2 / n, r2 = 1 - rss / tss
+        const float rss = a.sse[col * a.out_stride], so = a.st[col * a.out_stride];
+        const float sso = a.stt[col * a.out_stride];
+        const float tss = sso - (so * so) / static_cast<float>(a.num_obs);
+        const float r2 = 1.f - rss / tss;
+        if (a.mse_mode == 3) {
+          a.mse_out[col] = a.num_regressors != 0 ? adjust_r2(r2, a.num_obs, a.num_regressors) : r2;
+        } else {
+          a.mse_part_f[col] = r2;
+          a.mse_part_f[d + col] = tss;
+        }
       }
     }
     if (blockIdx.x == 0 && c == 0 && a.sw) {
@@ -313,9 +348,13 @@ int launch_column_moments(const MomentsArgs& a, hipStream_t stream) {
   else
     hipLaunchKernelGGL(moments_partial_kernel<1>, dim3(P, ct), dim3(kB), 0, stream, a);
   const unsigned fb = static_cast<unsigned>(column_moments_finalize_blocks(a.d));
-  if (a.mse_mode && (!a.overwrite || !a.sse || (a.mse_mode == 2 && !a.mse_part_f))) return -2;
+  const bool scalar = a.mse_mode == 2 || a.mse_mode == 4 || a.mse_mode == 5;
+  if (a.mse_mode && (!a.overwrite || !a.sse || (scalar && !a.mse_part_f))) return -2;
+  if (a.mse_mode >= 3 && (!a.st || !a.stt)) return -2;
   hipLaunchKernelGGL(moments_finalize_kernel, dim3(fb), dim3(kB), 0, stream, a, P);
-  if (a.mse_mode == 2) hipLaunchKernelGGL(mse_mean_kernel, dim3(1), dim3(kB), 0, stream, a.mse_part_f, a.d, a.mse_out);
+  if (scalar)
+    hipLaunchKernelGGL(post_reduce_kernel, dim3(1), dim3(kB), 0, stream, a.mse_part_f, a.mse_part_f + a.d, a.d,
+                       a.mse_mode, a.num_obs, a.num_regressors, a.mse_out);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -55,6 +55,26 @@ def mse_fused(
     return out
 
 
+_R2_MODES = {"raw_values": 3, "uniform_average": 4, "variance_weighted": 5}
+
+
+def r2_fused(x: torch.Tensor, t: torch.Tensor, multioutput: str, num_regressors: int) -> torch.Tensor:
+    """Functional r2_score: K5 partials, then a finalize that forms tss, r2 (and the adjusted
+    score) per column, plus one single-block launch for the uniform / variance-weighted mean."""
+    d = x.shape[1] if x.dim() == 2 else 1
+    x2 = x[:, None] if x.dim() == 1 else x
+    t2 = t[:, None] if t.dim() == 1 else t
+    if t2.dtype == torch.bool:
+        t2 = t2.to(torch.uint8)
+    buf = torch.empty(3, d, dtype=torch.float32, device=x.device)
+    mode = _R2_MODES[multioutput]
+    out = torch.empty(d if mode == 3 else (), dtype=torch.float32, device=x.device)
+    native().column_moments(x2, t2, None, buf[0], buf[1], buf[2], None, None, 1, mode, out, int(num_regressors))
+    if mode == 3 and x.dim() == 1:
+        return out[0]
+    return out
+
+
 def ne_sums(
     input: torch.Tensor,
     target: torch.Tensor,
