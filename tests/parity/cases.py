@@ -678,3 +678,67 @@ _err("cls_ne_update", "cls", "BinaryNormalizedEntropy", lambda: ({"num_tasks": 2
 _err("cls_topk_ml_k", "cls", "TopKMultilabelAccuracy", lambda: ({"k": 1}, []))
 _err("cls_ctr_tasks", "cls", "ClickThroughRate", lambda: ({"num_tasks": 0}, []))
 _err("cls_hit_rate_k", "cls", "HitRate", lambda: ({"k": 0}, [((_x(4, 4), _y(4, 4)), {})]))
+
+
+# ----------------------------------------------------------------------------------------
+# empty inputs (0 samples): whatever the reference does - a value, NaN, or an exception - the
+# CPU paths and the HIP kernels (which must not launch a 0-sized grid) have to do the same
+# ----------------------------------------------------------------------------------------
+def _e(*shape):
+    return torch.zeros(*shape)
+
+
+def _ei(*shape):
+    return torch.zeros(*shape, dtype=torch.long)
+
+
+for _name, _fn, _b in [
+    ("binary_accuracy", "binary_accuracy", lambda: ((_e(0), _ei(0)), {})),
+    ("multiclass_accuracy", "multiclass_accuracy", lambda: ((_e(0, C), _ei(0)), {})),
+    ("multiclass_accuracy_macro", "multiclass_accuracy", lambda: ((_e(0, C), _ei(0)), {"average": "macro", "num_classes": C})),
+    ("multilabel_accuracy", "multilabel_accuracy", lambda: ((_e(0, L), _ei(0, L)), {})),
+    ("topk_multilabel_accuracy", "topk_multilabel_accuracy", lambda: ((_e(0, L), _ei(0, L)), {"k": 2})),
+    ("binary_precision", "binary_precision", lambda: ((_e(0), _ei(0)), {})),
+    ("binary_recall", "binary_recall", lambda: ((_e(0), _ei(0)), {})),
+    ("binary_f1_score", "binary_f1_score", lambda: ((_e(0), _ei(0)), {})),
+    ("multiclass_precision", "multiclass_precision", lambda: ((_e(0, C), _ei(0)), {"num_classes": C, "average": "macro"})),
+    ("multiclass_recall", "multiclass_recall", lambda: ((_e(0, C), _ei(0)), {"num_classes": C})),
+    ("multiclass_f1_score", "multiclass_f1_score", lambda: ((_e(0, C), _ei(0)), {"num_classes": C, "average": None})),
+    ("binary_confusion_matrix", "binary_confusion_matrix", lambda: ((_e(0), _ei(0)), {})),
+    ("multiclass_confusion_matrix", "multiclass_confusion_matrix", lambda: ((_e(0, C), _ei(0), C), {})),
+    ("binary_auroc", "binary_auroc", lambda: ((_e(0), _ei(0)), {})),
+    ("binary_auprc", "binary_auprc", lambda: ((_e(0), _ei(0)), {})),
+    ("multiclass_auroc", "multiclass_auroc", lambda: ((_e(0, C), _ei(0)), {"num_classes": C})),
+    ("multiclass_auprc", "multiclass_auprc", lambda: ((_e(0, C), _ei(0)), {"num_classes": C})),
+    ("binary_precision_recall_curve", "binary_precision_recall_curve", lambda: ((_e(0), _ei(0)), {})),
+    ("binary_binned_auroc", "binary_binned_auroc", lambda: ((_e(0), _ei(0)), {"threshold": 5})),
+    ("binary_binned_precision_recall_curve", "binary_binned_precision_recall_curve", lambda: ((_e(0), _ei(0)), {"threshold": 5})),
+    ("multiclass_binned_auprc", "multiclass_binned_auprc", lambda: ((_e(0, C), _ei(0)), {"num_classes": C, "threshold": 5})),
+    ("binary_normalized_entropy", "binary_normalized_entropy", lambda: ((_e(0), _e(0)), {})),
+    ("mean_squared_error", "mean_squared_error", lambda: ((_e(0), _e(0)), {})),
+    ("mean_squared_error_2d", "mean_squared_error", lambda: ((_e(0, 3), _e(0, 3)), {})),
+    ("r2_score", "r2_score", lambda: ((_e(0), _e(0)), {})),
+    ("perplexity", "perplexity", lambda: ((_e(0, 4, 7), _ei(0, 4)), {})),
+    ("hit_rate", "hit_rate", lambda: ((_e(0, C), _ei(0)), {"k": 2})),
+    ("reciprocal_rank", "reciprocal_rank", lambda: ((_e(0, C), _ei(0)), {})),
+    ("click_through_rate", "click_through_rate", lambda: ((_e(0),), {})),
+    ("weighted_calibration", "weighted_calibration", lambda: ((_e(0), _ei(0)), {})),
+    ("sum", "sum", lambda: ((_e(0),), {})),
+    ("mean", "mean", lambda: ((_e(0),), {})),
+]:
+    _err(f"empty_{_name}", "fn", _fn, _b)
+for _name, _cls, _b in [
+    ("MulticlassAccuracy", "MulticlassAccuracy", lambda: ({}, [((_e(0, C), _ei(0)), {})])),
+    ("MulticlassAccuracy_macro", "MulticlassAccuracy", lambda: ({"average": "macro", "num_classes": C}, [((_e(0, C), _ei(0)), {})])),
+    ("BinaryAccuracy", "BinaryAccuracy", lambda: ({}, [((_e(0), _ei(0)), {})])),
+    ("MultilabelAccuracy", "MultilabelAccuracy", lambda: ({}, [((_e(0, L), _ei(0, L)), {})])),
+    ("MulticlassConfusionMatrix", "MulticlassConfusionMatrix", lambda: ({"num_classes": C}, [((_e(0, C), _ei(0)), {})])),
+    ("MulticlassPrecision", "MulticlassPrecision", lambda: ({"num_classes": C, "average": None}, [((_e(0, C), _ei(0)), {})])),
+    ("BinaryBinnedAUPRC", "BinaryBinnedAUPRC", lambda: ({"threshold": 5}, [((_e(0), _ei(0)), {})])),
+    ("MulticlassBinnedAUPRC", "MulticlassBinnedAUPRC", lambda: ({"num_classes": C, "threshold": 5}, [((_e(0, C), _ei(0)), {})])),
+    ("MeanSquaredError", "MeanSquaredError", lambda: ({}, [((_e(0), _e(0)), {})])),
+    ("BinaryNormalizedEntropy", "BinaryNormalizedEntropy", lambda: ({}, [((_e(0), _e(0)), {})])),
+    ("Perplexity", "Perplexity", lambda: ({}, [((_e(0, 4, 7), _ei(0, 4)), {})])),
+    ("ClickThroughRate", "ClickThroughRate", lambda: ({}, [((_e(0),), {})])),
+]:
+    _err(f"empty_cls_{_name}", "cls", _cls, _b)

@@ -10,6 +10,8 @@ from typing import Optional
 
 import torch
 
+from torcheval_amd.metrics.functional.tensor_utils import _require_samples
+
 from torcheval_amd.metrics.functional.classification._curve import binary_areas, multiclass_areas
 
 
@@ -18,6 +20,7 @@ def binary_auprc(input: torch.Tensor, target: torch.Tensor, *, num_tasks: int = 
     """Area under the precision-recall curve of ``[n]`` / ``[num_tasks, n]`` data.
     Class version: ``BinaryAUPRC``."""
     _binary_auprc_update_input_check(input, target, num_tasks)
+    _require_samples(input.shape[-1] if input.ndim else 1, "binary_auprc")
     return _binary_auprc_compute(input, target, num_tasks)
 
 
@@ -35,6 +38,7 @@ def multiclass_auprc(
         num_classes = input.shape[1]
     _multiclass_auprc_param_check(num_classes, average)
     _multiclass_auprc_update_input_check(input, target, num_classes)
+    _require_samples(input.shape[0], "multiclass_auprc")
     return _multiclass_auprc_compute(input, target, average, num_classes)
 
 

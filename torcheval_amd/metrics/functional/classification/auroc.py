@@ -10,6 +10,8 @@ from typing import Optional
 
 import torch
 
+from torcheval_amd.metrics.functional.tensor_utils import _require_samples
+
 from torcheval_amd.metrics.functional.classification._curve import binary_areas, multiclass_areas
 
 
@@ -27,6 +29,7 @@ def binary_auroc(
     optional ``weight`` of the same shape.  Class version: ``BinaryAUROC``.
     """
     _binary_auroc_update_input_check(input, target, num_tasks, weight)
+    _require_samples(input.shape[-1] if input.ndim else 1, "binary_auroc")
     return _binary_auroc_compute(input, target, weight, use_fbgemm)
 
 
@@ -42,6 +45,7 @@ def multiclass_auroc(
     Class version: ``MulticlassAUROC``."""
     _multiclass_auroc_param_check(num_classes, average)
     _multiclass_auroc_update_input_check(input, target, num_classes)
+    _require_samples(input.shape[0], "multiclass_auroc")
     return _multiclass_auroc_compute(input, target, num_classes, average)
 
 

@@ -10,6 +10,8 @@ the reference's host-synchronising ``input.max()/min()``).
 from typing import Optional, Tuple
 
 import torch
+
+from torcheval_amd.metrics.functional.tensor_utils import _require_samples
 import torch.nn.functional as F
 
 from torcheval_amd.ops import use_native
@@ -46,6 +48,7 @@ def _binary_normalized_entropy_update(
 
     On the GPU path a range violation is recorded in ``err`` (int32[1]) when given (checked
     later by the caller); otherwise it is checked immediately (one sync)."""
+    _require_samples(input.numel(), "binary_normalized_entropy")
     _ne_shape_check(input, target, num_tasks, weight)
     if use_native(input) and target.is_cuda and (weight is None or weight.is_cuda):
         from torcheval_amd.ops.reductions import ne_sums

@@ -112,7 +112,8 @@ def _confusion_matrix_update(
 ) -> torch.Tensor:
     """Dense [C, C] counts.  GPU path validates on device: pass ``err`` (int32[1]) to collect
     the flag; without it the flag is checked here (one sync, like the reference's check)."""
-    if native_cls(input, target):
+    # an empty batch takes the checking path: the reference's torch.max check raises on it
+    if native_cls(input, target) and input.shape[0] > 0:
         _confusion_matrix_shape_check(input, target, num_classes)
         cm = torch.zeros(num_classes, num_classes, device=input.device)
         own_err = err is None

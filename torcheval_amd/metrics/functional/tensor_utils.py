@@ -85,3 +85,10 @@ def _threshold_check(threshold: torch.Tensor, endpoints: bool = False) -> None:
     _VALIDATED[id(threshold)] = threshold
     if endpoints:
         _ENDPOINTS_OK[id(threshold)] = threshold
+
+
+def _require_samples(n: int, name: str) -> None:
+    """The reference crashes inside TorchScript / ``torch.max`` on an empty input
+    (RuntimeError with an internal message); raise the same exception type, with a clear one."""
+    if n == 0:
+        raise RuntimeError(f"{name}: the input has no samples (the metric is undefined on an empty input).")
