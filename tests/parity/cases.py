@@ -742,3 +742,16 @@ for _name, _cls, _b in [
     ("ClickThroughRate", "ClickThroughRate", lambda: ({}, [((_e(0),), {})])),
 ]:
     _err(f"empty_cls_{_name}", "cls", _cls, _b)
+
+
+class _FlatFeatures(torch.nn.Module):
+    """FID feature-model stand-in (the default Inception-v3 needs torchvision weights): the
+    activations are the flattened images, so the covariance path sees real, varying data."""
+
+    def forward(self, x):
+        return x.flatten(1)
+
+
+_ccase("FrechetInceptionDistance", "FrechetInceptionDistance",
+       lambda: {"model": _FlatFeatures(), "feature_dim": 12},
+       lambda s: ((_randn(_g(s), 32, 3, 1, 4) * (1.0 + 0.5 * ((s // 10) % 2)), bool((s // 10) % 2 == 0)), {}))
