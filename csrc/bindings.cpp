@@ -628,14 +628,16 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   if (a.rows == 0 || a.n == 0) return;
   a.tiles = tea::radix_sort_tiles(a.n);
   const int64_t m = a.rows * a.n;
-  Tensor ws = at::empty({4 * m + a.rows * 256 * a.tiles + a.rows * 256}, x.options().dtype(at::kInt));
+  Tensor ws = at::empty({4 * m + a.rows * 256 * a.tiles}, x.options().dtype(at::kInt));
   uint32_t* base = reinterpret_cast<uint32_t*>(ws.data_ptr<int32_t>());
   a.keys0 = base;
   a.vals0 = base + m;
   a.keys1 = base + 2 * m;
   a.vals1 = base + 3 * m;
   a.hist = base + 4 * m;
-  a.dtotal = a.hist + a.rows * 256 * a.tiles;
+  a.ngroups = tea::radix_sort_groups(a.tiles);
+  Tensor groups = at::zeros({4 * a.rows * a.ngroups * 256}, x.options().dtype(at::kInt));
+  a.groups = reinterpret_cast<uint32_t*>(groups.data_ptr<int32_t>());
   a.out_sorted = out_sorted.data_ptr<float>();
   a.out_order = out_order.data_ptr<int32_t>();
   Tensor pl;

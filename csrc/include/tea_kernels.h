@@ -284,8 +284,9 @@ struct RadixArgs {
   uint32_t* vals0 = nullptr;
   uint32_t* keys1 = nullptr;
   uint32_t* vals1 = nullptr;
-  uint32_t* hist = nullptr;   // [rows, tiles, 256]
-  uint32_t* dtotal = nullptr; // [rows, 256]
+  uint32_t* hist = nullptr;   // [rows, tiles, 256] per-tile digit counts of the current pass
+  uint32_t* groups = nullptr; // [4 passes, rows, ngroups, 256] digit counts per group of tiles, zero on entry
+  int64_t ngroups = 0;        // radix_sort_groups(tiles)
   float* out_sorted = nullptr;  // [rows, n] descending
   int32_t* out_order = nullptr; // [rows, n] source index within the row (or the payload)
   // optional payload carried instead of the source index (pass 0 reads it, coalesced):
@@ -297,6 +298,7 @@ struct RadixArgs {
   int64_t payload_row_stride = 0;
 };
 int64_t radix_sort_tiles(int64_t n);
+int64_t radix_sort_groups(int64_t tiles);
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream);
 int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream);
 }  // namespace tea

@@ -9,10 +9,10 @@
 //     yields descending scores; the permutation payload is generated in the first pass (no
 //     iota kernel) and the last pass writes the scores back as floats;
 //   * 4 passes x 8 bits; each pass = upsweep (per-tile digit histogram, tile-major rows of
-//     1 KB) -> digit-parallel scan (grid = 256 digits x rows; each block scans one digit's
-//     counts across the row's tiles with one independent load per thread and emits the digit
-//     total) -> downsweep (each block re-scans the 256 digit totals in LDS for its bases, then
-//     a stable scatter).  Tiles are 4096 keys (256 threads x 16 striped rounds, coalesced);
+//     1 KB, plus one atomic per non-zero digit into the count of its group of kGroup tiles) ->
+//     downsweep (each block forms its digit bases from the <= ngroups group counts and the
+//     < kGroup tile counts before it in its group - no scan launch: v2 ran a digit-parallel scan
+//     kernel between the two, 4 launches and ~20 us per 1M-key sort - then a stable scatter).  Tiles are 4096 keys (256 threads x 16 striped rounds, coalesced);
 //     each thread loads all 16 of its keys up front so the loads overlap (v1 loaded per round
 //     and ran a single-block serial scan: ~60 us per pass at 1M).  Stable in-tile ranking uses wave64 "match" masks
 //     built from 8 ballots: each lane's rank among equal digits is popc(peers & lanes_below),
@@ -36,6 +36,7 @@ constexpr int kRounds = TEA_RADIX_ROUNDS;
 constexpr int kRTile = kRT * kRounds;  // 2048 keys per tile (8 rounds: 115 vs 132 us for a 1M binary_auroc over 16)
 constexpr int kBins = 256;
 constexpr int kRWaves = kRT / 64;
+constexpr int kGroup = 32;  // tiles per group count
 
 __device__ __forceinline__ uint32_t f2key_desc(float f) {
   uint32_t u = __float_as_uint(f);
@@ -127,41 +128,9 @@ __global__ __launch_bounds__(kRT) void radix_upsweep_kernel(RadixArgs a, const u
       atomicAdd(&h[d], static_cast<uint32_t>(__popcll(peers)));
   }
   __syncthreads();
-  a.hist[(row * a.tiles + tile) * kBins + threadIdx.x] = h[threadIdx.x];
-}
-
-// grid (digit, row): exclusive scan of one digit's counts over the row's tiles (in place) and
-// the digit total.  Threads own tiles, so every load is independent (no serial chains).
-__global__ __launch_bounds__(kRT) void radix_scan_kernel(RadixArgs a) {
-  const int d = blockIdx.x;
-  const int64_t row = blockIdx.y;
-  uint32_t* h = a.hist + row * a.tiles * kBins + d;
-  __shared__ uint32_t wsum[kRWaves];
-  const int lane = lane_id();
-  const int w = threadIdx.x >> 6;
-  uint32_t carry = 0;
-  for (int64_t t0 = 0; t0 < a.tiles; t0 += kRT) {
-    const int64_t t = t0 + threadIdx.x;
-    const uint32_t c = t < a.tiles ? h[t * kBins] : 0u;
-    uint32_t inc = c;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, 64);
-      if (lane >= o) inc += u;
-    }
-    if (lane == 63) wsum[w] = inc;
-    __syncthreads();
-    uint32_t off = carry, tot = 0;
-#pragma unroll
-    for (int q = 0; q < kRWaves; ++q) {
-      if (q < w) off += wsum[q];
-      tot += wsum[q];
-    }
-    if (t < a.tiles) h[t * kBins] = off + inc - c;
-    carry += tot;
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) a.dtotal[row * kBins + d] = carry;
+  const uint32_t c = h[threadIdx.x];
+  a.hist[(row * a.tiles + tile) * kBins + threadIdx.x] = c;
+  if (c) atomicAdd(&a.groups[((static_cast<int64_t>(pass) * a.rows + row) * a.ngroups + tile / kGroup) * kBins + threadIdx.x], c);
 }
 
 // Downsweep: wave w owns the contiguous sub-tile [w * 1024, (w + 1) * 1024) of the tile
@@ -205,8 +174,21 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
   }
 #pragma unroll
   for (int q = 0; q < kBins / 64; ++q) wc[w][lane + 64 * q] = 0;
-  {  // digit bases = exclusive scan of the row's digit totals + this tile's prefix in the digit
-    const uint32_t tot = a.dtotal[row * kBins + threadIdx.x];
+  {  // digit bases = exclusive scan of the row's digit totals + this tile's prefix in the digit:
+     // totals and the prefix of whole groups from the group counts, the rest from the tile
+     // counts of this tile's own group (all independent, L2-resident loads)
+    const uint32_t* G = a.groups + (static_cast<int64_t>(pass) * a.rows + row) * a.ngroups * kBins + threadIdx.x;
+    const int mg = tile / kGroup;
+    uint32_t tot = 0, pre = 0;
+#pragma unroll 8
+    for (int g = 0; g < a.ngroups; ++g) {
+      const uint32_t v = G[static_cast<int64_t>(g) * kBins];
+      tot += v;
+      pre += g < mg ? v : 0u;
+    }
+    const uint32_t* H = a.hist + row * a.tiles * kBins + threadIdx.x;
+#pragma unroll 8
+    for (int t2 = mg * kGroup; t2 < tile; ++t2) pre += H[static_cast<int64_t>(t2) * kBins];
     uint32_t inc = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -219,7 +201,7 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
 #pragma unroll
     for (int q = 0; q < kRWaves; ++q)
       if (q < w) off += wsum[q];
-    base[threadIdx.x] = off + inc - tot + a.hist[(row * a.tiles + tile) * kBins + threadIdx.x];
+    base[threadIdx.x] = off + inc - tot + pre;
   }
   // wave-local stable ranks (wave-private counters; a wave's LDS ops are in program order)
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -306,6 +288,8 @@ __global__ __launch_bounds__(kRT) void transpose_kernel(const float* in, int64_t
 
 int64_t radix_sort_tiles(int64_t n) { return (n + kRTile - 1) / kRTile; }
 
+int64_t radix_sort_groups(int64_t tiles) { return (tiles + kGroup - 1) / kGroup; }
+
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream) {
   if (n <= 0 || c <= 0) return 0;
   const dim3 grid(static_cast<unsigned>((n + 63) / 64), static_cast<unsigned>((c + 63) / 64));
@@ -322,7 +306,6 @@ int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
   uint32_t* vout[4] = {a.vals0, a.vals1, a.vals0, nullptr};
   for (int p = 0; p < 4; ++p) {
     hipLaunchKernelGGL(radix_upsweep_kernel, grid, dim3(kRT), 0, stream, a, kin[p], p);
-    hipLaunchKernelGGL(radix_scan_kernel, dim3(kBins, static_cast<unsigned>(a.rows)), dim3(kRT), 0, stream, a);
 #define TEA_DOWNSWEEP(...) \
   hipLaunchKernelGGL((radix_downsweep_kernel<__VA_ARGS__>), grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p)
     if (p > 0) {
