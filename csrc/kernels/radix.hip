@@ -180,15 +180,24 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     const uint32_t* G = a.groups + (static_cast<int64_t>(pass) * a.rows + row) * a.ngroups * kBins + threadIdx.x;
     const int mg = tile / kGroup;
     uint32_t tot = 0, pre = 0;
-#pragma unroll 8
-    for (int g = 0; g < a.ngroups; ++g) {
-      const uint32_t v = G[static_cast<int64_t>(g) * kBins];
-      tot += v;
-      pre += g < mg ? v : 0u;
+    // fixed-trip, fully unrolled chunks: every load of a chunk is in flight at once
+    for (int g0 = 0; g0 < a.ngroups; g0 += 16) {
+      uint32_t v[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = g0 + q < a.ngroups ? G[static_cast<int64_t>(g0 + q) * kBins] : 0u;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        tot += v[q];
+        pre += g0 + q < mg ? v[q] : 0u;
+      }
     }
-    const uint32_t* H = a.hist + row * a.tiles * kBins + threadIdx.x;
-#pragma unroll 8
-    for (int t2 = mg * kGroup; t2 < tile; ++t2) pre += H[static_cast<int64_t>(t2) * kBins];
+    const uint32_t* H = a.hist + (row * a.tiles + static_cast<int64_t>(mg) * kGroup) * kBins + threadIdx.x;
+    const int in_group = tile - mg * kGroup;  // tiles of this group before this one
+    uint32_t hv[kGroup];
+#pragma unroll
+    for (int q = 0; q < kGroup; ++q) hv[q] = q < in_group ? H[static_cast<int64_t>(q) * kBins] : 0u;
+#pragma unroll
+    for (int q = 0; q < kGroup; ++q) pre += hv[q];
     uint32_t inc = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
