@@ -110,25 +110,25 @@ __global__ __launch_bounds__(kRT) void radix_upsweep_kernel(RadixArgs a, const u
   const int64_t row = blockIdx.y;
   const int tile = blockIdx.x;
   const int shift = 8 * pass;
-  __shared__ uint32_t h[kBins];
-  h[threadIdx.x] = 0;
+  // wave-private LDS histograms fed by plain per-lane LDS atomics: counting needs no ranks, so
+  // the 8-ballot digit match of the downsweep is not needed here (equal digits in a wave only
+  // serialise inside the LDS atomic unit); the 4 wave copies are summed at the end
+  __shared__ uint32_t h[kRWaves][kBins];
+#pragma unroll
+  for (int q = 0; q < kRWaves; ++q) h[q][threadIdx.x] = 0;
   uint32_t k[kRounds], v[kRounds];
   load_tile(a, keys_in, nullptr, pass, row, tile, k, v, false);
   __syncthreads();
-  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
   const int64_t t0 = static_cast<int64_t>(tile) * kRTile + threadIdx.x;
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
-    const bool valid = t0 + j * kRT < a.n;
-    const uint64_t active = __ballot(valid);
-    if (active == 0ull) break;
-    const uint32_t d = (k[j] >> shift) & 0xffu;
-    const uint64_t peers = match_digit(d, active);
-    if (valid && (__ffsll(static_cast<long long>(peers)) - 1) == lane)
-      atomicAdd(&h[d], static_cast<uint32_t>(__popcll(peers)));
+    if (t0 + j * kRT < a.n) atomicAdd(&h[w][(k[j] >> shift) & 0xffu], 1u);
   }
   __syncthreads();
-  const uint32_t c = h[threadIdx.x];
+  uint32_t c = 0;
+#pragma unroll
+  for (int q = 0; q < kRWaves; ++q) c += h[q][threadIdx.x];
   a.hist[(row * a.tiles + tile) * kBins + threadIdx.x] = c;
   if (c) atomicAdd(&a.groups[((static_cast<int64_t>(pass) * a.rows + row) * a.ngroups + tile / kGroup) * kBins + threadIdx.x], c);
 }
