@@ -25,7 +25,8 @@ namespace tea {
 namespace {
 
 constexpr int kT = 256;              // threads per block
-constexpr int kPer = 4;              // samples per thread (1024-sample tiles: ~1000 blocks at 1M)
+constexpr int kPer = 4;              // samples per thread (1024-sample tiles: ~1000 blocks at 1M;
+                                     // measured: 512- and 2048-sample tiles are 5-6% slower end to end)
 constexpr int kTile = kT * kPer;     // samples per tile
 
 struct alignas(16) D2 {
