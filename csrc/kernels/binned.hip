@@ -253,7 +253,7 @@ template <bool XF32, bool YI64, int MODE, bool FAST, bool UNIFORM, bool TAIL>
 __device__ __forceinline__ void dense_round(const BinnedArgs& a, DenseWalk<typename DenseTypes<FAST>::Off>& w,
                                             const DenseStep<typename DenseTypes<FAST>::Off>& sp, uint32_t left,
                                             bool cf, float tm1, float margin, const float* s_thr,
-                                            unsigned* s_hist, int C) {
+                                            unsigned* s_hist, int C, uint32_t c0) {
   float x[kDU];
   bool pos[kDU];
   int cc[kDU];
@@ -261,7 +261,7 @@ __device__ __forceinline__ void dense_round(const BinnedArgs& a, DenseWalk<typen
   for (int u = 0; u < kDU; ++u) {
     const uint32_t c = cf ? w.mn : w.maj;
     cc[u] = static_cast<int>(c);
-    if (!TAIL || static_cast<uint32_t>(u) < left) dense_load<XF32, YI64, MODE, FAST>(a, w.ox, w.ot, c, x[u], pos[u]);
+    if (!TAIL || static_cast<uint32_t>(u) < left) dense_load<XF32, YI64, MODE, FAST>(a, w.ox, w.ot, c0 + c, x[u], pos[u]);
     w.mn += sp.dmin;
     w.maj += sp.dmaj;
     w.ox += sp.sx;
@@ -295,13 +295,17 @@ __device__ __forceinline__ void dense_round(const BinnedArgs& a, DenseWalk<typen
 // checks.  History at 100k x 100 classes, T=100 (MI355X): v4a per-element 64-bit div/mul and
 // branches 34 us (VALU-bound, ~68 VALU per element); incremental walker + templated mode 21.5 us.
 template <bool XF32, bool YI64, int MODE, bool FAST, bool UNIFORM>
-__global__ __launch_bounds__(kDB) void binned_hist_dense_kernel(BinnedArgs a, unsigned* slab) {
+__global__ __launch_bounds__(kDB) void binned_hist_dense_kernel(BinnedArgs a, unsigned* slab, int cb) {
+  // grid.y walks class chunks of cb classes: chunk y owns classes [c0, c0 + C) and its own
+  // [T+1][C] LDS histogram (v4 required the whole [T+1][classes] histogram in one block: more
+  // than 16k bins fell back to the sparse atomic-flush path, 0.6 TB/s at 1000 classes)
   using OffT = typename DenseTypes<FAST>::Off;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* s_thr = reinterpret_cast<float*>(smem);
   const int thr_bytes = ((a.T * 4 + 15) / 16) * 16;
   unsigned* s_hist = reinterpret_cast<unsigned*>(smem + thr_bytes);
-  const int C = static_cast<int>(a.c);
+  const uint32_t c0 = blockIdx.y * static_cast<uint32_t>(cb);
+  const int C = static_cast<int>(min(static_cast<int64_t>(cb), a.c - c0));
   const int W = (a.T + 1) * C;
   for (int k = threadIdx.x; k < a.T; k += kDB) s_thr[k] = a.thr[k];
   for (int k = threadIdx.x; k < W; k += kDB) s_hist[k] = 0u;
@@ -331,40 +335,51 @@ __global__ __launch_bounds__(kDB) void binned_hist_dense_kernel(BinnedArgs a, un
   DenseWalk<OffT> w;
   w.maj = e0 / sp.M;
   w.mn = e0 - w.maj * sp.M;
-  w.ox = static_cast<OffT>(w.maj * xs_maj + w.mn * xs_min);
-  w.ot = static_cast<OffT>(w.maj * ts_maj + w.mn * ts_min);
+  // offsets relative to the chunk's first class column
+  const int64_t xc0 = static_cast<int64_t>(c0) * a.in_col_stride * xu;
+  const int64_t tc0 = lab ? 0 : static_cast<int64_t>(c0) * a.tg_col_stride * tu;
+  w.ox = static_cast<OffT>(xc0 + w.maj * xs_maj + w.mn * xs_min);
+  w.ot = static_cast<OffT>(tc0 + w.maj * ts_maj + w.mn * ts_min);
   const float tm1 = static_cast<float>(a.T - 1);
   const float margin = 4e-7f * static_cast<float>(a.T) + 1e-6f;
   const uint32_t cnt = e0 < hi ? (hi - e0 + kDB - 1) / kDB : 0;
   uint32_t done = 0;
   for (; done + kDU <= cnt; done += kDU)
-    dense_round<XF32, YI64, MODE, FAST, UNIFORM, false>(a, w, sp, kDU, cf, tm1, margin, s_thr, s_hist, C);
+    dense_round<XF32, YI64, MODE, FAST, UNIFORM, false>(a, w, sp, kDU, cf, tm1, margin, s_thr, s_hist, C, c0);
   if (done < cnt)
-    dense_round<XF32, YI64, MODE, FAST, UNIFORM, true>(a, w, sp, cnt - done, cf, tm1, margin, s_thr, s_hist, C);
+    dense_round<XF32, YI64, MODE, FAST, UNIFORM, true>(a, w, sp, cnt - done, cf, tm1, margin, s_thr, s_hist, C, c0);
   __syncthreads();
-  unsigned* row = slab + static_cast<int64_t>(blockIdx.x) * W;
+  const int64_t wc = static_cast<int64_t>(a.T + 1) * cb;  // slab row stride
+  unsigned* row = slab + (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * wc;
   for (int k = threadIdx.x; k < W; k += kDB) row[k] = s_hist[k];
 }
 
-// slab [G][W] packed -> acc[(w) * 2 + {0: neg, 1: pos}] (u32, zero on entry; the suffix kernel
-// consumes and re-zeroes it as replica 0)
-__global__ __launch_bounds__(256) void binned_dense_reduce_kernel(const unsigned* slab, int G, int W,
-                                                                  unsigned* acc) {
+// slab [chunk][G][(T+1) x cb] packed -> acc[((bin * classes) + c0 + c) * 2 + {0: neg, 1: pos}]
+// (u32, zero on entry; the suffix kernel consumes and re-zeroes it as replica 0)
+__global__ __launch_bounds__(256) void binned_dense_reduce_kernel(const unsigned* slab, int G, int T, int64_t classes,
+                                                                  int cb, unsigned* acc) {
+  const int c0 = blockIdx.z * cb;
+  const int C = static_cast<int>(min(static_cast<int64_t>(cb), classes - c0));
+  const int W = (T + 1) * C;
   const int w = blockIdx.x * 256 + threadIdx.x;
   if (w >= W) return;
+  const int64_t wc = static_cast<int64_t>(T + 1) * cb;
+  const unsigned* base = slab + static_cast<int64_t>(blockIdx.z) * G * wc;
   const int g0 = blockIdx.y * kReduceRows;
   unsigned v[kReduceRows];
 #pragma unroll
   for (int r = 0; r < kReduceRows; ++r)
-    v[r] = g0 + r < G ? slab[static_cast<int64_t>(g0 + r) * W + w] : 0u;
+    v[r] = g0 + r < G ? base[static_cast<int64_t>(g0 + r) * wc + w] : 0u;
   unsigned neg = 0, pos = 0;
 #pragma unroll
   for (int r = 0; r < kReduceRows; ++r) {
     neg += v[r] & 0xffffu;
     pos += v[r] >> 16;
   }
-  if (neg) atomicAdd(&acc[2 * w], neg);
-  if (pos) atomicAdd(&acc[2 * w + 1], pos);
+  const int b = w / C, c = w - b * C;
+  const int64_t o = (static_cast<int64_t>(b) * classes + c0 + c) * 2;
+  if (neg) atomicAdd(&acc[o], neg);
+  if (pos) atomicAdd(&acc[o + 1], pos);
 }
 
 __device__ __forceinline__ unsigned long long wave_incl_sum_u64(unsigned long long v) {
@@ -542,9 +557,15 @@ int launch_binned_finalize(const BinnedFinalizeArgs& a, hipStream_t stream) {
 }
 
 namespace {
+// classes per dense chunk: a [T+1][cb] histogram plus the thresholds in 64 KB of LDS
+int dense_chunk(int T, int64_t c) {
+  const int64_t thr_words = ((T * 4 + 15) / 16) * 4;
+  const int64_t cb = (kDenseMaxWords - thr_words) / (T + 1);
+  return static_cast<int>(cb < c ? cb : c);
+}
+
 bool dense_eligible(int T, int64_t c) {
-  const int64_t W = (T + 1) * c;
-  return W >= 256 && W + T + 4 <= kDenseMaxWords;  // histogram + thresholds in 64 KB of LDS
+  return (T + 1) * c >= 256 && dense_chunk(T, c) >= 1;
 }
 int dtype_bytes(DType d) {
   switch (d) {
@@ -559,29 +580,31 @@ int dtype_bytes(DType d) {
 int64_t binned_workspace_words(int T, int64_t c) { return static_cast<int64_t>(kReplicas) * (T + 1) * c * 2; }
 
 int64_t binned_slab_words(int T, int64_t c) {
-  return dense_eligible(T, c) ? static_cast<int64_t>(kDenseMaxBlocks) * (T + 1) * c : 0;
+  if (!dense_eligible(T, c)) return 0;
+  const int64_t cb = dense_chunk(T, c), chunks = (c + cb - 1) / cb;
+  return std::max<int64_t>(kDenseMaxBlocks, chunks) * (T + 1) * cb;  // G * chunks <= this many rows
 }
 
 namespace {
 template <bool XF32, bool YI64, int MODE, bool FAST, bool UNIFORM>
-void dense_go(const BinnedArgs& s, dim3 grid, size_t smem, hipStream_t stream, unsigned* slab) {
-  hipLaunchKernelGGL((binned_hist_dense_kernel<XF32, YI64, MODE, FAST, UNIFORM>), grid, dim3(kDB), smem, stream, s, slab);
+void dense_go(const BinnedArgs& s, dim3 grid, size_t smem, hipStream_t stream, unsigned* slab, int cb) {
+  hipLaunchKernelGGL((binned_hist_dense_kernel<XF32, YI64, MODE, FAST, UNIFORM>), grid, dim3(kDB), smem, stream, s, slab, cb);
 }
 
 template <int MODE>
 void launch_dense_mode(const BinnedArgs& s, dim3 grid, size_t smem, hipStream_t stream, unsigned* slab, bool xf32,
-                       bool yi64, bool fast) {
+                       bool yi64, bool fast, int cb) {
   if (fast) {
-    if (s.uniform) dense_go<true, true, MODE, true, true>(s, grid, smem, stream, slab);
-    else dense_go<true, true, MODE, true, false>(s, grid, smem, stream, slab);
+    if (s.uniform) dense_go<true, true, MODE, true, true>(s, grid, smem, stream, slab, cb);
+    else dense_go<true, true, MODE, true, false>(s, grid, smem, stream, slab, cb);
   } else if (xf32 && yi64) {
-    dense_go<true, true, MODE, false, false>(s, grid, smem, stream, slab);
+    dense_go<true, true, MODE, false, false>(s, grid, smem, stream, slab, cb);
   } else if (xf32) {
-    dense_go<true, false, MODE, false, false>(s, grid, smem, stream, slab);
+    dense_go<true, false, MODE, false, false>(s, grid, smem, stream, slab, cb);
   } else if (yi64) {
-    dense_go<false, true, MODE, false, false>(s, grid, smem, stream, slab);
+    dense_go<false, true, MODE, false, false>(s, grid, smem, stream, slab, cb);
   } else {
-    dense_go<false, false, MODE, false, false>(s, grid, smem, stream, slab);
+    dense_go<false, false, MODE, false, false>(s, grid, smem, stream, slab, cb);
   }
 }
 
@@ -591,45 +614,50 @@ int64_t max_offset(int64_t n, int64_t c, int64_t rs, int64_t cs) {
 }
 
 void launch_dense(const BinnedArgs& s, dim3 grid, size_t smem, hipStream_t stream, unsigned* slab, bool xf32,
-                  bool yi64) {
+                  bool yi64, int cb) {
   // byte offsets in 32 bits: the walker can step one kDB stride past the range before the
   // bound check stops it, so keep 2^30 of headroom
   const int64_t lim = (int64_t{1} << 30);
   const bool fast = xf32 && yi64 && 4 * max_offset(s.n, s.c, s.in_row_stride, s.in_col_stride) < lim &&
                     8 * max_offset(s.n, s.mode == 1 ? 1 : s.c, s.tg_row_stride, s.tg_col_stride) < lim;
-  if (s.mode == 1) launch_dense_mode<1>(s, grid, smem, stream, slab, xf32, yi64, fast);
-  else launch_dense_mode<0>(s, grid, smem, stream, slab, xf32, yi64, fast);
+  if (s.mode == 1) launch_dense_mode<1>(s, grid, smem, stream, slab, xf32, yi64, fast, cb);
+  else launch_dense_mode<0>(s, grid, smem, stream, slab, xf32, yi64, fast, cb);
 }
 }  // namespace
 
 int launch_binned(const BinnedArgs& a, hipStream_t stream) {
   if (a.n <= 0 || a.c <= 0 || a.T <= 0) return 0;
   if (dense_eligible(a.T, a.c)) {
-    const int W = static_cast<int>((a.T + 1) * a.c);
-    unsigned* acc = a.ws;    // [W][2], replica 0 of the suffix kernel (zero contract)
-    unsigned* slab = a.slab;  // [G][W], fully overwritten per launch (separate scratch)
+    const int cb = dense_chunk(a.T, a.c);
+    const int chunks = static_cast<int>((a.c + cb - 1) / cb);
+    const int64_t wc = static_cast<int64_t>(a.T + 1) * cb;
+    unsigned* acc = a.ws;    // [T+1][classes][2], replica 0 of the suffix kernel (zero contract)
+    unsigned* slab = a.slab;  // [chunks][G][wc], fully overwritten per launch (separate scratch)
     if (slab == nullptr) return -2;
     const int thr_bytes = ((a.T * 4 + 15) / 16) * 16;
-    const size_t smem = thr_bytes + static_cast<size_t>(W) * 4;
+    const size_t smem = thr_bytes + static_cast<size_t>(wc) * 4;
     const bool xf32 = a.in_dt == DType::f32, yi64 = a.tg_dt == DType::i64;
-    // row slabs of <= kDenseMaxBlocks * kDenseBlockElems elements
-    const int64_t rows_per = std::max<int64_t>(1, kDenseMaxBlocks * kDenseBlockElems / a.c);
+    // <= kDenseMaxBlocks blocks over all chunks; row slabs keep every block <= 65535 elements
+    const int64_t gmax = std::max<int64_t>(1, kDenseMaxBlocks / chunks);
+    const int64_t rows_per = std::max<int64_t>(1, gmax * kDenseBlockElems / cb);
     for (int64_t r0 = 0; r0 < a.n; r0 += rows_per) {
       BinnedArgs s = a;
       s.n = std::min(rows_per, a.n - r0);
       s.input = static_cast<const char*>(a.input) + r0 * a.in_row_stride * dtype_bytes(a.in_dt);
       s.target = static_cast<const char*>(a.target) + r0 * a.tg_row_stride * dtype_bytes(a.tg_dt);
-      const int64_t E = s.n * a.c;
+      const int64_t E = s.n * cb;  // elements of a full chunk
       // ~one round of kDU elements per thread, never more than 65535 per block, and a flush
-      // (G * W words written and read back) of at most ~half the input's own bytes
+      // (G * wc words written and read back) of at most ~half the input's own bytes
       int64_t lo = (E + kDenseBlockElems - 1) / kDenseBlockElems;
-      int64_t hi = std::max<int64_t>(lo, std::min<int64_t>(kDenseMaxBlocks, E / (4 * W)));
+      int64_t hi = std::max<int64_t>(lo, std::min<int64_t>(gmax, E / (4 * wc)));
       int64_t G = std::min(std::max((E + kDB * kDU - 1) / (kDB * kDU), lo), hi);
       if (G < 1) G = 1;
-      const dim3 grid(static_cast<unsigned>(G));
-      launch_dense(s, grid, smem, stream, slab, xf32, yi64);
-      const dim3 rgrid((W + 255) / 256, static_cast<unsigned>((G + kReduceRows - 1) / kReduceRows));
-      hipLaunchKernelGGL(binned_dense_reduce_kernel, rgrid, dim3(256), 0, stream, slab, static_cast<int>(G), W, acc);
+      const dim3 grid(static_cast<unsigned>(G), static_cast<unsigned>(chunks));
+      launch_dense(s, grid, smem, stream, slab, xf32, yi64, cb);
+      const dim3 rgrid(static_cast<unsigned>((wc + 255) / 256), static_cast<unsigned>((G + kReduceRows - 1) / kReduceRows),
+                       static_cast<unsigned>(chunks));
+      hipLaunchKernelGGL(binned_dense_reduce_kernel, rgrid, dim3(256), 0, stream, slab, static_cast<int>(G), a.T, a.c,
+                         cb, acc);
     }
     const size_t smem2 = static_cast<size_t>(a.T + 1) * 2 * sizeof(unsigned);
     hipLaunchKernelGGL(binned_suffix_kernel, dim3(static_cast<unsigned>(a.c)), dim3(kB), smem2, stream, a, 1);

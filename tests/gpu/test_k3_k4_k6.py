@@ -140,6 +140,22 @@ def test_k4_dense_path(case):
         torch.testing.assert_close(a.cpu(), b)
 
 
+@pytest.mark.parametrize("shape", [(3000, 1000, 100), (2000, 100, 1000), (500, 7, 8000), (4000, 300, 57)])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_k4_dense_class_chunks(shape, mode):
+    """[T+1] x C beyond one block's LDS: the dense path splits classes into chunks (grid.y),
+    including a ragged last chunk and column-major (transposed) scores."""
+    n, C, T = shape
+    g = torch.Generator().manual_seed(n + C + T)
+    x = torch.rand(C, n, generator=g).t() if C == 300 else torch.rand(n, C, generator=g)
+    thr = torch.linspace(0, 1, T)
+    t = torch.randint(0, C, (n,), generator=g) if mode == 1 else torch.randint(0, 2, (n, C), generator=g)
+    exp = _binned_counts_aten(x.contiguous(), t, thr, mode)
+    got = binned_counts(x.to(DEV), t.to(DEV), thr.to(DEV), mode)
+    for a, b in zip(got, exp):
+        torch.testing.assert_close(a.cpu(), b)
+
+
 @pytest.mark.parametrize("T", [2, 3, 100, 201, 2000])
 @pytest.mark.parametrize("mode", [0, 1])
 def test_k4_uniform_threshold_boundaries(T, mode):
