@@ -76,7 +76,8 @@ unsigned long long* fold_workspace(const Tensor& like, hipStream_t stream) {
 
 // Self-cleaning scratch: zeroed once per (device, stream, slot), grown on demand; kernels that
 // use it leave it zeroed again, so no memset launch per call.
-void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot) {
+void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot,
+                       int64_t* capacity = nullptr) {
   static std::mutex mu;
   static std::unordered_map<uint64_t, Tensor> cache;
   const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
@@ -89,6 +90,7 @@ void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, in
     if (it == cache.end()) it = cache.emplace(key, ws).first;
     else it->second = ws;
   }
+  if (capacity) *capacity = it->second.numel();
   return it->second.data_ptr();
 }
 
@@ -636,8 +638,13 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   a.vals1 = base + 3 * m;
   a.hist = base + 4 * m;
   a.ngroups = tea::radix_sort_groups(a.tiles);
-  Tensor groups = at::zeros({4 * a.rows * a.ngroups * 256}, x.options().dtype(at::kInt));
-  a.groups = reinterpret_cast<uint32_t*>(groups.data_ptr<int32_t>());
+  // self-cleaning: [header: cells left dirty in region 3 | pad | 4 regions of `region` cells]
+  int64_t cap = 0;
+  uint32_t* gws = static_cast<uint32_t*>(
+      zeroed_workspace(x, stream_for(x), (4 + 4 * a.rows * a.ngroups * 256) * 4, 4, &cap));
+  a.dirty = gws;
+  a.groups = gws + 4;
+  a.region = (cap / 4 - 4) / 4;  // fixed per buffer, so the next call finds region 3 at the same place
   a.out_sorted = out_sorted.data_ptr<float>();
   a.out_order = out_order.data_ptr<int32_t>();
   Tensor pl;

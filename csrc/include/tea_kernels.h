@@ -285,7 +285,13 @@ struct RadixArgs {
   uint32_t* keys1 = nullptr;
   uint32_t* vals1 = nullptr;
   uint32_t* hist = nullptr;   // [rows, tiles, 256] per-tile digit counts of the current pass
-  uint32_t* groups = nullptr; // [4 passes, rows, ngroups, 256] digit counts per group of tiles, zero on entry
+  uint32_t* groups = nullptr; // 4 pass regions (`region` cells apart) of [rows, ngroups, 256] digit
+                              // counts per group of tiles.  Self-cleaning: passes 1-3 clear the
+                              // previous pass's region; pass 3's is cleared by the next sort's pass 0
+                              // (a last-block-done clear in the final downsweep serialised 512
+                              // same-address atomics: +5 us per 1M-key sort)
+  int64_t region = 0;
+  uint32_t* dirty = nullptr;  // cells of region 3 left to clear (written by the final downsweep)
   int64_t ngroups = 0;        // radix_sort_groups(tiles)
   float* out_sorted = nullptr;  // [rows, n] descending
   int32_t* out_order = nullptr; // [rows, n] source index within the row (or the payload)

@@ -130,7 +130,13 @@ __global__ __launch_bounds__(kRT) void radix_upsweep_kernel(RadixArgs a, const u
 #pragma unroll
   for (int q = 0; q < kRWaves; ++q) c += h[q][threadIdx.x];
   a.hist[(row * a.tiles + tile) * kBins + threadIdx.x] = c;
-  if (c) atomicAdd(&a.groups[((static_cast<int64_t>(pass) * a.rows + row) * a.ngroups + tile / kGroup) * kBins + threadIdx.x], c);
+  if (c) atomicAdd(&a.groups[pass * a.region + (row * a.ngroups + tile / kGroup) * kBins + threadIdx.x], c);
+  // self-cleaning group counts (no memset launch): clear the region consumed last - the previous
+  // pass's, or for pass 0 what the previous sort left in region 3
+  const int64_t cells = pass > 0 ? a.rows * a.ngroups * kBins : static_cast<int64_t>(*a.dirty);
+  uint32_t* prev = a.groups + (pass > 0 ? pass - 1 : 3) * a.region;
+  const int64_t nb = static_cast<int64_t>(gridDim.x) * gridDim.y;
+  for (int64_t q = (row * gridDim.x + tile) * kRT + threadIdx.x; q < cells; q += nb * kRT) prev[q] = 0u;
 }
 
 // Downsweep: wave w owns the contiguous sub-tile [w * 1024, (w + 1) * 1024) of the tile
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
   {  // digit bases = exclusive scan of the row's digit totals + this tile's prefix in the digit:
      // totals and the prefix of whole groups from the group counts, the rest from the tile
      // counts of this tile's own group (all independent, L2-resident loads)
-    const uint32_t* G = a.groups + (static_cast<int64_t>(pass) * a.rows + row) * a.ngroups * kBins + threadIdx.x;
+    const uint32_t* G = a.groups + pass * a.region + row * a.ngroups * kBins + threadIdx.x;
     const int mg = tile / kGroup;
     uint32_t tot = 0, pre = 0;
     // fixed-trip, fully unrolled chunks: every load of a chunk is in flight at once
@@ -260,6 +266,8 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     }
   }
   __syncthreads();
+  if (last && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    *a.dirty = static_cast<uint32_t>(a.rows * a.ngroups * kBins);  // for the next sort's pass 0
   const int64_t tn64 = a.n - tbase;
   const int tn = static_cast<int>(tn64 < kRTile ? tn64 : kRTile);
   for (int p = threadIdx.x; p < tn; p += kRT) {

@@ -4,10 +4,13 @@
 //   auroc.py:115-152, 206-235   diff != 0 -> pad -> gather x2 -> cumsum x2 -> masked_scatter x2
 //                               (host-synchronising) -> trapz -> where
 //   auprc.py / precision_recall_curve.py:156-231   same prefix + per-class Python loops
-// with four small launches that never leave the device:
-//   1 tile_sums : per 4096-sample tile, gather (target, weight) through the sort permutation,
-//                 write a = w*t, b = w*(1-t) (float2) and the tile totals (double).
-//   2 tile_scan : one block per row: exclusive scan of tile totals (TP / FP before each tile).
+// with three launches (rows of <= kFuseTiles tiles) or four that never leave the device:
+//   1 tile_sums : per 1024-sample tile, the tile totals (double) of a = w*t, b = w*(1-t); when the
+//                 sort carried the targets / labels (payload kinds 1, 2) they are read in place,
+//                 otherwise (target, weight) are gathered through the permutation into float2 ab.
+//   2 tile_scan : (long rows only) one block per row: exclusive scan of the tile totals.  Short
+//                 rows fold it into tile_area: each block sums the totals of the tiles before it
+//                 (<= kFuseTiles L2-resident loads), one launch and ~8 us less at 1M samples.
 //   3 tile_area : per tile, LDS block scans give TP/FP at every element; prefix-max / suffix-min
 //                 scans locate each sample's tie group (head / tail) inside the tile; groups that
 //                 straddle a tile edge are resolved once per block by a binary search on the
@@ -28,6 +31,7 @@ constexpr int kT = 256;              // threads per block
 constexpr int kPer = 4;              // samples per thread (1024-sample tiles: ~1000 blocks at 1M;
                                      // measured: 512- and 2048-sample tiles are 5-6% slower end to end)
 constexpr int kTile = kT * kPer;     // samples per tile
+constexpr int kFuseTiles = 1536;     // (<= 4) rows up to this many tiles skip the tile_scan launch
 
 struct alignas(16) D2 {
   double x, y;
@@ -111,6 +115,14 @@ __device__ __forceinline__ float2 sample_ab(const AucScanArgs& a, int r, int64_t
   return make_float2(w * t, w * (1.f - t));
 }
 
+// (a, b) of sorted sample i: in place for payload kinds 1 / 2, else the gathered ab copy
+template <bool DIRECT>
+__device__ __forceinline__ float2 load_ab(const AucScanArgs& a, const float2* ab, int r, int64_t i) {
+  if constexpr (DIRECT) return sample_ab(a, r, i);
+  return ab[i];
+}
+
+template <bool DIRECT>
 __global__ __launch_bounds__(kT) void tile_sums_kernel(AucScanArgs a) {
   const int r = blockIdx.y;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile;
@@ -121,7 +133,7 @@ __global__ __launch_bounds__(kT) void tile_sums_kernel(AucScanArgs a) {
     const int64_t i = base + k * kT + threadIdx.x;  // coalesced gather order
     if (i < a.n) {
       const float2 v = sample_ab(a, r, i);
-      ab[i] = v;
+      if constexpr (!DIRECT) ab[i] = v;
       sa += v.x;
       sb += v.y;
     }
@@ -161,11 +173,26 @@ __global__ __launch_bounds__(kT) void tile_scan_kernel(AucScanArgs a, int ntiles
   if (threadIdx.x == 0) reinterpret_cast<D2*>(a.totals)[r] = D2{carry.x - init.x, carry.y - init.y};
 }
 
+// init + the totals of tiles [0, upto) of row r (block-cooperative; fused tile_scan)
+__device__ D2 tiles_prefix(const AucScanArgs& a, const D2* ts, int upto, int r, D2* lds) {
+  double sa = 0.0, sb = 0.0;
+  for (int t = threadIdx.x; t < upto; t += kT) {
+    const D2 v = ts[t];
+    sa += v.x;
+    sb += v.y;
+  }
+  D2 tot;
+  block_excl_scan(D2{sa, sb}, lds, tot);
+  if (a.init) tot = d2add(tot, D2{a.init[2 * r], a.init[2 * r + 1]});
+  return tot;
+}
+
 // sum of a/b over [lo, hi] (inclusive, hi may be < lo -> empty) of row r, block-cooperative
-__device__ D2 block_range_sum(const float2* ab, int64_t lo, int64_t hi, D2* lds) {
+template <bool DIRECT>
+__device__ D2 block_range_sum(const AucScanArgs& a, const float2* ab, int r, int64_t lo, int64_t hi, D2* lds) {
   double sa = 0.0, sb = 0.0;
   for (int64_t i = lo + threadIdx.x; i <= hi; i += kT) {
-    const float2 v = ab[i];
+    const float2 v = load_ab<DIRECT>(a, ab, r, i);
     sa += v.x;
     sb += v.y;
   }
@@ -196,14 +223,53 @@ __device__ int64_t last_equal(const AucScanArgs& a, int r, int64_t lo, int64_t h
   return l - 1;
 }
 
-template <typename K>
+// tile start (TP, FP): from tile_scan's table, or (FUSED) summed here from the tile totals
+template <bool FUSED>
+__device__ __forceinline__ D2 tile_start(const AucScanArgs& a, int r, int tile, int ntiles, D2* lds) {
+  if constexpr (FUSED)
+    return tiles_prefix(a, reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles, tile, r, lds);
+  return reinterpret_cast<const D2*>(a.tstart)[static_cast<int64_t>(r) * ntiles + tile];
+}
+
+// row r: AUROC = roc / (P * N) (0.5 if degenerate), AUPRC = pr / P (0 if P = 0)
+__device__ void finalize_row(const AucScanArgs& a, int r, int ntiles, bool fused, D2* lds) {
+  const D2* ta = reinterpret_cast<const D2*>(a.tarea) + static_cast<int64_t>(r) * ntiles;
+  const D2* ts = reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
+  double roc = 0.0, pr = 0.0, p = 0.0, q = 0.0;
+  for (int t = threadIdx.x; t < ntiles; t += kT) {
+    const D2 v = ta[t];
+    roc += v.x;
+    pr += v.y;
+    if (fused) {
+      const D2 u = ts[t];
+      p += u.x;
+      q += u.y;
+    }
+  }
+  D2 tot, pn;
+  block_excl_scan(D2{roc, pr}, lds, tot);
+  block_excl_scan(D2{p, q}, lds, pn);
+  if (threadIdx.x == 0) {
+    if (!fused) pn = reinterpret_cast<const D2*>(a.totals)[r];  // this shard's own P, N
+    if (a.out_raw) {
+      a.out_raw[4 * r] = tot.x;
+      a.out_raw[4 * r + 1] = tot.y;
+      a.out_raw[4 * r + 2] = pn.x;
+      a.out_raw[4 * r + 3] = pn.y;
+    }
+    const double factor = pn.x * pn.y;
+    if (a.out_auroc) a.out_auroc[r] = factor == 0.0 ? 0.5 : tot.x / factor;
+    if (a.out_auprc) a.out_auprc[r] = pn.x == 0.0 ? 0.0 : tot.y / pn.x;
+  }
+}
+
+template <typename K, bool DIRECT, bool FUSED>
 __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   const int r = blockIdx.y;
   const int ntiles = gridDim.x;
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile;
   const int tile_n = static_cast<int>(min(static_cast<int64_t>(kTile), a.n - base));
   const float2* ab = reinterpret_cast<const float2*>(a.ab) + static_cast<int64_t>(r) * a.n;
-  const D2* st = reinterpret_cast<const D2*>(a.tstart) + static_cast<int64_t>(r) * ntiles;
 
   __shared__ double s_tpx[kTile];  // TP before each element (exclusive)
   __shared__ double s_fpi[kTile];  // FP up to each element (inclusive)
@@ -222,7 +288,7 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
     const int64_t i = base + j0 + k;
     if (j0 + k < tile_n) {
       key[k] = key_at<K>(a, r, i);
-      v[k] = ab[i];
+      v[k] = load_ab<DIRECT>(a, ab, r, i);
     } else {
       key[k] = K(0);
       v[k] = make_float2(0.f, 0.f);
@@ -232,7 +298,7 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   }
   D2 tot;
   const D2 ex = block_excl_scan(D2{la, lb}, lds, tot);
-  const D2 t0 = st[blockIdx.x];
+  const D2 t0 = tile_start<FUSED>(a, r, blockIdx.x, ntiles, lds);
   const K prev_key = (base > 0) ? key_at<K>(a, r, base - 1) : K(0);
   const K next_key = (base + tile_n < a.n) ? key_at<K>(a, r, base + tile_n) : K(0);
 
@@ -296,8 +362,9 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
     __syncthreads();
     const int64_t hpos = s_pos;
     const int64_t ht = hpos / kTile;
-    const D2 part = block_range_sum(ab, ht * kTile, hpos - 1, lds);
-    if (threadIdx.x == 0) s_bound[0] = st[ht].x + part.x;
+    const D2 part = block_range_sum<DIRECT>(a, ab, r, ht * kTile, hpos - 1, lds);
+    const D2 hs = tile_start<FUSED>(a, r, static_cast<int>(ht), ntiles, lds);
+    if (threadIdx.x == 0) s_bound[0] = hs.x + part.x;
     __syncthreads();
   }
   if (s_flags[1]) {
@@ -306,10 +373,11 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
     __syncthreads();
     const int64_t epos = s_pos;
     const int64_t et = epos / kTile;
-    const D2 part = block_range_sum(ab, et * kTile, epos, lds);
+    const D2 part = block_range_sum<DIRECT>(a, ab, r, et * kTile, epos, lds);
+    const D2 es = tile_start<FUSED>(a, r, static_cast<int>(et), ntiles, lds);
     if (threadIdx.x == 0) {
-      s_bound[1] = st[et].x + part.x;
-      s_bound[2] = st[et].y + part.y;
+      s_bound[1] = es.x + part.x;
+      s_bound[2] = es.y + part.y;
     }
     __syncthreads();
   }
@@ -353,29 +421,12 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
     reinterpret_cast<D2*>(a.tarea)[static_cast<int64_t>(r) * ntiles + blockIdx.x] = area;
 }
 
-__global__ __launch_bounds__(kT) void finalize_kernel(AucScanArgs a, int ntiles) {
-  const int r = blockIdx.x;
-  const D2* ta = reinterpret_cast<const D2*>(a.tarea) + static_cast<int64_t>(r) * ntiles;
-  double roc = 0.0, pr = 0.0;
-  for (int t = threadIdx.x; t < ntiles; t += kT) {
-    roc += ta[t].x;
-    pr += ta[t].y;
-  }
+// one block per row.  (A "last block finalises" fold inside tile_area was measured: the
+// agent-scope release / acquire fences it needs per block - the XCDs' L2s are not coherent -
+// doubled tile_area, 16 -> 34 us at 1M samples; a separate launch costs ~4 us.)
+__global__ __launch_bounds__(kT) void finalize_kernel(AucScanArgs a, int ntiles, int fused) {
   __shared__ D2 lds[kT / 64];
-  D2 tot;
-  block_excl_scan(D2{roc, pr}, lds, tot);
-  if (threadIdx.x == 0) {
-    const D2 pn = reinterpret_cast<const D2*>(a.totals)[r];
-    if (a.out_raw) {
-      a.out_raw[4 * r] = tot.x;
-      a.out_raw[4 * r + 1] = tot.y;
-      a.out_raw[4 * r + 2] = pn.x;
-      a.out_raw[4 * r + 3] = pn.y;
-    }
-    const double factor = pn.x * pn.y;
-    if (a.out_auroc) a.out_auroc[r] = factor == 0.0 ? 0.5 : tot.x / factor;
-    if (a.out_auprc) a.out_auprc[r] = pn.x == 0.0 ? 0.0 : tot.y / pn.x;
-  }
+  finalize_row(a, blockIdx.x, ntiles, fused != 0, lds);
 }
 
 }  // namespace
@@ -400,13 +451,23 @@ int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream) {
   ws += a.rows * ntiles * 16;
   a.totals = ws;
   const dim3 grid(ntiles, static_cast<unsigned>(a.rows));
-  hipLaunchKernelGGL(tile_sums_kernel, grid, dim3(kT), 0, stream, a);
-  hipLaunchKernelGGL(tile_scan_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles);
-  if (a.key_dt == DType::f64)
-    hipLaunchKernelGGL(tile_area_kernel<double>, grid, dim3(kT), 0, stream, a);
-  else
-    hipLaunchKernelGGL(tile_area_kernel<float>, grid, dim3(kT), 0, stream, a);
-  hipLaunchKernelGGL(finalize_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles);
+  // fused prefix: single / few rows only - it lengthens every block's dependency chain (an extra
+  // block reduction before the scan), which 100 rows x 98 tiles paid for with +12 us per call
+  const bool direct = a.payload_kind != 0, fused = ntiles <= kFuseTiles && a.rows <= 4;
+  const bool f64 = a.key_dt == DType::f64;
+  if (direct) hipLaunchKernelGGL(tile_sums_kernel<true>, grid, dim3(kT), 0, stream, a);
+  else hipLaunchKernelGGL(tile_sums_kernel<false>, grid, dim3(kT), 0, stream, a);
+  if (!fused) hipLaunchKernelGGL(tile_scan_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles);
+#define TEA_AREA(K, D, F) hipLaunchKernelGGL((tile_area_kernel<K, D, F>), grid, dim3(kT), 0, stream, a)
+  if (f64) {
+    if (direct) { if (fused) TEA_AREA(double, true, true); else TEA_AREA(double, true, false); }
+    else { if (fused) TEA_AREA(double, false, true); else TEA_AREA(double, false, false); }
+  } else {
+    if (direct) { if (fused) TEA_AREA(float, true, true); else TEA_AREA(float, true, false); }
+    else { if (fused) TEA_AREA(float, false, true); else TEA_AREA(float, false, false); }
+  }
+#undef TEA_AREA
+  hipLaunchKernelGGL(finalize_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles, fused ? 1 : 0);
   return static_cast<int>(hipGetLastError());
 }
 
