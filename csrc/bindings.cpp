@@ -153,6 +153,7 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
     TORCH_CHECK(err->scalar_type() == at::kInt && err->numel() >= 1 && err->device() == input.device(),
                 "cls_counts: err must be an int32 tensor on the input device");
     a.err = err->data_ptr<int>();
+    if (err->numel() >= 3) a.err_max = a.err + 1;  // [flags, max bad target, max bad prediction]
     a.check_target = 1;
   }
   a.max_blocks = static_cast<int>(max_blocks);
@@ -481,6 +482,8 @@ void ne_sums(const Tensor& x, const Tensor& t, const optional<Tensor>& w, bool f
   if (err.has_value()) {
     TORCH_CHECK(err->scalar_type() == at::kInt, "ne_sums: err must be int32");
     a.err = err->data_ptr<int>();
+    // [flag, pad, range keys as 2 x u64] (8-byte aligned: caching-allocator blocks are)
+    if (err->numel() >= 6) a.range = reinterpret_cast<unsigned long long*>(a.err + 2);
   }
   Tensor ws;
   if (deterministic && a.rows > 0) {

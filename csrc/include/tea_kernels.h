@@ -31,6 +31,7 @@ struct ClsCountsArgs {
   float* cls_fp = nullptr;       // [num_classes] wrong predictions per predicted class
   float* confusion = nullptr;    // [num_classes, num_classes] (target, pred)
   int* err = nullptr;            // error bits (1: bad target, 2: bad prediction)
+  int* err_max = nullptr;        // optional [2]: largest target / prediction >= num_classes
   int check_target = 0;          // flag bad targets even without histograms
   unsigned long long* fold_ws = nullptr;  // tea_fold.h cells (per-stream, self-cleaning)
   int max_blocks = 0;
@@ -207,6 +208,9 @@ struct NeArgs {
   int from_logits = 0;
   double* out = nullptr;  // [rows, 3]: sum w*bce, sum w*t, sum w (accumulated)
   int* err = nullptr;
+  // optional: order-preserving u64 keys of max(x) and (complemented) min(x) over the launch,
+  // atomicMax-accumulated (zero = unset), so a deferred range error can print the batch range
+  unsigned long long* range = nullptr;
   double* ordered_ws = nullptr;  // deterministic mode: [rows * 3, ne_sums_blocks] partials
 };
 int ne_sums_blocks(int64_t n);

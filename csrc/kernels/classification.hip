@@ -90,12 +90,18 @@ struct Hist {
 };
 
 __device__ __forceinline__ void row_hist(const Hist& h, int64_t C, int64_t t, int64_t pred,
-                                         bool correct, int* err, int check_target) {
+                                         bool correct, int* err, int check_target, int* err_max) {
   const bool t_ok = t >= 0 && t < C;
   const bool p_ok = pred >= 0 && pred < C;
   if (err) {
-    if (!t_ok && (h.cls_label || h.cls_correct || h.confusion || check_target)) atomicOr(err, 1);
-    if (!p_ok && (h.cls_pred || h.confusion || (h.cls_fp && !correct))) atomicOr(err, 2);
+    const bool bad_t = !t_ok && (h.cls_label || h.cls_correct || h.confusion || check_target);
+    const bool bad_p = !p_ok && (h.cls_pred || h.confusion || (h.cls_fp && !correct));
+    if (bad_t) atomicOr(err, 1);
+    if (bad_p) atomicOr(err, 2);
+    // the largest offending label / prediction: the reference's message prints torch.max of
+    // the batch, which is that value whenever one is >= C (its check)
+    if (err_max && bad_t && t >= C) atomicMax(err_max, static_cast<int>(t < 2147483647 ? t : 2147483647));
+    if (err_max && bad_p && pred >= C) atomicMax(err_max + 1, static_cast<int>(pred < 2147483647 ? pred : 2147483647));
   }
   if (t_ok) {
     if (h.cls_correct && correct) atomicAdd(h.cls_correct + t, 1.f);
@@ -290,7 +296,7 @@ __global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
     if (lane == 0) {
       correct_acc += correct;
       rows_acc += 1;
-      row_hist(h, a.num_classes, t, pred, correct, a.err, a.check_target);
+      row_hist(h, a.num_classes, t, pred, correct, a.err, a.check_target, a.err_max);
     }
   }
   block_micro(a, correct_acc, rows_acc);
@@ -344,7 +350,7 @@ __global__ __launch_bounds__(kBlock) void cls_narrow_kernel(ClsCountsArgs a) {
     }
     correct_acc += correct;
     rows_acc += 1;
-    row_hist(lh, C, t, pred, correct, a.err, a.check_target);
+    row_hist(lh, C, t, pred, correct, a.err, a.check_target, a.err_max);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < C; i += kBlock) {
@@ -370,7 +376,7 @@ __global__ __launch_bounds__(kBlock) void cls_labels_kernel(ClsCountsArgs a) {
     const bool correct = p == t;
     correct_acc += correct;
     rows_acc += 1;
-    row_hist(h, a.num_classes, t, p, correct, a.err, a.check_target);
+    row_hist(h, a.num_classes, t, p, correct, a.err, a.check_target, a.err_max);
   }
   block_micro(a, correct_acc, rows_acc);
 }

@@ -275,21 +275,42 @@ __device__ __forceinline__ double bce(double x, double t, bool logits) {
   return -(t * (lp < -100.0 ? -100.0 : lp) + (1.0 - t) * (lq < -100.0 ? -100.0 : lq));
 }
 
+// order-preserving u64 key of a double (larger key = larger value)
+__device__ __forceinline__ unsigned long long ord_key(double x) {
+  const unsigned long long u = static_cast<unsigned long long>(__double_as_longlong(x));
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+
 __global__ __launch_bounds__(kB) void ne_sums_kernel(NeArgs a) {
   const int r = blockIdx.y;
   double s_ce = 0, s_w = 0, s_pos = 0;
+  double mn = INFINITY, mx = -INFINITY;
   bool bad = false;
   for (int64_t i = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x; i < a.n;
        i += static_cast<int64_t>(gridDim.x) * kB) {
     const double x = load_as_f64(a.x, a.x_dt, r * a.x_row_stride + i);
     const double t = load_as_f64(a.t, a.t_dt, r * a.t_row_stride + i);
     const double w = a.w ? load_as_f64(a.w, a.w_dt, r * a.w_row_stride + i) : 1.0;
-    if (!a.from_logits && !(x >= 0.0 && x <= 1.0)) bad = true;
+    // the reference's check is max > 1 or min < 0: NaN passes it
+    if (!a.from_logits && (x < 0.0 || x > 1.0)) bad = true;
+    mn = fmin(mn, x);
+    mx = fmax(mx, x);
     s_ce += w * bce(x, t, a.from_logits != 0);
     s_w += w;
     s_pos += w * t;
   }
   if (bad && a.err) atomicOr(a.err, 1);
+  if (a.range && !a.from_logits) {  // one pair of atomics per block
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mn = fmin(mn, __shfl_xor(mn, o, 64));
+      mx = fmax(mx, __shfl_xor(mx, o, 64));
+    }
+    if (lane_id() == 0 && mx >= mn) {
+      atomicMax(a.range, ord_key(mx));
+      atomicMax(a.range + 1, ~ord_key(mn));
+    }
+  }
   s_ce = wave_sum(s_ce);
   s_w = wave_sum(s_w);
   s_pos = wave_sum(s_pos);

@@ -678,6 +678,74 @@ _err("cls_ne_update", "cls", "BinaryNormalizedEntropy", lambda: ({"num_tasks": 2
 _err("cls_topk_ml_k", "cls", "TopKMultilabelAccuracy", lambda: ({"k": 1}, []))
 _err("cls_ctr_tasks", "cls", "ClickThroughRate", lambda: ({"num_tasks": 0}, []))
 _err("cls_hit_rate_k", "cls", "HitRate", lambda: ({"k": 0}, [((_x(4, 4), _y(4, 4)), {})]))
+# class constructors / update checks of every classification family (same message as the
+# reference; GPU class updates may defer a data check to compute(), which the runner includes)
+_U = lambda *a: [(a, {})]  # noqa: E731
+_err("cls_bacc_shape", "cls", "BinaryAccuracy", lambda: ({}, _U(_x(4), _y(2, 5))))
+_err("cls_mcacc_len", "cls", "MulticlassAccuracy", lambda: ({}, _U(_x(4, 3), _y(3, 5))))
+_err("cls_mcacc_k0", "cls", "MulticlassAccuracy", lambda: ({"k": 0}, []))
+_err("cls_mcacc_macro_nc", "cls", "MulticlassAccuracy", lambda: ({"average": "macro"}, []))
+_err("cls_mlacc_criteria", "cls", "MultilabelAccuracy", lambda: ({"criteria": "foo"}, []))
+_err("cls_mlacc_shape", "cls", "MultilabelAccuracy", lambda: ({}, _U(_x(4, 3), _y(2, 4, 2))))
+_err("cls_topk_ml_criteria", "cls", "TopKMultilabelAccuracy", lambda: ({"criteria": "x", "k": 2}, []))
+_err("cls_topk_ml_1d", "cls", "TopKMultilabelAccuracy", lambda: ({"k": 2}, _U(_x(4), _y(2, 4))))
+for _fam, _cls in (("prec", "Precision"), ("rec", "Recall"), ("f1", "F1Score")):
+    _err(f"cls_b{_fam}_shape", "cls", f"Binary{_cls}", lambda _c=_cls: ({}, _U(_x(4), _y(2, 5))))
+    _err(f"cls_mc{_fam}_average", "cls", f"Multiclass{_cls}", lambda _c=_cls: ({"average": "samples", "num_classes": 3}, []))
+    _err(f"cls_mc{_fam}_macro_nc", "cls", f"Multiclass{_cls}", lambda _c=_cls: ({"average": "macro"}, []))
+    _err(f"cls_mc{_fam}_len", "cls", f"Multiclass{_cls}", lambda _c=_cls: ({"num_classes": 3}, _U(_x(4, 3), _y(3, 5))))
+_err("cls_bcm_normalize", "cls", "BinaryConfusionMatrix", lambda: ({"normalize": "rows"}, []))
+_err("cls_bcm_shape", "cls", "BinaryConfusionMatrix", lambda: ({}, _U(_x(4), _y(2, 3))))
+_err("cls_mccm_one_class", "cls", "MulticlassConfusionMatrix", lambda: ({"num_classes": 1}, []))
+_err("cls_mccm_normalize", "cls", "MulticlassConfusionMatrix", lambda: ({"num_classes": 3, "normalize": "x"}, []))
+_err("cls_mccm_target_range", "cls", "MulticlassConfusionMatrix",
+     lambda: ({"num_classes": 3}, _U(_x(4, 3), torch.tensor([0, 1, 5, 2]))))
+_err("cls_mccm_target_range_i32", "cls", "MulticlassConfusionMatrix",
+     lambda: ({"num_classes": 3}, _U(_x(4, 3), torch.tensor([0, 4, 1, 2], dtype=torch.int32))))
+_err("cls_mccm_input_range", "cls", "MulticlassConfusionMatrix",
+     lambda: ({"num_classes": 3}, _U(torch.tensor([0, 1, 7, 2]), torch.tensor([0, 1, 1, 2]))))
+_err("cls_mccm_input_shape", "cls", "MulticlassConfusionMatrix", lambda: ({"num_classes": 3}, _U(_x(4, 2), _y(3, 4))))
+_err("cls_bauprc_shape", "cls", "BinaryAUPRC", lambda: ({}, _U(_x(4), _y(2, 5))))
+_err("cls_bauprc_tasks", "cls", "BinaryAUPRC", lambda: ({"num_tasks": 0}, []))
+_err("cls_mcauprc_classes", "cls", "MulticlassAUPRC", lambda: ({"num_classes": 1}, []))
+_err("cls_mcauprc_average", "cls", "MulticlassAUPRC", lambda: ({"num_classes": 3, "average": "x"}, []))
+_err("cls_mcauprc_shape", "cls", "MulticlassAUPRC", lambda: ({"num_classes": 3}, _U(_x(4, 2), _y(3, 4))))
+_err("cls_mlauprc_labels", "cls", "MultilabelAUPRC", lambda: ({"num_labels": 1}, []))
+_err("cls_mlauprc_average", "cls", "MultilabelAUPRC", lambda: ({"num_labels": 3, "average": "x"}, []))
+_err("cls_mlauprc_shape", "cls", "MultilabelAUPRC", lambda: ({"num_labels": 3}, _U(_x(4, 3), _y(2, 4, 2))))
+_err("cls_mcauroc_average", "cls", "MulticlassAUROC", lambda: ({"num_classes": 3, "average": "x"}, []))
+_err("cls_mcauroc_shape", "cls", "MulticlassAUROC", lambda: ({"num_classes": 3}, _U(_x(4, 2), _y(3, 4))))
+_err("cls_bbauprc_thr", "cls", "BinaryBinnedAUPRC", lambda: ({"threshold": [0.5, 0.2]}, []))
+_err("cls_bbauprc_shape", "cls", "BinaryBinnedAUPRC", lambda: ({}, _U(_x(4), _y(2, 5))))
+_err("cls_mcbauprc_classes", "cls", "MulticlassBinnedAUPRC", lambda: ({"num_classes": 1}, []))
+_err("cls_mcbauprc_thr", "cls", "MulticlassBinnedAUPRC", lambda: ({"num_classes": 3, "threshold": [0.9, 0.1]}, []))
+_err("cls_mcbauprc_shape", "cls", "MulticlassBinnedAUPRC", lambda: ({"num_classes": 3}, _U(_x(4, 2), _y(3, 4))))
+_err("cls_mlbauprc_thr", "cls", "MultilabelBinnedAUPRC", lambda: ({"num_labels": 3, "threshold": [0.9, 0.1]}, []))
+_err("cls_mlbauprc_shape", "cls", "MultilabelBinnedAUPRC", lambda: ({"num_labels": 3}, _U(_x(4, 3), _y(2, 4, 2))))
+_err("cls_bbauroc_shape", "cls", "BinaryBinnedAUROC", lambda: ({}, _U(_x(4), _y(2, 5))))
+_err("cls_mcbauroc_thr", "cls", "MulticlassBinnedAUROC", lambda: ({"num_classes": 3, "threshold": [0.9, 0.1]}, []))
+_err("cls_bbprc_thr", "cls", "BinaryBinnedPrecisionRecallCurve", lambda: ({"threshold": [0.5, 0.2]}, []))
+_err("cls_bbprc_shape", "cls", "BinaryBinnedPrecisionRecallCurve", lambda: ({}, _U(_x(4), _y(2, 5))))
+_err("cls_mlbprc_thr", "cls", "MultilabelBinnedPrecisionRecallCurve", lambda: ({"num_labels": 3, "threshold": [0.9, 0.1]}, []))
+_err("cls_bprc_shape", "cls", "BinaryPrecisionRecallCurve", lambda: ({}, _U(_x(4), _y(2, 5))))
+_err("cls_mcprc_shape", "cls", "MulticlassPrecisionRecallCurve", lambda: ({"num_classes": 3}, _U(_x(4, 2), _y(3, 4))))
+_err("cls_mlprc_shape", "cls", "MultilabelPrecisionRecallCurve", lambda: ({"num_labels": 3}, _U(_x(4, 3), _y(2, 4, 2))))
+_err("cls_brafp_min_precision", "cls", "BinaryRecallAtFixedPrecision", lambda: ({"min_precision": 1.5}, []))
+_err("cls_mlrafp_min_precision", "cls", "MultilabelRecallAtFixedPrecision",
+     lambda: ({"num_labels": 3, "min_precision": -0.1}, []))
+_err("cls_bne_range", "cls", "BinaryNormalizedEntropy", lambda: ({}, _U(_x(4) + 1.5, _y(2, 4).float())))
+_err("cls_mean_weight_shape", "cls", "Mean", lambda: ({}, [((_x(4),), {"weight": _x(3)})]))
+_err("cls_sum_weight_shape", "cls", "Sum", lambda: ({}, [((_x(4),), {"weight": _x(3)})]))
+_err("cls_cat_dim", "cls", "Cat", lambda: ({"dim": 1}, _U(_x(4))))
+_err("cls_mse_shape", "cls", "MeanSquaredError", lambda: ({}, _U(_x(4), _x(5))))
+_err("cls_r2_shape", "cls", "R2Score", lambda: ({}, _U(_x(4), _x(5))))
+_err("cls_r2_multioutput", "cls", "R2Score", lambda: ({"multioutput": "x"}, []))
+_err("cls_psnr_shape", "cls", "PeakSignalNoiseRatio", lambda: ({}, _U(_x(1, 3, 4, 4), _x(1, 3, 4, 5))))
+_err("cls_ctr_shape", "cls", "ClickThroughRate", lambda: ({}, [((_y(2, 4),), {"weights": _x(3)})]))
+_err("cls_wc_shape", "cls", "WeightedCalibration", lambda: ({}, _U(_x(4), _x(5))))
+_err("cls_rr_shape", "cls", "ReciprocalRank", lambda: ({}, _U(_x(4, 4), _y(4, 3))))
+_err("cls_wer_len", "cls", "WordErrorRate", lambda: ({}, _U(["a b"], ["a b", "c"])))
+_err("cls_perplexity_shape", "cls", "Perplexity", lambda: ({}, _U(_x(2, 3, 5), _y(5, 2, 4))))
 
 
 # ----------------------------------------------------------------------------------------

@@ -11,7 +11,7 @@ import torch
 from torcheval_amd.metrics.functional.classification.binary_normalized_entropy import (
     _baseline_update,
     _binary_normalized_entropy_update,
-    _ne_range_check,
+    _ne_device_error,
 )
 from torcheval_amd.metrics.metric import Metric
 
@@ -61,7 +61,8 @@ class BinaryNormalizedEntropy(Metric[torch.Tensor]):
         if weight is not None:
             weight = weight.to(self.device)
         if input.is_cuda and self._err is None:
-            self._err = torch.zeros(1, dtype=torch.int32, device=input.device)
+            self._err = torch.zeros(6, dtype=torch.int32, device=input.device)
+        self._x_dtype = input.dtype
         cross_entropy, num_positive, num_examples = _binary_normalized_entropy_update(
             input, target, self.from_logits, self.num_tasks, weight,
             err=self._err if input.is_cuda else None,
@@ -72,9 +73,8 @@ class BinaryNormalizedEntropy(Metric[torch.Tensor]):
         return self
 
     def _check_device_errors(self) -> None:
-        if self._err is not None and int(self._err.item()) != 0:
-            self._err.zero_()
-            _ne_range_check(torch.tensor([2.0]), self.from_logits)
+        if self._err is not None:
+            _ne_device_error(self._err, self.from_logits, getattr(self, "_x_dtype", torch.float32))
 
     @torch.inference_mode()
     def compute(self: TNormalizedEntropy) -> torch.Tensor:

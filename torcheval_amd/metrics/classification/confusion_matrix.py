@@ -45,7 +45,10 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
         _confusion_matrix_param_check(num_classes, normalize)
         self.normalize = normalize
         self.num_classes = num_classes
+        # GPU updates: [flags, max bad target, max bad prediction] (int32, on device), and the
+        # dtypes the error message prints them with
         self._err: Optional[torch.Tensor] = None
+        self._err_dtypes = (torch.int64, torch.int64)
         self._add_state(
             "confusion_matrix",
             torch.zeros([num_classes, num_classes], device=self.device),
@@ -60,7 +63,8 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
         if native_cls(input, target, self.confusion_matrix) and input.shape[0] > 0:
             _confusion_matrix_shape_check(input, target, self.num_classes)
             if self._err is None:
-                self._err = torch.zeros(1, dtype=torch.int32, device=input.device)
+                self._err = torch.zeros(3, dtype=torch.int32, device=input.device)
+            self._err_dtypes = (target.dtype, input.dtype)
             cls_counts(input, target, num_classes=self.num_classes,
                        confusion=self.confusion_matrix.view(-1), err=self._err)
             return self
@@ -69,10 +73,15 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
         return self
 
     def _check_device_errors(self) -> None:
-        if self._err is not None and int(self._err.item()) != 0:
-            err = self._err.clone()
+        if self._err is None:
+            return
+        code, max_t, max_p = self._err.tolist()
+        if code != 0:
             self._err.zero_()
-            _raise_confusion_err(err, torch.tensor([-1]), torch.tensor([-1]), self.num_classes)
+            # same message as the reference's update-time check (its torch.max of the batch is
+            # the largest offending value, which the kernel records)
+            _raise_confusion_err(torch.tensor([code]), torch.tensor(max_p, dtype=self._err_dtypes[1]),
+                                 torch.tensor(max_t, dtype=self._err_dtypes[0]), self.num_classes)
 
     @torch.inference_mode()
     def compute(self: TMulticlassConfusionMatrix) -> torch.Tensor:

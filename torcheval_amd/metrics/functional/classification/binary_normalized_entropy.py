@@ -7,6 +7,7 @@ and the probability-range check in one pass; the range check is a device flag in
 the reference's host-synchronising ``input.max()/min()``).
 """
 
+import struct
 from typing import Optional, Tuple
 
 import torch
@@ -115,6 +116,29 @@ def _ne_shape_check(
         raise ValueError(
             f"`num_tasks = {num_tasks}`, `input`'s shape is expected to be ({num_tasks}, num_samples), but got shape ({input.shape})."
         )
+
+
+def _ne_device_error(err: torch.Tensor, from_logits: bool, dtype: torch.dtype) -> None:
+    """Raise a range violation that GPU class updates recorded in ``err`` (int32[6]: flag, pad,
+    then the kernel's order-preserving u64 keys of max / complemented min of the inputs) with
+    the reference's message.  The range is over every update since the last check, which is
+    the failing batch's own range when one update was bad (the reference raises at that
+    update)."""
+    vals = err.cpu()
+    if int(vals[0]) == 0:
+        return
+    err.zero_()
+    mask = (1 << 64) - 1
+    kmax, kmin = (k & mask for k in vals[2:6].view(torch.int64).tolist())
+
+    def decode(key: int) -> float:
+        u = key & ~(1 << 63) if key >> 63 else ~key & mask
+        return struct.unpack("<d", u.to_bytes(8, "little"))[0]
+
+    if kmax == 0 or kmin == 0:  # no range recorded: report the violation without one
+        _ne_range_check(torch.tensor([2.0]), from_logits)
+        return
+    _ne_range_check(torch.tensor([decode(~kmin & mask), decode(kmax)], dtype=dtype), from_logits)
 
 
 def _ne_range_check(input: torch.Tensor, from_logits: bool) -> None:
