@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -x "$@" > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -m pytest tests -m gpu -q --maxfail=25 "$@" > gpurun_out/pytest_gpu.log 2>&1
 rc=$?
 tail -30 gpurun_out/pytest_gpu.log
 [ $rc -ne 0 ] && exit $rc

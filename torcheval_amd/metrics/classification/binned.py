@@ -42,7 +42,7 @@ from torcheval_amd.metrics.functional.classification.precision_recall_curve impo
     _multiclass_precision_recall_curve_update_input_check,
     _multilabel_precision_recall_curve_update_input_check,
 )
-from torcheval_amd.metrics.functional.tensor_utils import _create_threshold_tensor
+from torcheval_amd.metrics.functional.tensor_utils import _create_threshold_tensor, _move_threshold
 from torcheval_amd.metrics.metric import Metric
 from torcheval_amd.ops.binned import binned_counts
 
@@ -53,7 +53,18 @@ def _as_threshold(threshold, device) -> torch.Tensor:
     return torch.as_tensor(threshold, device=device)
 
 
-class _BinnedCountsMetric(Metric):
+class _ThresholdFollowsDevice:
+    """Mixin: ``to()`` moves the threshold tensor with the states (the reference moves only
+    the states, so its binned metrics mix devices after ``.to()``)."""
+
+    def to(self, device, *args, **kwargs):
+        super().to(device, *args, **kwargs)
+        if isinstance(getattr(self, "threshold", None), torch.Tensor):
+            self.threshold = _move_threshold(self.threshold, self.device)
+        return self
+
+
+class _BinnedCountsMetric(_ThresholdFollowsDevice, Metric):
     """States num_tp / num_fp / num_fn of shape ``shape``; ``_views`` maps them to [T, C]."""
 
     def _init_counts(self, shape) -> None:
@@ -282,7 +293,7 @@ class MultilabelBinnedAUPRC(_BinnedCountsMetric):
         return auprc.mean() if self.average == "macro" else auprc
 
 
-class BinaryBinnedAUROC(SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
+class BinaryBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
     """(binned AUROC, thresholds) of ``[n]`` / ``[num_tasks, n]`` scores.
     Functional: ``binary_binned_auroc``."""
 
@@ -309,7 +320,7 @@ class BinaryBinnedAUROC(SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
         return _binary_binned_auroc_compute(*self._cat(), self.threshold)
 
 
-class MulticlassBinnedAUROC(SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
+class MulticlassBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
     """(one-vs-rest binned AUROC, thresholds).  Functional: ``multiclass_binned_auroc``."""
 
     def __init__(

@@ -19,6 +19,18 @@ def _is_uniform_linspace(t: torch.Tensor) -> bool:
     return _UNIFORM.get(id(t)) is t
 
 
+def _move_threshold(t: torch.Tensor, device: torch.device) -> torch.Tensor:
+    """``t`` on ``device``, keeping its validated / uniform-linspace markers."""
+    if t.device == device:
+        return t
+    moved = t.to(device)
+    if _VALIDATED.get(id(t)) is t:
+        _VALIDATED[id(moved)] = moved
+    if _UNIFORM.get(id(t)) is t:
+        _UNIFORM[id(moved)] = moved
+    return moved
+
+
 def _riemann_integral(x: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     """Left Riemann sum of y over the (descending) x grid: -sum((x[1:] - x[:-1]) * y[:-1])."""
     return -torch.sum((x[1:] - x[:-1]) * y[:-1])
