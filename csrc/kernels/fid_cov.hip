@@ -25,7 +25,13 @@
 //    the whole tile as 4 MFMA chains (2 x 2 register blocking, half the LDS operand reads):
 //    118 us - 176 VGPRs, and the waves still wait ~41% of their cycles on the per-stage
 //    operand fetch (SQ_WAIT_INST_ANY), so fewer LDS reads did not help; BK = 64: 104 us;
-//    8 x 8 super-tile enumeration (per-XCD runs needing ~16 instead of ~34 panels): 86 us.
+//    8 x 8 super-tile enumeration (per-XCD runs needing ~16 instead of ~34 panels): 86 us;
+//    register prefetch 2 / 3 / 4 stages deep: 83 / 83 / 84 us (so not global latency);
+//    k-contiguous [feature][sample] LDS operands (4x4 register transpose at staging) so one
+//    ds_read_b128 per operand feeds 4 MFMAs instead of one ds_read_b32 per MFMA: 89.6 vs
+//    82.5 us (so not LDS issue either).  What is left is block quantisation: D = 2048 gives
+//    528 tiles for 256 CUs, so 16 CUs run 3 tiles while the rest run 2 (~1.45x the mean);
+//    only a cross-block split of K (partials + fix-up pass) would even that out.
 #include "tea_common.h"
 #include "tea_kernels.h"
 
