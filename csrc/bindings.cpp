@@ -631,7 +631,7 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   a.rows = x.size(0);
   a.n = x.size(1);
   if (a.rows == 0 || a.n == 0) return;
-  a.tiles = tea::radix_sort_tiles(a.n);
+  a.tiles = tea::radix_sort_tiles(a.rows, a.n);
   const int64_t m = a.rows * a.n;
   Tensor ws = at::empty({4 * m + a.rows * 256 * a.tiles}, x.options().dtype(at::kInt));
   uint32_t* base = reinterpret_cast<uint32_t*>(ws.data_ptr<int32_t>());

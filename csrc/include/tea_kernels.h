@@ -283,7 +283,7 @@ struct RadixArgs {
   const float* in = nullptr;  // [rows, n] scores, rows at in_row_stride (unit column stride)
   int64_t in_row_stride = 0;
   int64_t rows = 0, n = 0;
-  int64_t tiles = 0;          // radix_sort_tiles(n)
+  int64_t tiles = 0;          // radix_sort_tiles(rows, n)
   uint32_t* keys0 = nullptr;  // ping-pong [rows * n]
   uint32_t* vals0 = nullptr;
   uint32_t* keys1 = nullptr;
@@ -307,7 +307,8 @@ struct RadixArgs {
   DType payload_dt = DType::f32;
   int64_t payload_row_stride = 0;
 };
-int64_t radix_sort_tiles(int64_t n);
+int radix_sort_rounds(int64_t rows, int64_t n);  // keys per thread of the tiling
+int64_t radix_sort_tiles(int64_t rows, int64_t n);
 int64_t radix_sort_groups(int64_t tiles);
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream);
 int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream);

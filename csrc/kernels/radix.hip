@@ -12,8 +12,8 @@
 //     1 KB, plus one atomic per non-zero digit into the count of its group of kGroup tiles) ->
 //     downsweep (each block forms its digit bases from the <= ngroups group counts and the
 //     < kGroup tile counts before it in its group - no scan launch: v2 ran a digit-parallel scan
-//     kernel between the two, 4 launches and ~20 us per 1M-key sort - then a stable scatter).  Tiles are 4096 keys (256 threads x 16 striped rounds, coalesced);
-//     each thread loads all 16 of its keys up front so the loads overlap (v1 loaded per round
+//     kernel between the two, 4 launches and ~20 us per 1M-key sort - then a stable scatter).  Tiles are 2048 or 4096 keys (256 threads x 8 or 16 rounds,
+//     coalesced, see radix_sort_rounds); each thread loads all of its keys up front so the loads overlap (v1 loaded per round
 //     and ran a single-block serial scan: ~60 us per pass at 1M).  Stable in-tile ranking uses wave64 "match" masks
 //     built from 8 ballots: each lane's rank among equal digits is popc(peers & lanes_below),
 //     per-wave digit counts are combined in wave order through LDS, so the scatter is stable
@@ -28,12 +28,12 @@ namespace tea {
 
 namespace {
 
-#ifndef TEA_RADIX_ROUNDS
-#define TEA_RADIX_ROUNDS 8
-#endif
 constexpr int kRT = 256;
-constexpr int kRounds = TEA_RADIX_ROUNDS;
-constexpr int kRTile = kRT * kRounds;  // 2048 keys per tile (8 rounds: 115 vs 132 us for a 1M binary_auroc over 16)
+// keys per thread (R) per tile of 256 * R keys, chosen per sort by radix_sort_rounds():
+// 1M keys: 8 rounds (2048-key tiles, 512 blocks) 100 us vs 114 us at 16 (half the blocks
+// leaves CUs idle); 100 rows x 100k: 16 rounds 402 vs 422 us (longer digit runs per tile,
+// so fuller write lines, and half the blocks' fixed cost)
+constexpr int kBigSort = 4 << 20;  // total keys from which 16 rounds win
 constexpr int kBins = 256;
 constexpr int kRWaves = kRT / 64;
 constexpr int kGroup = 32;  // tiles per group count
@@ -87,9 +87,11 @@ __device__ __forceinline__ uint32_t first_payload(const RadixArgs& a, int64_t ro
 }
 
 // keys of this thread's 16 striped rounds, loaded up front so the loads overlap
+template <int kRounds>
 __device__ __forceinline__ void load_tile(const RadixArgs& a, const uint32_t* keys_in, const uint32_t* vals_in,
                                           int pass, int64_t row, int tile, uint32_t (&k)[kRounds],
                                           uint32_t (&v)[kRounds], bool want_vals) {
+  constexpr int kRTile = kRT * kRounds;
   const int64_t t0 = static_cast<int64_t>(tile) * kRTile + threadIdx.x;
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
@@ -106,7 +108,9 @@ __device__ __forceinline__ void load_tile(const RadixArgs& a, const uint32_t* ke
 // hist layout: [row][tile][digit] (each block writes 1 KB contiguously).  Measured: the
 // digit-major alternative (coalesced scan reads, strided upsweep stores) made the scan 12%
 // faster and the upsweep 27% slower - 2.40 vs 2.31 ms per 20 1M-sample binary_auroc calls
+template <int kRounds>
 __global__ __launch_bounds__(kRT) void radix_upsweep_kernel(RadixArgs a, const uint32_t* keys_in, int pass) {
+  constexpr int kRTile = kRT * kRounds;
   const int64_t row = blockIdx.y;
   const int tile = blockIdx.x;
   const int shift = 8 * pass;
@@ -147,15 +151,16 @@ __global__ __launch_bounds__(kRT) void radix_upsweep_kernel(RadixArgs a, const u
 // addresses of each digit run (coalesced; v1 scattered 4-byte writes straight to HBM).
 // VMODE: 0 = values from the previous pass, 1 = source index (pass 0), 2 = caller payload of
 // dtype PT (pass 0); separate instantiations keep the payload conversion out of passes 1-3
-template <int VMODE, typename PT = uint32_t, int KIND = 0>
+template <int kRounds, int VMODE, typename PT = uint32_t, int KIND = 0>
 __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const uint32_t* keys_in,
                                                               const uint32_t* vals_in, uint32_t* keys_out,
                                                               uint32_t* vals_out, int pass) {
+  constexpr int kRTile = kRT * kRounds;
   const int64_t row = blockIdx.y;
   const int tile = blockIdx.x;
   const int shift = 8 * pass;
   const bool last = pass == 3;
-  constexpr int kSub = kRTile / kRWaves;  // 1024 keys per wave
+  constexpr int kSub = kRTile / kRWaves;  // keys per wave
   __shared__ uint32_t base[kBins];        // global (row-relative) start of each digit's run
   __shared__ uint32_t tstart[kBins];      // start of each digit inside the sorted tile
   __shared__ uint32_t wc[kRWaves][kBins]; // per-wave digit counts -> per-wave offsets
@@ -303,7 +308,12 @@ __global__ __launch_bounds__(kRT) void transpose_kernel(const float* in, int64_t
 
 }  // namespace
 
-int64_t radix_sort_tiles(int64_t n) { return (n + kRTile - 1) / kRTile; }
+int radix_sort_rounds(int64_t rows, int64_t n) { return rows * n >= kBigSort ? 16 : 8; }
+
+int64_t radix_sort_tiles(int64_t rows, int64_t n) {
+  const int64_t tile = static_cast<int64_t>(kRT) * radix_sort_rounds(rows, n);
+  return (n + tile - 1) / tile;
+}
 
 int64_t radix_sort_groups(int64_t tiles) { return (tiles + kGroup - 1) / kGroup; }
 
@@ -314,17 +324,19 @@ int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, f
   return static_cast<int>(hipGetLastError());
 }
 
-int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
-  if (a.n <= 0 || a.rows <= 0) return 0;
+namespace {
+
+template <int R>
+int radix_passes(const RadixArgs& a, hipStream_t stream) {
   const dim3 grid(static_cast<unsigned>(a.tiles), static_cast<unsigned>(a.rows));
   const uint32_t* kin[4] = {nullptr, a.keys0, a.keys1, a.keys0};
   const uint32_t* vin[4] = {nullptr, a.vals0, a.vals1, a.vals0};
   uint32_t* kout[4] = {a.keys0, a.keys1, a.keys0, nullptr};
   uint32_t* vout[4] = {a.vals0, a.vals1, a.vals0, nullptr};
   for (int p = 0; p < 4; ++p) {
-    hipLaunchKernelGGL(radix_upsweep_kernel, grid, dim3(kRT), 0, stream, a, kin[p], p);
+    hipLaunchKernelGGL(radix_upsweep_kernel<R>, grid, dim3(kRT), 0, stream, a, kin[p], p);
 #define TEA_DOWNSWEEP(...) \
-  hipLaunchKernelGGL((radix_downsweep_kernel<__VA_ARGS__>), grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p)
+  hipLaunchKernelGGL((radix_downsweep_kernel<R, __VA_ARGS__>), grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p)
     if (p > 0) {
       TEA_DOWNSWEEP(0);
     } else if (a.payload_kind == 0) {
@@ -347,6 +359,14 @@ int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
 #undef TEA_DOWNSWEEP
   }
   return static_cast<int>(hipGetLastError());
+}
+
+}  // namespace
+
+int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
+  if (a.n <= 0 || a.rows <= 0) return 0;
+  if (a.tiles != radix_sort_tiles(a.rows, a.n)) return -2;  // workspace sized for another tiling
+  return radix_sort_rounds(a.rows, a.n) == 16 ? radix_passes<16>(a, stream) : radix_passes<8>(a, stream);
 }
 
 }  // namespace tea
