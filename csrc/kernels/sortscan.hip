@@ -279,13 +279,15 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   __shared__ int s_hmax[kT / 64], s_tmin[kT / 64];
   __shared__ int64_t s_pos;
 
+  // every global load of the tile is issued up front (one round trip): the thread's keys and
+  // (a, b), its outer neighbour keys, and (fused) its share of the preceding tile totals
   const int j0 = threadIdx.x * kPer;
+  const int64_t i0 = base + j0;
   K key[kPer];
   float2 v[kPer];
-  double la = 0.0, lb = 0.0;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int64_t i = base + j0 + k;
+    const int64_t i = i0 + k;
     if (j0 + k < tile_n) {
       key[k] = key_at<K>(a, r, i);
       v[k] = load_ab<DIRECT>(a, ab, r, i);
@@ -293,14 +295,44 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
       key[k] = K(0);
       v[k] = make_float2(0.f, 0.f);
     }
+  }
+  const bool live = j0 < tile_n;
+  const K pk0 = (live && i0 > 0) ? key_at<K>(a, r, i0 - 1) : K(0);
+  const K nk_last = (live && i0 + kPer < a.n) ? key_at<K>(a, r, i0 + kPer) : K(0);
+  double pa = 0.0, pb = 0.0;
+  if constexpr (FUSED) {
+    const D2* ts = reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
+    for (int t = threadIdx.x; t < static_cast<int>(blockIdx.x); t += kT) {
+      const D2 q = ts[t];
+      pa += q.x;
+      pb += q.y;
+    }
+  } else {  // tile_scan's table (one broadcast load; a block scan here cost 53 -> 62 us at 100 x 100k)
+    const D2 q = reinterpret_cast<const D2*>(a.tstart)[static_cast<int64_t>(r) * ntiles + blockIdx.x];
+    pa = q.x;
+    pb = q.y;
+  }
+  double la = 0.0, lb = 0.0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
     la += v[k].x;
     lb += v[k].y;
   }
+  // tie groups straddling the tile edges: thread 0 holds key(base) and key(base - 1), the
+  // thread owning the tile's last sample holds it and the key after the tile
+  if (threadIdx.x == 0) {
+    s_flags[0] = (base > 0 && key[0] == pk0) ? 1 : 0;
+    s_bound[0] = s_bound[1] = s_bound[2] = 0.0;
+  }
+  if (j0 + kPer == tile_n) s_flags[1] = (base + tile_n < a.n && key[kPer - 1] == nk_last) ? 1 : 0;
+  if (j0 < tile_n && tile_n < j0 + kPer) s_flags[1] = 0;  // ragged last tile: nothing follows
   D2 tot;
   const D2 ex = block_excl_scan(D2{la, lb}, lds, tot);
-  const D2 t0 = tile_start<FUSED>(a, r, blockIdx.x, ntiles, lds);
-  const K prev_key = (base > 0) ? key_at<K>(a, r, base - 1) : K(0);
-  const K next_key = (base + tile_n < a.n) ? key_at<K>(a, r, base + tile_n) : K(0);
+  D2 t0{pa, pb};
+  if constexpr (FUSED) {
+    block_excl_scan(D2{pa, pb}, lds, t0);  // block total = the tiles before this one
+    if (a.init) t0 = d2add(t0, D2{a.init[2 * r], a.init[2 * r + 1]});
+  }
 
   bool headf[kPer], tailf[kPer];
   int my_head = -1, my_tail = kTile;
@@ -310,10 +342,8 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
     const int64_t i = base + j;
     bool h = false, tl = false;
     if (j < tile_n) {
-      const K pk = (k > 0) ? key[k - 1] : ((j == 0) ? prev_key : key_at<K>(a, r, i - 1));
-      const K nk = (k + 1 < kPer && j + 1 < tile_n)
-                       ? key[k + 1]
-                       : ((j + 1 == tile_n) ? next_key : key_at<K>(a, r, i + 1));
+      const K pk = (k > 0) ? key[k - 1] : pk0;
+      const K nk = (k + 1 < kPer) ? key[k + 1] : nk_last;
       h = (i == 0) || !(pk == key[k]);
       tl = (i == a.n - 1) || !(nk == key[k]);
     }
@@ -340,11 +370,6 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   const int tin = wave_incl_min_rev(my_tail);
   if (lane_id() == 63) s_hmax[w] = hin;
   if (lane_id() == 0) s_tmin[w] = tin;
-  if (threadIdx.x == 0) {
-    s_flags[0] = (base > 0 && key_at<K>(a, r, base) == prev_key) ? 1 : 0;
-    s_flags[1] = (base + tile_n < a.n && key_at<K>(a, r, base + tile_n - 1) == next_key) ? 1 : 0;
-    s_bound[0] = s_bound[1] = s_bound[2] = 0.0;
-  }
   __syncthreads();
   int hmax_before = -1, tmin_after = kTile;
   for (int k = 0; k < w; ++k) hmax_before = max(hmax_before, s_hmax[k]);
