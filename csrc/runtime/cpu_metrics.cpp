@@ -49,8 +49,8 @@ int64_t count_correct(const T* x, int64_t n, int64_t c, int64_t ld, const int64_
   return correct;
 }
 
-// input [N, C] float32/float64 scores (or [N] int64 labels), target [N] int64 -> 0-d float32
-at::Tensor cpu_micro_accuracy(const at::Tensor& input, const at::Tensor& target, int64_t k) {
+// correct predictions of input [N, C] float32/float64 scores (or [N] int64 labels) vs target [N] int64
+int64_t count_micro(const at::Tensor& input, const at::Tensor& target, int64_t k) {
   TORCH_CHECK(!input.is_cuda() && !target.is_cuda(), "cpu_micro_accuracy: CPU tensors only");
   TORCH_CHECK(target.dim() == 1 && target.scalar_type() == at::kLong, "cpu_micro_accuracy: target [N] int64");
   const int64_t n = target.size(0);
@@ -73,14 +73,38 @@ at::Tensor cpu_micro_accuracy(const at::Tensor& input, const at::Tensor& target,
     else
       TORCH_CHECK(false, "cpu_micro_accuracy: float32/float64 scores");
   }
+  return correct;
+}
+
+// -> 0-d float32 micro accuracy
+at::Tensor cpu_micro_accuracy(const at::Tensor& input, const at::Tensor& target, int64_t k) {
+  const int64_t correct = count_micro(input, target, k);
+  const int64_t n = target.size(0);
   at::Tensor out = at::empty({}, at::TensorOptions().dtype(at::kFloat));
   out.data_ptr<float>()[0] = static_cast<float>(static_cast<double>(correct) / static_cast<double>(n));
   return out;
 }
 
+// class-API update: correct / total (0-d float32 states) += this batch's counts, in place
+void cpu_micro_accuracy_update(const at::Tensor& input, const at::Tensor& target, int64_t k, at::Tensor& correct,
+                               at::Tensor& total) {
+  TORCH_CHECK(correct.dim() == 0 && total.dim() == 0 && correct.scalar_type() == at::kFloat &&
+                  total.scalar_type() == at::kFloat && !correct.is_cuda() && !total.is_cuda(),
+              "cpu_micro_accuracy_update: 0-d float32 CPU states");
+  const int64_t c = count_micro(input, target, k);
+  const int64_t n = target.size(0);
+  // float32 adds, like the reference's ``num_correct += mask.sum()`` on float32 states
+  correct.data_ptr<float>()[0] += static_cast<float>(c);
+  total.data_ptr<float>()[0] += static_cast<float>(n);
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
+  m.def("cpu_micro_accuracy_update", &cpu_micro_accuracy_update,
+        "host fast path of MulticlassAccuracy.update (micro): counts added into the states",
+        pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("k"), pybind11::arg("correct"),
+        pybind11::arg("total"));
   m.def("cpu_micro_accuracy", &cpu_micro_accuracy,
         "host fast path: fused argmax / top-k test + micro accuracy for small CPU batches",
         pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("k") = 1);

@@ -180,3 +180,38 @@ def test_topk_multilabel_param_errors() -> None:
         TopKMultilabelAccuracy(k=1)
     with pytest.raises(ValueError, match="`criteria` was not in the allowed value"):
         TopKMultilabelAccuracy(criteria="x")
+
+
+@pytest.mark.parametrize("case", ["scores", "f64", "labels", "topk", "nan_rows", "strided_target"])
+def test_cpu_fast_path_matches_aten(case) -> None:
+    """Small CPU batches take the fused C++ update (functional and class): same states and
+    result as the ATen update, including the NaN-is-max argmax and top-k."""
+    from torcheval_amd.metrics.functional import multiclass_accuracy
+    from torcheval_amd.metrics.functional.classification.accuracy import _multiclass_accuracy_update_aten
+
+    g = torch.Generator().manual_seed(len(case))
+    x = torch.rand(64, 7, generator=g)
+    y = torch.randint(0, 7, (64,), generator=g)
+    k = 1
+    if case == "f64":
+        x = x.double()
+    elif case == "labels":
+        x = torch.randint(0, 7, (64,), generator=g)
+    elif case == "topk":
+        k = 3
+    elif case == "nan_rows":
+        x[::5, 2] = float("nan")
+    elif case == "strided_target":
+        y = torch.randint(0, 7, (128,), generator=g)[::2]
+    fast = MulticlassAccuracy(k=k)
+    correct, total = torch.zeros(()), torch.zeros(())
+    for _ in range(3):
+        fast.update(x, y)
+        n_c, n_t = _multiclass_accuracy_update_aten(x, y, "micro", None, k)
+        correct += n_c
+        total += n_t
+    assert fast.num_correct.dtype == torch.float32
+    torch.testing.assert_close(fast.num_correct, correct)
+    torch.testing.assert_close(fast.num_total, total)
+    torch.testing.assert_close(fast.compute(), correct / total)
+    torch.testing.assert_close(multiclass_accuracy(x, y, k=k), n_c / n_t)

@@ -15,6 +15,7 @@ from typing import Iterable, Optional, TypeVar
 import torch
 
 from torcheval_amd.metrics.functional.classification.accuracy import (
+    _CPU_FAST_MAX,
     _accuracy_compute,
     _accuracy_param_check,
     _accuracy_update_input_check,
@@ -27,9 +28,10 @@ from torcheval_amd.metrics.functional.classification.accuracy import (
     _topk_multilabel_accuracy_param_check,
     _topk_multilabel_accuracy_update,
     _topk_multilabel_accuracy_update_input_check,
+    _cpu_fast_ok,
 )
 from torcheval_amd.metrics.metric import Metric
-from torcheval_amd.ops import use_native
+from torcheval_amd.ops import native, use_native
 from torcheval_amd.ops.classification import (
     binary_counts,
     cls_counts,
@@ -95,6 +97,17 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         if target.device != dev:
             target = target.to(dev)
         _accuracy_update_input_check(input, target, self.num_classes, self.k)
+        if (
+            self.average == "micro"
+            and not input.is_cuda
+            and input.numel() <= _CPU_FAST_MAX
+            and self.num_correct.dtype == torch.float32
+            and _cpu_fast_ok(input, target, self.k, None)
+        ):
+            # small CPU batches (BASELINE config 1 shape): one fused C++ call accumulates the
+            # counts into the states instead of ~6 ATen dispatches
+            native().cpu_micro_accuracy_update(input, target, self.k, self.num_correct, self.num_total)
+            return self
         if (
             use_native(input)
             and cls_counts_supported(input, target)
