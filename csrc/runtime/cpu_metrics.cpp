@@ -98,9 +98,149 @@ void cpu_micro_accuracy_update(const at::Tensor& input, const at::Tensor& target
   total.data_ptr<float>()[0] += static_cast<float>(n);
 }
 
+// ---- class-count updates (the CPU twin of the K1 kernel's contract, ops.classification) ----
+
+int64_t label_at(const at::Tensor& t, int64_t i) {
+  return t.scalar_type() == at::kLong ? t.data_ptr<int64_t>()[i * t.stride(0)]
+                                      : static_cast<int64_t>(t.data_ptr<int32_t>()[i * t.stride(0)]);
+}
+
+bool label_dtype(const at::Tensor& t) { return t.scalar_type() == at::kLong || t.scalar_type() == at::kInt; }
+
+// every target (and 1-D label input) in [0, num_classes): the CPU counts then never skip a row
+bool cpu_labels_valid(const at::Tensor& input, const at::Tensor& target, int64_t num_classes) {
+  if (input.is_cuda() || target.is_cuda() || target.dim() != 1 || !label_dtype(target)) return false;
+  const int64_t n = target.size(0);
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t y = label_at(target, i);
+    if (y < 0 || y >= num_classes) return false;
+  }
+  if (input.dim() == 1) {
+    if (!label_dtype(input) || input.size(0) != n) return false;
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t p = label_at(input, i);
+      if (p < 0 || p >= num_classes) return false;
+    }
+  }
+  return true;
+}
+
+// torch.argmax of one row: first index of the max, NaN counts as the max
+template <typename T>
+int64_t row_argmax(const T* row, int64_t c) {
+  int64_t best = 0;
+  T bv = row[0];
+  if (std::isnan(static_cast<double>(bv))) return 0;
+  for (int64_t j = 1; j < c; ++j) {
+    const T v = row[j];
+    if (std::isnan(static_cast<double>(v))) return j;
+    if (v > bv) {
+      bv = v;
+      best = j;
+    }
+  }
+  return best;
+}
+
+float* opt_f32(const c10::optional<at::Tensor>& t, int64_t numel, const char* name) {
+  if (!t.has_value()) return nullptr;
+  TORCH_CHECK(!t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == numel,
+              "cpu_cls_counts: ", name, " must be a contiguous float32 CPU tensor of ", numel, " elements");
+  return t->data_ptr<float>();
+}
+
+// Same arguments and semantics as the HIP ``cls_counts`` (csrc/bindings.cpp): per row the
+// prediction (argmax of [N, C] scores or the [N] label) or, for k > 1, the rank-of-target
+// test; then micro counts and the class histograms, accumulated in float32.  Rows with an
+// out-of-range label are skipped and flagged in ``err`` as on the GPU (callers validate first
+// with cpu_labels_valid, so that only happens on direct use).
+void cpu_cls_counts(const at::Tensor& input, const at::Tensor& target, int64_t k, int64_t num_classes,
+                    const c10::optional<at::Tensor>& micro_correct, const c10::optional<at::Tensor>& micro_total,
+                    const c10::optional<at::Tensor>& cls_correct, const c10::optional<at::Tensor>& cls_label,
+                    const c10::optional<at::Tensor>& cls_pred, const c10::optional<at::Tensor>& confusion,
+                    const c10::optional<at::Tensor>& err, int64_t /*max_blocks*/,
+                    const c10::optional<at::Tensor>& micro_incorrect, const c10::optional<at::Tensor>& micro_total2,
+                    const c10::optional<at::Tensor>& cls_fp) {
+  TORCH_CHECK(!input.is_cuda() && !target.is_cuda(), "cpu_cls_counts: CPU tensors only");
+  TORCH_CHECK(target.dim() == 1 && label_dtype(target), "cpu_cls_counts: target [N] int64 / int32");
+  const int64_t n = target.size(0), C = num_classes;
+  const bool scores = input.dim() == 2;
+  if (scores) {
+    TORCH_CHECK(input.size(0) == n && input.stride(1) == 1 &&
+                    (input.scalar_type() == at::kFloat || input.scalar_type() == at::kDouble),
+                "cpu_cls_counts: scores [N, C] float32 / float64 with unit column stride");
+    TORCH_CHECK(C == input.size(1), "cpu_cls_counts: num_classes must match input.size(1)");
+  } else {
+    TORCH_CHECK(input.dim() == 1 && input.size(0) == n && label_dtype(input) && k == 1,
+                "cpu_cls_counts: labels [N] int64 / int32 (k = 1)");
+  }
+  float* mc = opt_f32(micro_correct, 1, "micro_correct");
+  float* mt = opt_f32(micro_total, 1, "micro_total");
+  float* mi = opt_f32(micro_incorrect, 1, "micro_incorrect");
+  float* mt2 = opt_f32(micro_total2, 1, "micro_total2");
+  float* cc = opt_f32(cls_correct, C, "cls_correct");
+  float* cl = opt_f32(cls_label, C, "cls_label");
+  float* cp = opt_f32(cls_pred, C, "cls_pred");
+  float* cf = opt_f32(cls_fp, C, "cls_fp");
+  float* cm = opt_f32(confusion, C * C, "confusion");
+  TORCH_CHECK(!(k > 1 && (cp || cm || cf)), "cpu_cls_counts: predictions are undefined for k > 1");
+  int* eb = nullptr;
+  if (err.has_value()) {
+    TORCH_CHECK(!err->is_cuda() && err->scalar_type() == at::kInt && err->numel() >= 1, "cpu_cls_counts: err int32");
+    eb = err->data_ptr<int>();
+  }
+  int64_t correct_rows = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t t = label_at(target, i);
+    const bool t_ok = t >= 0 && t < C;
+    int64_t pred = -1;
+    bool correct;
+    if (!scores) {
+      pred = label_at(input, i);
+      correct = pred == t;
+    } else if (k == 1) {
+      pred = input.scalar_type() == at::kFloat
+                 ? row_argmax(input.data_ptr<float>() + i * input.stride(0), C)
+                 : row_argmax(input.data_ptr<double>() + i * input.stride(0), C);
+      correct = pred == t;
+    } else {
+      int64_t above = 0;
+      if (t_ok) {
+        if (input.scalar_type() == at::kFloat) {
+          const float* row = input.data_ptr<float>() + i * input.stride(0);
+          for (int64_t j = 0; j < C; ++j) above += row[j] > row[t];
+        } else {
+          const double* row = input.data_ptr<double>() + i * input.stride(0);
+          for (int64_t j = 0; j < C; ++j) above += row[j] > row[t];
+        }
+      }
+      correct = t_ok && above < k;
+    }
+    correct_rows += correct;
+    const bool p_ok = pred >= 0 && pred < C;
+    if (eb) {
+      if (!t_ok) *eb |= 1;
+      if (!p_ok && (cp || cm || (cf && !correct))) *eb |= 2;
+    }
+    if (t_ok) {
+      if (cc && correct) cc[t] += 1.f;
+      if (cl) cl[t] += 1.f;
+    }
+    if (p_ok && cp) cp[pred] += 1.f;
+    if (p_ok && cf && !correct) cf[pred] += 1.f;
+    if (t_ok && p_ok && cm) cm[t * C + pred] += 1.f;
+  }
+  if (mc) *mc += static_cast<float>(correct_rows);
+  if (mi) *mi += static_cast<float>(n - correct_rows);
+  if (mt) *mt += static_cast<float>(n);
+  if (mt2) *mt2 += static_cast<float>(n);
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
+  m.def("cpu_labels_valid", &cpu_labels_valid, "all targets / label predictions in [0, num_classes)");
+  m.def("cpu_cls_counts", &cpu_cls_counts, "host twin of cls_counts for small CPU batches");
   m.def("cpu_micro_accuracy_update", &cpu_micro_accuracy_update,
         "host fast path of MulticlassAccuracy.update (micro): counts added into the states",
         pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("k"), pybind11::arg("correct"),

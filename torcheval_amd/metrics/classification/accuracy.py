@@ -35,7 +35,7 @@ from torcheval_amd.ops import native, use_native
 from torcheval_amd.ops.classification import (
     binary_counts,
     cls_counts,
-    cls_counts_supported,
+    native_cls,
     multilabel_counts,
     native_multilabel,
 )
@@ -108,11 +108,8 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
             # counts into the states instead of ~6 ATen dispatches
             native().cpu_micro_accuracy_update(input, target, self.k, self.num_correct, self.num_total)
             return self
-        if (
-            use_native(input)
-            and cls_counts_supported(input, target)
-            and self.num_correct.dtype == torch.float32
-        ):
+        if native_cls(input, target, self.num_correct, self.num_total,
+                      num_classes=None if self.average == "micro" else self.num_classes):
             if self.average == "micro":
                 if self.k > 1 and self._err is None:
                     self._err = torch.zeros(1, dtype=torch.int32, device=dev)

@@ -60,7 +60,7 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
     ) -> TMulticlassConfusionMatrix:
         input = input.to(self.device)
         target = target.to(self.device)
-        if native_cls(input, target, self.confusion_matrix) and input.shape[0] > 0:
+        if native_cls(input, target, self.confusion_matrix, num_classes=self.num_classes) and input.shape[0] > 0:
             _confusion_matrix_shape_check(input, target, self.num_classes)
             if self._err is None:
                 self._err = torch.zeros(3, dtype=torch.int32, device=input.device)

@@ -8,7 +8,8 @@ from typing import Optional
 
 import torch
 
-from torcheval_amd.ops import MAX_BLOCKS, native, use_native
+import torcheval_amd.ops as _ops
+from torcheval_amd.ops import MAX_BLOCKS, native, native_loaded, use_native
 
 _SCORE_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
 _LABEL_DTYPES = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
@@ -26,14 +27,40 @@ def cls_counts_supported(input: torch.Tensor, target: torch.Tensor) -> bool:
     return False
 
 
-def native_cls(input: torch.Tensor, target: torch.Tensor, *states: torch.Tensor) -> bool:
-    """True when (input, target) go through K1 and every destination state is float32."""
-    return (
-        use_native(input)
-        and target.is_cuda
-        and cls_counts_supported(input, target)
-        and all(s.dtype == torch.float32 and s.is_contiguous() for s in states)
-    )
+# CPU batches up to this many scores take the host twin of K1 (csrc/runtime/cpu_metrics.cpp):
+# one C++ call instead of ~6-10 ATen dispatches, which dominate small updates
+_CPU_MAX = 1 << 16
+
+
+def _cpu_cls(input: torch.Tensor, target: torch.Tensor, num_classes: Optional[int]) -> bool:
+    if input.is_cuda or target.is_cuda or _ops.DISABLE_HIP or not native_loaded():
+        return False
+    if input.numel() > _CPU_MAX or target.dim() != 1 or target.dtype not in (torch.int64, torch.int32):
+        return False
+    if input.dim() == 2:
+        if input.dtype not in (torch.float32, torch.float64) or input.stride(1) != 1 or input.requires_grad:
+            return False
+        c = input.shape[1] if num_classes is None else num_classes
+        if c != input.shape[1] or input.shape[0] != target.shape[0]:
+            return False
+    elif input.dim() == 1 and input.dtype in (torch.int64, torch.int32) and num_classes:
+        c = num_classes
+    else:
+        return False
+    # out-of-range labels take the ATen path, which raises the reference's own error
+    return bool(native().cpu_labels_valid(input, target, int(c)))
+
+
+def native_cls(
+    input: torch.Tensor, target: torch.Tensor, *states: torch.Tensor, num_classes: Optional[int] = None
+) -> bool:
+    """True when (input, target) go through K1 (ROCm) or its host twin (small CPU batches with
+    valid labels) and every destination state is float32."""
+    if not all(s.dtype == torch.float32 and s.is_contiguous() for s in states):
+        return False
+    if input.is_cuda:
+        return use_native(input) and target.is_cuda and cls_counts_supported(input, target)
+    return _cpu_cls(input, target, num_classes)
 
 
 def native_binary(input: torch.Tensor, target: torch.Tensor, *states: torch.Tensor) -> bool:
@@ -73,7 +100,8 @@ def cls_counts(
         target = target.contiguous()
     if input.dim() == 2 and num_classes <= 0:
         num_classes = input.shape[1]
-    native().cls_counts(
+    op = native().cls_counts if input.is_cuda else native().cpu_cls_counts
+    op(
         input,
         target,
         int(k),
