@@ -10,8 +10,10 @@
 #include <pybind11/pybind11.h>
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <vector>
 
 #include "tea_runtime.h"
 
@@ -236,9 +238,81 @@ void cpu_cls_counts(const at::Tensor& input, const at::Tensor& target, int64_t k
   if (mt2) *mt2 += static_cast<float>(n);
 }
 
+// ---- binned counts (the CPU twin of K4 for small batches, ops.binned) ----
+
+double as_double(const at::Tensor& t, int64_t off) {
+  switch (t.scalar_type()) {
+    case at::kLong: return static_cast<double>(t.data_ptr<int64_t>()[off]);
+    case at::kInt: return static_cast<double>(t.data_ptr<int32_t>()[off]);
+    case at::kBool: return t.data_ptr<bool>()[off] ? 1.0 : 0.0;
+    case at::kByte: return static_cast<double>(t.data_ptr<uint8_t>()[off]);
+    case at::kFloat: return static_cast<double>(t.data_ptr<float>()[off]);
+    case at::kDouble: return t.data_ptr<double>()[off];
+    default: TORCH_CHECK(false, "cpu_binned_counts: unsupported target dtype ", t.scalar_type());
+  }
+  return 0.0;
+}
+
+template <typename S>
+void binned_hist(const at::Tensor& scores, const at::Tensor& target, const at::Tensor& thr, int64_t mode,
+                 std::vector<int64_t>& hist) {
+  const int64_t n = scores.size(0), C = scores.size(1), T = thr.size(0);
+  std::vector<S> th(T);  // thresholds in the score dtype, as thr.to(scores.dtype)
+  for (int64_t k = 0; k < T; ++k) th[k] = static_cast<S>(as_double(thr, k * thr.stride(0)));
+  const S* x = scores.data_ptr<S>();
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t lab = mode == 1 ? static_cast<int64_t>(as_double(target, i * target.stride(0))) : 0;
+    for (int64_t c = 0; c < C; ++c) {
+      const S v = x[i * scores.stride(0) + c * scores.stride(1)];
+      // searchsorted(thr, v, right=True): thresholds <= v; NaN sorts past every threshold
+      int64_t b = T;
+      if (!std::isnan(static_cast<double>(v))) b = std::upper_bound(th.begin(), th.end(), v) - th.begin();
+      const bool pos = mode == 1 ? lab == c
+                                 : as_double(target, i * target.stride(0) + c * target.stride(1)) == 1.0;
+      ++hist[(b * C + c) * 2 + (pos ? 1 : 0)];
+    }
+  }
+}
+
+// scores [n, C] float32 / float64 (any strides), target [n, C] (mode 0) or [n] labels (mode 1),
+// thr [T] sorted; tp / fp / fn [T, C] float32 views += the binned counts (tp[k] = positives
+// with score >= thr[k], fp the negatives, fn = positives - tp), as _binned_counts_aten
+void cpu_binned_counts(const at::Tensor& scores, const at::Tensor& target, const at::Tensor& thr, int64_t mode,
+                       at::Tensor& tp, at::Tensor& fp, at::Tensor& fn) {
+  TORCH_CHECK(!scores.is_cuda() && !target.is_cuda() && !thr.is_cuda(), "cpu_binned_counts: CPU tensors only");
+  TORCH_CHECK(scores.dim() == 2 && thr.dim() == 1, "cpu_binned_counts: scores [n, C], thr [T]");
+  const int64_t n = scores.size(0), C = scores.size(1), T = thr.size(0);
+  TORCH_CHECK(mode == 1 ? (target.dim() == 1 && target.size(0) == n)
+                        : (target.dim() == 2 && target.size(0) == n && target.size(1) == C),
+              "cpu_binned_counts: target shape");
+  for (const at::Tensor* o : {&tp, &fp, &fn})
+    TORCH_CHECK(o->scalar_type() == at::kFloat && !o->is_cuda() && o->dim() == 2 && o->size(0) == T &&
+                    o->size(1) == C, "cpu_binned_counts: outputs must be float32 [T, C]");
+  std::vector<int64_t> hist((T + 1) * C * 2, 0);
+  if (scores.scalar_type() == at::kFloat) binned_hist<float>(scores, target, thr, mode, hist);
+  else if (scores.scalar_type() == at::kDouble) binned_hist<double>(scores, target, thr, mode, hist);
+  else TORCH_CHECK(false, "cpu_binned_counts: float32 / float64 scores");
+  float* ptp = tp.data_ptr<float>();
+  float* pfp = fp.data_ptr<float>();
+  float* pfn = fn.data_ptr<float>();
+  for (int64_t c = 0; c < C; ++c) {
+    int64_t pos_all = 0;
+    for (int64_t b = 0; b <= T; ++b) pos_all += hist[(b * C + c) * 2 + 1];
+    int64_t sp = 0, sn = 0;  // suffix sums over bins > k
+    for (int64_t k = T - 1; k >= 0; --k) {
+      sp += hist[((k + 1) * C + c) * 2 + 1];
+      sn += hist[((k + 1) * C + c) * 2];
+      ptp[k * tp.stride(0) + c * tp.stride(1)] += static_cast<float>(sp);
+      pfp[k * fp.stride(0) + c * fp.stride(1)] += static_cast<float>(sn);
+      pfn[k * fn.stride(0) + c * fn.stride(1)] += static_cast<float>(pos_all - sp);
+    }
+  }
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
+  m.def("cpu_binned_counts", &cpu_binned_counts, "host twin of binned_counts for small CPU batches");
   m.def("cpu_labels_valid", &cpu_labels_valid, "all targets / label predictions in [0, num_classes)");
   m.def("cpu_cls_counts", &cpu_cls_counts, "host twin of cls_counts for small CPU batches");
   m.def("cpu_micro_accuracy_update", &cpu_micro_accuracy_update,

@@ -35,11 +35,27 @@ def binned_counts(
             t = t.to(torch.uint8)
         native().binned_counts(scores, t, thr.to(torch.float32).contiguous(), int(mode), *out, uniform=int(uniform))
         return out
+    if _cpu_binned(scores, target, thr, mode):
+        # small CPU batches: one C++ call (the ATen chain below is ~10 dispatches)
+        native().cpu_binned_counts(scores, target, thr, int(mode), *out)
+        return out
     tp, fp, fn = _binned_counts_aten(scores, target, thr, mode)
     out[0].add_(tp)
     out[1].add_(fp)
     out[2].add_(fn)
     return out
+
+
+def _cpu_binned(scores: torch.Tensor, target: torch.Tensor, thr: torch.Tensor, mode: int) -> bool:
+    import torcheval_amd.ops as ops
+
+    if scores.is_cuda or target.is_cuda or thr.is_cuda or ops.DISABLE_HIP or not ops.native_loaded():
+        return False
+    if scores.numel() > (1 << 16) or scores.dtype not in (torch.float32, torch.float64):
+        return False
+    ok_t = (torch.int64, torch.int32) if mode == 1 else (torch.int64, torch.int32, torch.bool, torch.uint8,
+                                                         torch.float32, torch.float64)
+    return target.dtype in ok_t and thr.dtype in (torch.float32, torch.float64)
 
 
 def _binned_counts_aten(
