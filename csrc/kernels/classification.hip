@@ -49,6 +49,7 @@ __device__ __forceinline__ float h16(uint16_t b) {
 template <int KIND, int VEC>
 __device__ __forceinline__ void load_vec(const void* row, int col, float (&v)[VEC]) {
   if constexpr (KIND == 0 && VEC == 4) {
+    // plain loads: __builtin_nontemporal_load here measured 116-117k vs 122-124k updates/s
     const float4 x = *reinterpret_cast<const float4*>(static_cast<const float*>(row) + col);
     v[0] = x.x;
     v[1] = x.y;
