@@ -164,6 +164,47 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
   check_launch(rc, "cls_counts");
 }
 
+// Lean entry of the north-star update (MulticlassAccuracy micro, k=1): every precondition of
+// the wide K1 launch is tested here, and anything unusual returns false so the caller takes
+// the general Python path (which raises the reference's own errors).  One pybind call with
+// four positional tensors instead of the 15-argument cls_counts plus its Python-side checks.
+bool micro_accuracy_update(const Tensor& input, const Tensor& target, const Tensor& correct,
+                           const Tensor& total) {
+  if (!input.is_cuda() || input.dim() != 2 || target.dim() != 1) return false;
+  const int64_t n = input.size(0), c = input.size(1);
+  if (target.size(0) != n || c <= 0 || c >= (int64_t(1) << 31) || input.stride(1) != 1) return false;
+  const auto st = input.scalar_type();
+  if (st != at::kFloat && st != at::kBFloat16 && st != at::kHalf) return false;
+  switch (target.scalar_type()) {
+    case at::kLong: case at::kInt: case at::kShort: case at::kChar: case at::kByte: case at::kBool:
+      break;
+    default: return false;
+  }
+  if (!target.is_contiguous()) return false;
+  const auto dev = input.device();
+  if (target.device() != dev || correct.device() != dev || total.device() != dev) return false;
+  if (correct.scalar_type() != at::kFloat || total.scalar_type() != at::kFloat ||
+      correct.numel() != 1 || total.numel() != 1)
+    return false;
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(dev);
+  tea::ClsCountsArgs a;
+  a.input = input.data_ptr();
+  a.in_dt = dt_of(input);
+  a.n = n;
+  a.c = c;
+  a.row_stride = input.stride(0);
+  a.target = target.data_ptr();
+  a.tg_dt = dt_of(target);
+  a.k = 1;
+  a.num_classes = c;
+  a.micro_correct = correct.data_ptr<float>();
+  a.micro_total = total.data_ptr<float>();
+  const hipStream_t stream = stream_for(input);
+  a.fold_ws = fold_workspace(input, stream);
+  check_launch(tea::launch_cls_counts(a, stream), "micro_accuracy_update");
+  return true;
+}
+
 // ---------------------------------------------------------------- K10 rank-of-target scores
 Tensor rank_scores(const Tensor& input, const Tensor& target, int64_t mode, int64_t k,
                    const optional<Tensor>& err) {
@@ -730,6 +771,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("ARCH") = "gfx950";
   m.def("rank_scores", &rank_scores, "K10 rank-of-target scores (hit rate / reciprocal rank)",
         py::arg("input"), py::arg("target"), py::arg("mode"), py::arg("k"), py::arg("err") = py::none());
+  m.def("micro_accuracy_update", &micro_accuracy_update,
+        "K1 micro accuracy (k=1) accumulated into float32 scalar states; false = not handled");
   m.def("cls_counts", &cls_counts, "K1 fused classification counts", py::arg("input"),
         py::arg("target"), py::arg("k"), py::arg("num_classes"), py::arg("micro_correct"),
         py::arg("micro_total"), py::arg("cls_correct"), py::arg("cls_label"),

@@ -31,7 +31,13 @@ from torcheval_amd.metrics.functional.classification.accuracy import (
     _cpu_fast_ok,
 )
 from torcheval_amd.metrics.metric import Metric
-from torcheval_amd.ops import native, use_native
+import torcheval_amd.ops as _ops
+from torcheval_amd.ops import native, native_loaded, use_native
+
+# K1 micro-accuracy entry of the loaded extension (None when unbuilt or HIP is disabled)
+_FAST_MICRO = (
+    getattr(_ops._C, "micro_accuracy_update", None) if native_loaded() and not _ops.DISABLE_HIP else None
+)
 from torcheval_amd.ops.classification import (
     binary_counts,
     cls_counts,
@@ -85,12 +91,31 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         shape = () if average == "micro" else (num_classes or 0,)
         self._add_state("num_correct", torch.zeros(shape, device=self.device), merge="sum")
         self._add_state("num_total", torch.zeros(shape, device=self.device), merge="sum")
+        self._refresh_fast_path()
+
+    def _refresh_fast_path(self) -> None:
+        # north-star fast path (ROCm states, micro, k=1): ONE native call that tests every
+        # precondition itself and returns False for anything it does not handle
+        self._fast = (
+            _FAST_MICRO is not None
+            and self.average == "micro"
+            and self.k == 1
+            and type(self) is MulticlassAccuracy
+            and self._device.type == "cuda"
+        )
+
+    def to(self: TAccuracy, device, *args, **kwargs) -> TAccuracy:
+        super().to(device, *args, **kwargs)
+        self._refresh_fast_path()
+        return self
 
     def update(self: TAccuracy, input: torch.Tensor, target: torch.Tensor) -> TAccuracy:
         """
         Update states with a batch of predictions (``[N]`` labels or ``[N, C]`` scores)
         and ``[N]`` ground-truth labels.
         """
+        if self._fast and _FAST_MICRO(input, target, self.num_correct, self.num_total):
+            return self
         dev = self._device
         if input.device != dev:
             input = input.to(dev)
