@@ -191,3 +191,18 @@ def test_windowed_ne_gpu():
     life, win = m.compute()
     torch.testing.assert_close(life.cpu(), binary_normalized_entropy(torch.cat(xs, 1).double(), torch.cat(ts, 1).double(), num_tasks=2), rtol=1e-6, atol=1e-8)
     torch.testing.assert_close(win.cpu(), binary_normalized_entropy(torch.cat(xs[-3:], 1).double(), torch.cat(ts[-3:], 1).double(), num_tasks=2), rtol=1e-6, atol=1e-8)
+
+
+def test_k8_misaligned_contiguous_view():
+    """A contiguous activation view at a 4-byte storage offset is re-allocated (16-B aligned)
+    before K8, instead of tripping the kernel's alignment check."""
+    from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
+
+    base = torch.rand(257 * 64 + 1, device=DEV)
+    act = base[1:].view(257, 64)
+    assert act.is_contiguous() and act.data_ptr() % 16 != 0
+    m = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=64, device=DEV)
+    m.update_activations(act, True)
+    ref = act.double().T @ act.double()
+    torch.testing.assert_close(m.real_cov_sum.double(), ref, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(m.real_sum.double(), act.double().sum(0), rtol=1e-5, atol=1e-4)

@@ -1,0 +1,69 @@
+"""The collective code paths with the ws == 1 shortcuts disabled (gloo, CPU), and the
+cross-rank merge of device error flags (a flag raised on one rank must surface on
+every rank, and the synced copy must not consume the caller's flag)."""
+
+import pytest
+import torch
+
+from torcheval_amd.utils.test_utils.dist_pool import run_distributed
+
+
+def _single_rank_job(rank, ws):
+    from torcheval_amd.metrics import BinaryAUROC, MulticlassBinnedAUPRC, MulticlassConfusionMatrix
+    from torcheval_amd.metrics.functional import binary_auroc
+    from torcheval_amd.metrics.toolkit import get_synced_metric
+    from torcheval_amd.parallel.class_shard import class_sharded_compute, reduce_scatter_classes
+    from torcheval_amd.parallel.collectives import collectives_at_world_size_1
+    from torcheval_amd.parallel.dist_auc import distributed_binary_areas
+
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(3000, 12, generator=g)
+    y = torch.randint(0, 12, (3000,), generator=g)
+    with collectives_at_world_size_1():
+        cm = MulticlassConfusionMatrix(12).update(x, y)
+        synced = get_synced_metric(cm)
+        assert synced is not cm
+        torch.testing.assert_close(synced.compute(), cm.compute())
+        torch.testing.assert_close(class_sharded_compute(cm), cm.compute())
+        b = MulticlassBinnedAUPRC(num_classes=12, threshold=16, average=None).update(x, y)
+        torch.testing.assert_close(class_sharded_compute(b), b.compute())
+        shard, s0, s1 = reduce_scatter_classes(x, dim=1)
+        assert (s0, s1) == (0, 12)
+        torch.testing.assert_close(shard, x.t())
+        s = (torch.randint(0, 50, (5000,), generator=g).float() / 50)
+        t = torch.randint(0, 2, (5000,), generator=g)
+        roc, _ = distributed_binary_areas(s, t)
+        torch.testing.assert_close(roc, binary_auroc(s, t).double(), rtol=1e-9, atol=1e-12)
+        au = BinaryAUROC().update(s, t)
+        torch.testing.assert_close(get_synced_metric(au).compute(), au.compute())
+    return True
+
+
+def test_collectives_at_world_size_1_gloo():
+    assert run_distributed(_single_rank_job, 1) == [True]
+
+
+def _err_job(rank, ws):
+    from torcheval_amd.metrics import MulticlassAccuracy, MulticlassConfusionMatrix
+    from torcheval_amd.metrics.toolkit import sync_and_compute_collection
+
+    acc = MulticlassAccuracy(num_classes=4, average="macro")
+    acc.update(torch.eye(4), torch.arange(4))
+    cm = MulticlassConfusionMatrix(4).update(torch.eye(4), torch.arange(4))
+    if rank == ws - 1:  # simulate a K1 kernel that recorded an out-of-range label on one rank
+        acc._err = torch.tensor([9], dtype=torch.int32)
+    try:
+        sync_and_compute_collection({"acc": acc, "cm": cm})
+        raised = False
+    except RuntimeError as e:
+        raised = "index out of bounds" in str(e)
+    own = None if acc._err is None else int(acc._err.item())
+    return raised, own
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_error_flags_raise_on_every_rank(ws):
+    res = run_distributed(_err_job, ws)
+    assert all(r[0] for r in res), res
+    assert res[-1][1] == 9  # the flagged rank's own metric still holds its flag
+    assert all(not r[1] for r in res[:-1])  # None, or a clean (zero) flag

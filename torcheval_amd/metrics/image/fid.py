@@ -35,8 +35,11 @@ def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
     ):
         from torcheval_amd.ops import native
 
-        a = act if (act.stride(1) == 1 and act.stride(0) % 4 == 0 and act.data_ptr() % 16 == 0) else act.contiguous()
-        if a.stride(0) % 4 == 0:  # K8 streams 16-B row segments
+        a = act
+        if not (a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0):
+            # a fresh allocation: contiguous() would return a contiguous but misaligned view as is
+            a = act.clone(memory_format=torch.contiguous_format)
+        if a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0:  # K8 streams 16-B row segments
             native().fid_cov_update(a, cov_sum, col_sum)
             return
     col_sum += torch.sum(act, dim=0)
@@ -50,10 +53,12 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
     fast path is one Cholesky, two triangular products and ONE eigenvalues-only ``eigvalsh``
     (no eigenvectors, no back-transformation).  A singular S1 (fewer samples than features)
     has no Cholesky factor; then a full ``eigh`` gives S1 = W W^T with W = V_r sqrt(lam_r) over
-    the numerically non-zero eigenvalues (rank r, the ``matrix_rank`` tolerance), and the
-    eigvalsh runs on the r x r matrix W^T S2 W: the same non-zero spectrum as S1 S2, without
-    the two D x D products and D x D eigvalsh of S1^1/2 S2 S1^1/2 (82 ms for this step at
-    D = 2048, r = 999 on MI355X; the full FID compute was 100 ms; benchmarks/fid_singular_probe.py)."""
+    the numerically non-zero eigenvalues (rank r, the ``matrix_rank`` tolerance of the FP64
+    matrix), and the eigvalsh runs on the r x r matrix W^T S2 W: the same non-zero spectrum as
+    S1 S2.  The tolerance is deliberately the FP64 one: covariances assembled from FP32 state
+    sums carry rounding "noise" eigenvalues well above it, and the reference's
+    ``eigvals(S1 S2)`` includes their square roots too, so they are kept (r is then the FP64
+    numerical rank, usually above the sample rank - the r x r saving shrinks accordingly)."""
     L, info = torch.linalg.cholesky_ex(s1)
     if int(info) == 0:
         m = L.T @ s2 @ L

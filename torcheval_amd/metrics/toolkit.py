@@ -19,7 +19,7 @@ from torcheval_amd.config import trace_range
 from torcheval_amd.metrics.metric import Metric, TComputeReturn
 from datetime import timedelta
 
-from torcheval_amd.parallel.collectives import sync_timeout
+from torcheval_amd.parallel.collectives import skip_collectives, sync_timeout
 from torcheval_amd.parallel.distributed import PGWrapper
 from torcheval_amd.parallel.state_sync import (
     PendingSync,
@@ -101,7 +101,7 @@ def get_synced_metric_async(
     single = isinstance(metric, Metric)
     world_size = PGWrapper(process_group).get_world_size()
     _validate_rank_and_world_size(world_size)
-    if world_size == 1:
+    if skip_collectives(world_size):
         return SyncFuture(None, clone_metric(metric) if single else {k: clone_metric(m) for k, m in metric.items()}, single)
     coll = {"_": metric} if single else metric
     with trace_range("torcheval_amd.start_sync"), sync_timeout(timeout):
@@ -164,7 +164,7 @@ def get_synced_metric(
     """
     world_size = PGWrapper(process_group).get_world_size()
     _validate_rank_and_world_size(world_size)
-    if world_size == 1:
+    if skip_collectives(world_size):
         return metric
     with trace_range("torcheval_amd.sync_metric"), sync_timeout(timeout):
         return sync_metric(metric, process_group if process_group else dist.group.WORLD, world_size)
@@ -179,7 +179,7 @@ def get_synced_metric_collection(
     """Return a dict of metrics whose states are synced across the ranks (one batched exchange)."""
     world_size = PGWrapper(process_group).get_world_size()
     _validate_rank_and_world_size(world_size)
-    if world_size == 1:
+    if skip_collectives(world_size):
         return metric_collection
     with trace_range("torcheval_amd.sync_metric_collection"), sync_timeout(timeout):
         return sync_metric_collection(

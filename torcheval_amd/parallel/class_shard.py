@@ -23,7 +23,7 @@ import torch
 import torch.distributed as dist
 import torch.nn.functional as F
 
-from torcheval_amd.parallel.collectives import _wait
+from torcheval_amd.parallel.collectives import _wait, skip_collectives
 
 __all__ = ["reduce_scatter_classes", "class_sharded_compute", "sharded_confusion_matrix", "ShardedRows"]
 
@@ -32,6 +32,10 @@ def _ws_rank(group) -> Tuple[int, int]:
     if not dist.is_initialized():
         return 1, 0
     return dist.get_world_size(group), dist.get_rank(group)
+
+
+def _local_only(ws: int) -> bool:
+    return not dist.is_initialized() or skip_collectives(ws)
 
 
 def reduce_scatter_classes(
@@ -47,7 +51,7 @@ def reduce_scatter_classes(
     chunk = -(-C // ws)
     start, stop = min(rank * chunk, C), min((rank + 1) * chunk, C)
     front = t.movedim(dim, 0)
-    if ws == 1:
+    if _local_only(ws):
         return front.contiguous(), 0, C
     rest = front.shape[1:]
     if dist.get_backend(group) == "gloo":
@@ -66,7 +70,7 @@ def reduce_scatter_classes(
 def _gather_classes(local: torch.Tensor, C: int, group) -> torch.Tensor:
     """Concatenate every rank's per-class result (chunked as in ``reduce_scatter_classes``)."""
     ws, _ = _ws_rank(group)
-    if ws == 1:
+    if _local_only(ws):
         return local
     chunk = -(-C // ws)
     padded = local.new_zeros((chunk,) + tuple(local.shape[1:]))
@@ -111,7 +115,7 @@ def sharded_confusion_matrix(
     if normalize in ("pred", "all"):
         col = torch.cat([rows.abs().sum(0), rows.sum().reshape(1)]).float()
         ws, _ = _ws_rank(group)
-        if ws > 1:
+        if not _local_only(ws):
             _wait(dist.all_reduce(col, group=group, async_op=True))
         if normalize == "pred":
             rows = rows.float() / col[:C].clamp_min(1e-12)

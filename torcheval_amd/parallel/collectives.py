@@ -48,6 +48,29 @@ _SYNC_TIMEOUT: "contextvars.ContextVar[Optional[timedelta]]" = contextvars.Conte
 )
 
 
+# Rehearsal switch: run the collective code paths even when the group has one rank (the
+# shortcuts in class_shard / dist_auc otherwise skip them).  Lets a 1-GPU box execute every
+# RCCL branch (reduce_scatter_tensor, all_to_all_single, all_gather_into_tensor) for real.
+_COLLECTIVES_AT_WS1: "contextvars.ContextVar[bool]" = contextvars.ContextVar(
+    "torcheval_amd_collectives_at_ws1", default=False
+)
+
+
+@contextlib.contextmanager
+def collectives_at_world_size_1(enabled: bool = True):
+    """Inside the block, single-rank groups take the same collective path as multi-rank ones."""
+    token = _COLLECTIVES_AT_WS1.set(enabled)
+    try:
+        yield
+    finally:
+        _COLLECTIVES_AT_WS1.reset(token)
+
+
+def skip_collectives(ws: int) -> bool:
+    """True when a world of ``ws`` ranks may short-circuit its collectives."""
+    return ws == 1 and not _COLLECTIVES_AT_WS1.get()
+
+
 @contextlib.contextmanager
 def sync_timeout(timeout: Optional[timedelta]):
     """Bound every metric-sync collective issued inside the block by ``timeout``."""
@@ -298,15 +321,38 @@ def packed_all_gather(
     return out
 
 
-def _all_gather_fixed(t: torch.Tensor, group, ws: int) -> torch.Tensor:
-    """All-gather equal-size 1-D tensors into one flat [ws * n] tensor."""
+class GatherHandle:
+    """In-flight fixed-size all-gather; ``wait()`` returns the flat [ws * n] result."""
+
+    def __init__(self, work, out: Optional[torch.Tensor], outs: Optional[List[torch.Tensor]]) -> None:
+        self._work = work
+        self._out = out
+        self._outs = outs
+        self._timeout = _SYNC_TIMEOUT.get()
+
+    def wait(self) -> torch.Tensor:
+        if self._work is not None:
+            _wait(self._work, self._timeout)
+            self._work = None
+            if self._outs is not None:
+                self._out = torch.cat(self._outs)
+                self._outs = None
+        return self._out  # type: ignore[return-value]
+
+
+def all_gather_fixed_async(t: torch.Tensor, group, ws: int) -> GatherHandle:
+    """Issue an all-gather of equal-size 1-D tensors (one flat RCCL all-gather on HBM)."""
+    t = t.reshape(-1)
     if backend_of(group) == "nccl":
         out = torch.empty(ws * t.numel(), dtype=t.dtype, device=t.device)
-        _wait(dist.all_gather_into_tensor(out, t, group=group, async_op=True))
-        return out
+        return GatherHandle(dist.all_gather_into_tensor(out, t, group=group, async_op=True), out, None)
     outs = [torch.empty_like(t) for _ in range(ws)]
-    _wait(dist.all_gather(outs, t, group=group, async_op=True))
-    return torch.cat(outs)
+    return GatherHandle(dist.all_gather(outs, t, group=group, async_op=True), None, outs)
+
+
+def _all_gather_fixed(t: torch.Tensor, group, ws: int) -> torch.Tensor:
+    """All-gather equal-size 1-D tensors into one flat [ws * n] tensor."""
+    return all_gather_fixed_async(t, group, ws).wait()
 
 
 def all_gather_tensors(
