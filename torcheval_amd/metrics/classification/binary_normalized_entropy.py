@@ -28,6 +28,8 @@ class BinaryNormalizedEntropy(Metric[torch.Tensor]):
     Functional version: ``binary_normalized_entropy``.
     """
 
+    _err_merge = "first"  # int32[6] record: flag + packed 64-bit range keys
+
     def __init__(
         self: TNormalizedEntropy,
         *,

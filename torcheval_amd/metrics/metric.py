@@ -94,6 +94,11 @@ class Metric(Generic[TComputeReturn], ABC):
             if fn is not None and callable(fn):
                 setattr(cls, label, _instrument(fn, label, check_after=label == "update"))
 
+    # How a device error flag (``self._err``, when a metric has one) merges across ranks in the
+    # distributed sync: "max" (elementwise; codes and largest offending labels) or "first"
+    # (the lowest flagged rank's whole record, for multi-word records).
+    _err_merge: str = "max"
+
     def _check_device_errors(self) -> None:
         """Raise input-validation errors that native kernels recorded on the device.
 

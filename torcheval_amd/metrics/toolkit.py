@@ -188,7 +188,7 @@ def get_synced_metric_collection(
 
 
 def _validate_rank_and_world_size(world_size: int) -> None:
-    if world_size == 1:
+    if world_size == 1 and skip_collectives(1):
         log.warning(
             "World size is 1, and metric(s) not synced. returning the input metric(s)."
         )

@@ -111,7 +111,8 @@ class AllReduceHandle:
             return self._out
         out: List[Optional[torch.Tensor]] = [None] * self._n
         for work, flat, is_bool, layout in self._pending:
-            _wait(work, self._timeout)
+            if work is not None:
+                _wait(work, self._timeout)
             if is_bool:
                 flat = flat.to(torch.bool)
             off = 0
@@ -128,6 +129,8 @@ def allreduce_coalesced_async(
     ops: Sequence[str],
     group: Optional[dist.ProcessGroup] = None,
     bucket_cap_bytes: int = DEFAULT_BUCKET_CAP_BYTES,
+    *,
+    blocking: bool = False,
 ) -> AllReduceHandle:
     """Issue the bucketed all-reduce of ``tensors`` (each with its op) without waiting.
 
@@ -161,7 +164,7 @@ def allreduce_coalesced_async(
             is_bool = flat.dtype == torch.bool
             if is_bool:  # no bool reductions in RCCL/gloo: logical or/and via uint8 max/min
                 flat = flat.to(torch.uint8)
-            work = dist.all_reduce(flat, op=_REDUCE_OPS[op], group=group, async_op=True)
+            work = dist.all_reduce(flat, op=_REDUCE_OPS[op], group=group, async_op=_issue_async(blocking))
             layout = [(i, tensors[i].numel(), tensors[i].shape) for i in b]
             pending.append((work, flat, is_bool, layout))
     return AllReduceHandle(pending, len(tensors))
@@ -174,7 +177,7 @@ def allreduce_coalesced(
     bucket_cap_bytes: int = DEFAULT_BUCKET_CAP_BYTES,
 ) -> List[torch.Tensor]:
     """Blocking form of :func:`allreduce_coalesced_async` (inputs are left untouched)."""
-    return allreduce_coalesced_async(tensors, ops, group, bucket_cap_bytes).wait()
+    return allreduce_coalesced_async(tensors, ops, group, bucket_cap_bytes, blocking=True).wait()
 
 
 # ---------------------------------------------------------------------------- all-gather-v
@@ -331,8 +334,9 @@ class GatherHandle:
         self._timeout = _SYNC_TIMEOUT.get()
 
     def wait(self) -> torch.Tensor:
-        if self._work is not None:
-            _wait(self._work, self._timeout)
+        if self._work is not None or self._outs is not None:
+            if self._work is not None:
+                _wait(self._work, self._timeout)
             self._work = None
             if self._outs is not None:
                 self._out = torch.cat(self._outs)
@@ -340,19 +344,27 @@ class GatherHandle:
         return self._out  # type: ignore[return-value]
 
 
-def all_gather_fixed_async(t: torch.Tensor, group, ws: int) -> GatherHandle:
+def _issue_async(blocking: bool) -> bool:
+    """Blocking callers without a deadline issue plain (stream-ordered) collectives: a Work
+    handle plus ``wait()`` costs ~20 us of host time per call on RCCL (1-rank probe,
+    benchmarks/rccl_primitive_latency.py)."""
+    return not blocking or _SYNC_TIMEOUT.get() is not None
+
+
+def all_gather_fixed_async(t: torch.Tensor, group, ws: int, *, blocking: bool = False) -> GatherHandle:
     """Issue an all-gather of equal-size 1-D tensors (one flat RCCL all-gather on HBM)."""
     t = t.reshape(-1)
+    a = _issue_async(blocking)
     if backend_of(group) == "nccl":
         out = torch.empty(ws * t.numel(), dtype=t.dtype, device=t.device)
-        return GatherHandle(dist.all_gather_into_tensor(out, t, group=group, async_op=True), out, None)
+        return GatherHandle(dist.all_gather_into_tensor(out, t, group=group, async_op=a), out, None)
     outs = [torch.empty_like(t) for _ in range(ws)]
-    return GatherHandle(dist.all_gather(outs, t, group=group, async_op=True), None, outs)
+    return GatherHandle(dist.all_gather(outs, t, group=group, async_op=a), None, outs)
 
 
 def _all_gather_fixed(t: torch.Tensor, group, ws: int) -> torch.Tensor:
     """All-gather equal-size 1-D tensors into one flat [ws * n] tensor."""
-    return all_gather_fixed_async(t, group, ws).wait()
+    return all_gather_fixed_async(t, group, ws, blocking=True).wait()
 
 
 def all_gather_tensors(

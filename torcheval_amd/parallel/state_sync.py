@@ -7,24 +7,31 @@ same object on every rank.
 
 Here the same result is produced with device-resident RCCL traffic:
 
-* **typed metrics** — every state declares a merge kind (``Metric._add_state(merge=...)``):
-  ``sum``/``max``/``min`` tensors of every metric in the collection are packed into one
-  bucket per (op, dtype) and ``all_reduce``d (O(|state|) bytes per rank instead of the
-  reference's O(world_size * |state|)); ``cat`` list states are all-gathered (v) and
-  concatenated in rank order.  ``merge_state`` is not called.
+* **typed metrics** — every state declares a merge kind (``Metric._add_state(merge=...)``).
+  - *small* ``sum``/``max``/``min`` tensors (<= ``SMALL_STATE_BYTES`` in total: counters,
+    per-class vectors) and every metric's device error flags are packed as raw bytes into ONE
+    fixed-size buffer and exchanged with ONE ``all_gather_into_tensor``; each rank then
+    reduces the [world, n] rows itself (same kernel, same order on every rank, so results
+    are bit-identical everywhere).  For a few KB this costs one collective's latency, where
+    one all-reduce per (op, dtype) plus a flag gather cost three.
+  - *large* ones (confusion matrices, FID covariances, binned counts) go into one bucket per
+    (op, dtype) and are ``all_reduce``d (O(|state|) bytes per rank instead of the reference's
+    O(world_size * |state|)).
+  - ``cat`` list states are all-gathered (v) and concatenated in rank order.
+  ``merge_state`` is not called.
 * **untyped metrics** (any state with merge kind ``None``, custom user metrics) — every state
   plus the small per-rank Python attributes travel through ONE packed all-gather-v and the
   metric's own ``merge_state`` runs on rank-ordered shadows, reproducing the reference result
   exactly (including order-dependent merges such as window metrics).
 
-The all-reduce buckets are issued before the all-gather, so both are in flight together.
-``start_sync_collection`` / ``PendingSync.finish`` split the exchange so the all-reduce can
-overlap further ``update()`` calls (``toolkit.sync_and_compute_async``).
+All collectives are issued before the first wait, so they are in flight together.
+``start_sync_collection`` / ``PendingSync.finish`` split the exchange so the sync can overlap
+further ``update()`` calls (``toolkit.sync_and_compute_async``).
 """
 
 import copy
 from collections import defaultdict
-from typing import Any, Dict, List, MutableMapping, Optional
+from typing import Any, Dict, List, MutableMapping, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -35,42 +42,16 @@ from torcheval_amd.parallel.distributed import transport_device
 
 _PLAIN = (int, float, str, bool, type(None))
 _SKIP_ATTRS = {"_state_name_to_default", "_state_merge_kind", "_device"}
+# Reduce states up to this many bytes (summed over the collection) ride the packed gather.
+SMALL_STATE_BYTES = 64 << 10
+_SEG_ALIGN = 16
 # Device error flags (``_err``: int32 vectors of <= 6 words written by the native kernels'
-# input validation) travel in one fixed [M, 8] int32 all-gather; word 7 carries the length.
+# input validation) take an [8] int32 slot each in the packed gather; word 7 = the length.
 _ERR_SLOT = 8
 
 
 def _has_err_flag(metric: Metric) -> bool:
     return hasattr(metric, "_err")
-
-
-def _pack_err_flags(metrics, keys: List[str], dev: torch.device) -> torch.Tensor:
-    packed = torch.zeros(len(keys), _ERR_SLOT, dtype=torch.int32, device=dev)
-    for i, key in enumerate(keys):
-        e = getattr(metrics[key], "_err", None)
-        if isinstance(e, torch.Tensor) and e.numel():
-            n = min(e.numel(), _ERR_SLOT - 1)
-            packed[i, :n] = e.reshape(-1)[:n].to(device=dev, dtype=torch.int32)
-            packed[i, _ERR_SLOT - 1] = n
-    return packed.reshape(-1)
-
-
-def _merge_err_flags(flat: torch.Tensor, ws: int, keys: List[str], metrics, result) -> None:
-    """Every rank adopts the error record of the lowest rank that flagged one (so all ranks
-    raise the same error in ``compute()``); each synced metric gets its own flag tensor."""
-    g = flat.view(ws, len(keys), _ERR_SLOT)
-    first = (g[:, :, 0] != 0).to(torch.int32).argmax(0)  # lowest flagged rank (0 if none)
-    chosen = g[first, torch.arange(len(keys), device=g.device)]  # [M, 8]
-    for i, key in enumerate(keys):
-        local = getattr(metrics[key], "_err", None)
-        if isinstance(local, torch.Tensor):
-            n, dev = local.numel(), local.device
-        else:  # this rank never ran a flagged update: size the flag from the record itself
-            n = int(chosen[i, _ERR_SLOT - 1].item())
-            if n == 0:
-                continue
-            dev = metrics[key].device
-        result[key]._err = chosen[i, :n].to(dev).clone()
 
 
 def _is_plain(v: Any) -> bool:
@@ -100,20 +81,152 @@ def _shallow_clone(metric: Metric) -> Metric:
     return copy.copy(metric)
 
 
+def _pad(n: int) -> int:
+    return (n + _SEG_ALIGN - 1) // _SEG_ALIGN * _SEG_ALIGN
+
+
+class _SmallPack:
+    """Byte layout of the packed gather: one contiguous segment per (op, dtype) group of small
+    reduce states (one reduction launch per group after the gather), then the error-flag
+    blocks ([M, 8] int32 each: a "max" block merged by one amax, a "first" block by the
+    lowest flagged rank)."""
+
+    def __init__(self, dev: torch.device) -> None:
+        self.dev = dev
+        self.parts: List[torch.Tensor] = []
+        # (op, dtype, byte offset, elements, [(key, name, shape, element offset, numel)])
+        self.groups: List[Tuple[str, torch.dtype, int, int, List[tuple]]] = []
+        self.flag_blocks: List[Tuple[str, int, List[str]]] = []
+        self.nbytes = 0
+
+    def _align(self, n: int) -> None:
+        if _pad(n) != n:
+            self.parts.append(_zero_pad(self.dev, _pad(n) - n))
+        self.nbytes += _pad(n)
+
+    def add_group(self, op: str, dtype: torch.dtype, items: List[Tuple[str, str, torch.Tensor]]) -> None:
+        off, elems, members = self.nbytes, 0, []
+        for key, name, t in items:
+            flat = t.detach().reshape(-1)
+            if flat.device != self.dev:
+                flat = flat.to(self.dev)
+            self.parts.append(flat.view(torch.uint8))
+            members.append((key, name, t.shape, elems, flat.numel()))
+            elems += flat.numel()
+        self.groups.append((op, dtype, off, elems, members))
+        self._align(elems * (1 if dtype == torch.bool else torch.empty(0, dtype=dtype).element_size()))
+
+    def add_flags(self, metrics, mode: str, keys: List[str]) -> None:
+        """Each flag's own words plus a cached device tail (zeros, then its length) go straight
+        into the packing ``cat``: no extra kernel launches for the flags."""
+        self.flag_blocks.append((mode, self.nbytes, keys))
+        for key in keys:
+            e = getattr(metrics[key], "_err", None)
+            if isinstance(e, torch.Tensor) and e.numel():
+                n = min(e.numel(), _ERR_SLOT - 1)
+                head = e.detach().reshape(-1)[:n]
+                if head.dtype != torch.int32 or head.device != self.dev:
+                    head = head.to(device=self.dev, dtype=torch.int32)
+                self.parts.append(head.view(torch.uint8))
+                self.parts.append(_flag_tail(self.dev, n))
+            else:
+                self.parts.append(_flag_tail(self.dev, 0))
+        self.nbytes += len(keys) * _ERR_SLOT * 4
+
+    def buffer(self) -> torch.Tensor:
+        return torch.cat(self.parts) if len(self.parts) > 1 else self.parts[0].clone()
+
+    def unpack(self, flat: torch.Tensor, ws: int, metrics, result) -> None:
+        rows = flat.view(ws, self.nbytes)
+        for op, dtype, off, elems, members in self.groups:
+            esize = 1 if dtype == torch.bool else torch.empty(0, dtype=dtype).element_size()
+            seg = rows[:, off : off + elems * esize]
+            seg = seg.view(dtype) if dtype != torch.bool else seg
+            red = _reduce_rows(seg, op, dtype)
+            for key, name, shape, eoff, n in members:
+                value = red[eoff : eoff + n].view(shape)
+                dev = metrics[key].device
+                setattr(result[key], name, value if value.device == dev else value.to(dev))
+        for mode, off, keys in self.flag_blocks:
+            M = len(keys)
+            flags = rows[:, off : off + M * _ERR_SLOT * 4].view(torch.int32).view(ws, M, _ERR_SLOT)
+            _merge_err_flags(flags, mode, keys, metrics, result)
+
+
+_TAILS: Dict[Tuple[torch.device, int], torch.Tensor] = {}
+_PADS: Dict[Tuple[torch.device, int], torch.Tensor] = {}
+
+
+def _zero_pad(dev: torch.device, n: int) -> torch.Tensor:
+    t = _PADS.get((dev, n))
+    if t is None:
+        t = _PADS[(dev, n)] = torch.zeros(n, dtype=torch.uint8, device=dev)
+    return t
+
+
+def _flag_tail(dev: torch.device, n: int) -> torch.Tensor:
+    """Bytes of flag-slot words n..7: zeros, with the flag length n in word 7 (cached)."""
+    t = _TAILS.get((dev, n))
+    if t is None:
+        words = torch.zeros(_ERR_SLOT - n, dtype=torch.int32)
+        words[-1] = n
+        t = words.to(dev).view(torch.uint8)
+        _TAILS[(dev, n)] = t
+    return t
+
+
+def _reduce_rows(rows: torch.Tensor, op: str, dtype: torch.dtype) -> torch.Tensor:
+    """Reduce [ws, n] along ranks (ascending rank order on every rank).  With one rank the
+    gathered row itself is the result (a fresh buffer: no copy needed)."""
+    if rows.shape[0] == 1:
+        return rows[0] if dtype != torch.bool else rows[0].to(torch.bool)
+    if dtype == torch.bool:
+        return (rows.amax(0) if op != "min" else rows.amin(0)).to(torch.bool)
+    if op == "sum":
+        return rows.sum(0, dtype=dtype)
+    return rows.amax(0) if op == "max" else rows.amin(0)
+
+
+def _merge_err_flags(flags: torch.Tensor, mode: str, keys: List[str], metrics, result) -> None:
+    """Merge the [ws, M, 8] flag records so every rank raises in ``compute()``.
+
+    ``max`` (the default ``Metric._err_merge``: single codes / largest offending labels) takes
+    the elementwise max over ranks - one launch; ``first`` (records whose words only make sense
+    together, e.g. normalized entropy's packed 64-bit range keys) adopts the record of the
+    lowest rank that flagged one.  Each synced metric gets its own view of a fresh tensor."""
+    ws, M = flags.shape[0], len(keys)
+    if ws == 1:
+        chosen = flags[0]
+    elif mode == "max":
+        chosen = flags.amax(0)
+    else:
+        first = (flags[:, :, 0] != 0).to(torch.int32).argmax(0)  # lowest flagged rank (0 if none)
+        chosen = flags.gather(0, first.view(1, M, 1).expand(1, M, _ERR_SLOT))[0]  # [M, 8]
+    for i, key in enumerate(keys):
+        local = getattr(metrics[key], "_err", None)
+        if isinstance(local, torch.Tensor):
+            n, dev = local.numel(), local.device
+        else:  # this rank never ran a flagged update: size the flag from the record itself
+            n = int(chosen[i, _ERR_SLOT - 1].item())
+            if n == 0:
+                continue
+            dev = metrics[key].device
+        v = chosen[i, :n]
+        result[key]._err = v.to(dev) if v.device != dev else v
+
+
 class PendingSync:
     """An in-flight metric sync (see :func:`start_sync_collection`).
 
-    At creation every state that will travel has been snapshotted (the all-reduce buckets are
-    packing copies already queued on RCCL's own stream; gathered states are cloned), so the
-    caller may keep calling ``update()`` on the original metrics while the all-reduce runs.
-    ``finish()`` issues the all-gather-v (if any), waits, and assembles the merged metrics.
+    At creation every state that will travel has been snapshotted (packing copies queued
+    ahead of the collectives; gathered states are cloned), so the caller may keep calling
+    ``update()`` on the original metrics while the exchange runs.  ``finish()`` issues the
+    all-gather-v of list / untyped states (if any), waits, and assembles the merged metrics.
     """
 
     def __init__(self, metrics, group, ws, typed, gather_tree, reduced, reduce_slots, outs,
-                 err_keys=(), err_gather=None) -> None:
+                 small: Optional[_SmallPack] = None, small_gather=None) -> None:
         self._metrics = metrics
-        self._err_keys = list(err_keys)
-        self._err_gather = err_gather
         self._group = group
         self._ws = ws
         self._typed = typed
@@ -121,6 +234,8 @@ class PendingSync:
         self._reduced = reduced
         self._reduce_slots = reduce_slots
         self._outs = outs
+        self._small = small
+        self._small_gather = small_gather
         self._result: Optional[Dict[str, Metric]] = None
 
     def finish(self) -> Dict[str, Metric]:
@@ -176,8 +291,9 @@ class PendingSync:
                 elif isinstance(v, list):
                     setattr(base, name, [t.clone() for t in v])
             result[key] = base.merge_state(shadows[1:])
-        if self._err_gather is not None:
-            _merge_err_flags(self._err_gather.wait(), ws, self._err_keys, metrics, result)
+
+        if self._small is not None:
+            self._small.unpack(self._small_gather.wait(), ws, metrics, result)
         self._result = result
         return result
 
@@ -198,15 +314,19 @@ def start_sync_collection(
     world_size: Optional[int] = None,
     *,
     snapshot: bool = True,
+    small_state_bytes: int = SMALL_STATE_BYTES,
+    blocking: bool = False,
 ) -> PendingSync:
-    """Snapshot the states of ``metrics`` and issue the bucketed all-reduce asynchronously.
+    """Snapshot the states of ``metrics`` and issue the collectives asynchronously.
 
-    The all-reduce rides RCCL's internal stream, so it overlaps whatever the caller enqueues
+    The collectives ride RCCL's internal stream, so they overlap whatever the caller enqueues
     next on the compute stream (typically more ``update()`` calls).  With ``snapshot=False``
     gathered states are referenced instead of cloned (the blocking path, which finishes
-    immediately, uses this to avoid a copy)."""
+    immediately, uses this to avoid a copy).  Every rank must pass the same collection (same
+    keys, metric types and state shapes): the byte layout of the packed gather follows it."""
     group = process_group
     ws = world_size if world_size is not None else dist.get_world_size(group)
+    dev = transport_device(group)
 
     for m in metrics.values():
         m._prepare_for_merge_state()
@@ -214,6 +334,7 @@ def start_sync_collection(
     reduce_tensors: List[torch.Tensor] = []
     reduce_ops: List[str] = []
     reduce_slots: List[tuple] = []  # (key, state_name)
+    small_cands: List[Tuple[str, str, str, torch.Tensor]] = []
     gather_tree: Dict[str, Any] = {}
     typed: Dict[str, bool] = {}
     outs: Dict[str, Metric] = {}
@@ -229,9 +350,7 @@ def start_sync_collection(
             for name, kind in kinds.items():
                 value = getattr(m, name)
                 if kind in ("sum", "max", "min"):
-                    reduce_tensors.append(value)
-                    reduce_ops.append(kind)
-                    reduce_slots.append((key, name))
+                    small_cands.append((key, name, kind, value))
                 else:
                     cat_states[name] = keep(list(value))
             if cat_states:
@@ -245,15 +364,33 @@ def start_sync_collection(
             }
             gather_tree[key] = {"states": states, "extras": extras}
 
-    # the packing copies inside snapshot the reduce states; RCCL runs them asynchronously
-    reduced = collectives.allreduce_coalesced_async(reduce_tensors, reduce_ops, group)
-    err_keys = [key for key, m in metrics.items() if _has_err_flag(m)]
-    err_gather = None
-    if err_keys:  # same keys on every rank: the flag attribute exists from __init__
-        flags = _pack_err_flags(metrics, err_keys, transport_device(group))
-        err_gather = collectives.all_gather_fixed_async(flags, group, ws)
+    # split the reduce states: the smallest first into the packed gather, up to the budget
+    small = _SmallPack(dev)
+    groups: Dict[Tuple[str, torch.dtype], List[Tuple[str, str, torch.Tensor]]] = defaultdict(list)
+    used = 0
+    for key, name, kind, value in sorted(small_cands, key=lambda c: c[3].numel() * c[3].element_size()):
+        nb = value.numel() * value.element_size()
+        if used + nb <= small_state_bytes:
+            groups[(kind, value.dtype)].append((key, name, value))
+            used += nb
+        else:
+            reduce_tensors.append(value)
+            reduce_ops.append(kind)
+            reduce_slots.append((key, name))
+    for (kind, dtype) in sorted(groups, key=lambda g: (g[0], str(g[1]))):
+        small.add_group(kind, dtype, groups[(kind, dtype)])
+    # same keys on every rank: the flag attribute exists from __init__
+    for mode in ("max", "first"):
+        keys = [k for k, m in metrics.items() if _has_err_flag(m) and getattr(m, "_err_merge", "max") == mode]
+        if keys:
+            small.add_flags(metrics, mode, keys)
+
+    # the packing copies snapshot the states; RCCL runs the collectives asynchronously
+    small_gather = (collectives.all_gather_fixed_async(small.buffer(), group, ws, blocking=blocking)
+                    if small.parts else None)
+    reduced = collectives.allreduce_coalesced_async(reduce_tensors, reduce_ops, group, blocking=blocking)
     return PendingSync(metrics, group, ws, typed, gather_tree, reduced, reduce_slots, outs,
-                       err_keys, err_gather)
+                       small if small.parts else None, small_gather)
 
 
 def sync_metric_collection(
@@ -262,7 +399,7 @@ def sync_metric_collection(
     world_size: Optional[int] = None,
 ) -> Dict[str, Metric]:
     """Return a dict of new metrics whose states are merged over every rank of the group."""
-    return start_sync_collection(metrics, process_group, world_size, snapshot=False).finish()
+    return start_sync_collection(metrics, process_group, world_size, snapshot=False, blocking=True).finish()
 
 
 def sync_metric(
