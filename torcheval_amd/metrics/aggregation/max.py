@@ -1,0 +1,32 @@
+"""Max class metric (parity: metrics/aggregation/max.py)."""
+
+from typing import Iterable, Optional
+
+import torch
+
+from torcheval_amd.metrics.metric import Metric
+
+__all__ = ["Max"]
+
+
+class Max(Metric[torch.Tensor]):
+    """Running maximum of all inputs."""
+
+    def __init__(self, *, device: Optional[torch.device] = None) -> None:
+        super().__init__(device=device)
+        self._add_state("max", torch.tensor(float("-inf"), device=self.device), merge="max")
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor) -> "Max":
+        self.max = torch.max(self.max, torch.max(input))
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        return self.max
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["Max"]) -> "Max":
+        for metric in metrics:
+            self.max = torch.max(self.max, metric.max.to(self.device))
+        return self

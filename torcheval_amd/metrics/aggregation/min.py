@@ -1,0 +1,32 @@
+"""Min class metric (parity: metrics/aggregation/min.py)."""
+
+from typing import Iterable, Optional
+
+import torch
+
+from torcheval_amd.metrics.metric import Metric
+
+__all__ = ["Min"]
+
+
+class Min(Metric[torch.Tensor]):
+    """Running minimum of all inputs."""
+
+    def __init__(self, *, device: Optional[torch.device] = None) -> None:
+        super().__init__(device=device)
+        self._add_state("min", torch.tensor(float("inf"), device=self.device), merge="min")
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor) -> "Min":
+        self.min = torch.min(self.min, torch.min(input))
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        return self.min
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["Min"]) -> "Min":
+        for metric in metrics:
+            self.min = torch.min(self.min, metric.min.to(self.device))
+        return self

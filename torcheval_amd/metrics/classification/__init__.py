@@ -7,14 +7,15 @@ from torcheval_amd.metrics.classification.accuracy import (
 from torcheval_amd.metrics.classification.auprc import BinaryAUPRC, MulticlassAUPRC, MultilabelAUPRC
 from torcheval_amd.metrics.classification.auroc import BinaryAUROC, MulticlassAUROC
 from torcheval_amd.metrics.classification.binary_normalized_entropy import BinaryNormalizedEntropy
-from torcheval_amd.metrics.classification.binned import (
+from torcheval_amd.metrics.classification.binned_auprc import (
     BinaryBinnedAUPRC,
-    BinaryBinnedAUROC,
-    BinaryBinnedPrecisionRecallCurve,
     MulticlassBinnedAUPRC,
-    MulticlassBinnedAUROC,
-    MulticlassBinnedPrecisionRecallCurve,
     MultilabelBinnedAUPRC,
+)
+from torcheval_amd.metrics.classification.binned_auroc import BinaryBinnedAUROC, MulticlassBinnedAUROC
+from torcheval_amd.metrics.classification.binned_precision_recall_curve import (
+    BinaryBinnedPrecisionRecallCurve,
+    MulticlassBinnedPrecisionRecallCurve,
     MultilabelBinnedPrecisionRecallCurve,
 )
 from torcheval_amd.metrics.classification.confusion_matrix import (

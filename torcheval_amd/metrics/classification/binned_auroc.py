@@ -1,0 +1,72 @@
+"""Binned AUROC class metrics on the K4 binned counts (parity: metrics/classification/binned_auroc.py)."""
+
+from typing import List, Optional, Tuple, Union
+
+import torch
+
+from torcheval_amd.metrics.classification._sample_store import SampleStoreMetric
+from torcheval_amd.metrics.functional.classification.binned_auroc import (
+    _binary_binned_auroc_compute,
+    _binary_binned_auroc_param_check,
+    _binary_binned_auroc_update_input_check,
+    _multiclass_binned_auroc_compute,
+    _multiclass_binned_auroc_param_check,
+    _multiclass_binned_auroc_update_input_check,
+)
+from torcheval_amd.metrics.functional.tensor_utils import _create_threshold_tensor
+from torcheval_amd.metrics.classification.binned_precision_recall_curve import _ThresholdFollowsDevice
+
+__all__ = ["BinaryBinnedAUROC", "MulticlassBinnedAUROC"]
+
+
+class BinaryBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
+    """(binned AUROC, thresholds) of ``[n]`` / ``[num_tasks, n]`` scores.
+    Functional: ``binary_binned_auroc``."""
+
+    _cat_dim = -1
+
+    def __init__(
+        self,
+        *,
+        num_tasks: int = 1,
+        threshold: Union[int, List[float], torch.Tensor] = 200,
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        threshold = _create_threshold_tensor(threshold, self.device)
+        _binary_binned_auroc_param_check(num_tasks, threshold)
+        self.num_tasks = num_tasks
+        self.threshold = threshold
+
+    def _check(self, input, target) -> None:
+        _binary_binned_auroc_update_input_check(input, target, self.num_tasks, self.threshold)
+
+    @torch.inference_mode()
+    def compute(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        return _binary_binned_auroc_compute(*self._cat(), self.threshold)
+
+
+class MulticlassBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
+    """(one-vs-rest binned AUROC, thresholds).  Functional: ``multiclass_binned_auroc``."""
+
+    def __init__(
+        self,
+        *,
+        num_classes: int,
+        threshold: Union[int, List[float], torch.Tensor] = 200,
+        average: Optional[str] = "macro",
+        device: Optional[torch.device] = None,
+    ) -> None:
+        super().__init__(device=device)
+        threshold = _create_threshold_tensor(threshold, self.device)
+        _multiclass_binned_auroc_param_check(num_classes, threshold, average)
+        self.num_classes = num_classes
+        self.threshold = threshold
+        self.average = average
+
+    def _check(self, input, target) -> None:
+        _multiclass_binned_auroc_update_input_check(input, target, self.num_classes)
+
+    @torch.inference_mode()
+    def compute(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        return _multiclass_binned_auroc_compute(*self._cat(), self.num_classes, self.threshold, self.average)

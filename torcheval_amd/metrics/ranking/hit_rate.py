@@ -1,0 +1,17 @@
+"""HitRate class metric (parity: metrics/ranking/hit_rate.py)."""
+
+import torch
+
+from torcheval_amd.metrics.functional.ranking import hit_rate
+from torcheval_amd.metrics.ranking._score_list import _RankScoreList
+
+__all__ = ["HitRate"]
+
+
+class HitRate(_RankScoreList):
+    """Per-sample hit (target within top-k) scores, concatenated over updates."""
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "HitRate":
+        self.scores.append(hit_rate(input, target, k=self.k, _err=self._err_for(input)))
+        return self

@@ -1,0 +1,17 @@
+"""ReciprocalRank class metric (parity: metrics/ranking/reciprocal_rank.py)."""
+
+import torch
+
+from torcheval_amd.metrics.functional.ranking import reciprocal_rank
+from torcheval_amd.metrics.ranking._score_list import _RankScoreList
+
+__all__ = ["ReciprocalRank"]
+
+
+class ReciprocalRank(_RankScoreList):
+    """Per-sample reciprocal rank scores, concatenated over updates."""
+
+    @torch.inference_mode()
+    def update(self, input: torch.Tensor, target: torch.Tensor) -> "ReciprocalRank":
+        self.scores.append(reciprocal_rank(input, target, k=self.k, _err=self._err_for(input)))
+        return self

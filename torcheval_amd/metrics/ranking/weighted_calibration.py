@@ -1,0 +1,46 @@
+"""WeightedCalibration class metric (parity: metrics/ranking/weighted_calibration.py)."""
+
+from typing import Iterable, Optional, Union
+
+import torch
+
+from torcheval_amd.metrics.functional.ranking import _weighted_calibration_update
+from torcheval_amd.metrics.metric import Metric
+
+__all__ = ["WeightedCalibration"]
+
+
+class WeightedCalibration(Metric[torch.Tensor]):
+    """sum(w * input) / sum(w * target) per task (float64 sums, ``merge="sum"``)."""
+
+    def __init__(self, *, num_tasks: int = 1, device: Optional[torch.device] = None) -> None:
+        super().__init__(device=device)
+        if num_tasks < 1:
+            raise ValueError(
+                "`num_tasks` value should be greater than and equal to 1, but received {num_tasks}. "
+            )
+        self.num_tasks = num_tasks
+        for name in ("weighted_input_sum", "weighted_target_sum"):
+            self._add_state(name, torch.zeros(num_tasks, dtype=torch.float64, device=self.device), merge="sum")
+
+    @torch.inference_mode()
+    def update(
+        self, input: torch.Tensor, target: torch.Tensor, weight: Union[float, int, torch.Tensor] = 1.0
+    ) -> "WeightedCalibration":
+        wi, wt = _weighted_calibration_update(input, target, weight, num_tasks=self.num_tasks)
+        self.weighted_input_sum += wi
+        self.weighted_target_sum += wt
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        if torch.any(self.weighted_target_sum == 0.0):
+            return torch.empty(0)
+        return self.weighted_input_sum / self.weighted_target_sum
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["WeightedCalibration"]) -> "WeightedCalibration":
+        for metric in metrics:
+            self.weighted_input_sum += metric.weighted_input_sum.to(self.device)
+            self.weighted_target_sum += metric.weighted_target_sum.to(self.device)
+        return self

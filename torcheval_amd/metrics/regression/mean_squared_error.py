@@ -1,0 +1,52 @@
+"""MeanSquaredError class metric (parity: metrics/regression/mean_squared_error.py)."""
+
+from typing import Iterable, Optional
+
+import torch
+
+from torcheval_amd.metrics.functional.regression import (
+    _mean_squared_error_compute,
+    _mean_squared_error_param_check,
+    _mean_squared_error_update,
+)
+from torcheval_amd.metrics.metric import Metric
+
+__all__ = ["MeanSquaredError"]
+
+
+class MeanSquaredError(Metric[torch.Tensor]):
+    """Mean squared error; ``multioutput`` in uniform_average | raw_values.
+    Functional version: ``mean_squared_error``."""
+
+    def __init__(self, *, multioutput: str = "uniform_average", device: Optional[torch.device] = None) -> None:
+        super().__init__(device=device)
+        _mean_squared_error_param_check(multioutput)
+        self.multioutput = multioutput
+        self._add_state("sum_squared_error", torch.tensor(0.0, device=self.device))
+        self._add_state("sum_weight", torch.tensor(0.0, device=self.device))
+
+    @torch.inference_mode()
+    def update(
+        self, input: torch.Tensor, target: torch.Tensor, *, sample_weight: Optional[torch.Tensor] = None
+    ) -> "MeanSquaredError":
+        sse, sum_weight = _mean_squared_error_update(input, target, sample_weight)
+        if self.sum_squared_error.ndim == 0 and sse.ndim == 1:
+            self.sum_squared_error = sse
+        else:
+            self.sum_squared_error += sse
+        self.sum_weight += sum_weight
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        return _mean_squared_error_compute(self.sum_squared_error, self.multioutput, self.sum_weight)
+
+    @torch.inference_mode()
+    def merge_state(self, metrics: Iterable["MeanSquaredError"]) -> "MeanSquaredError":
+        for metric in metrics:
+            if self.sum_squared_error.ndim == 0 and metric.sum_squared_error.ndim == 1:
+                self.sum_squared_error = metric.sum_squared_error.to(self.device)
+            else:
+                self.sum_squared_error += metric.sum_squared_error.to(self.device)
+            self.sum_weight += metric.sum_weight.to(self.device)
+        return self

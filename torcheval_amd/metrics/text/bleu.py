@@ -1,0 +1,50 @@
+"""BLEUScore class metric (parity: metrics/text/bleu.py)."""
+
+from typing import Optional, Sequence, Union
+
+import torch
+
+from torcheval_amd.metrics.functional.text import _bleu_score_compute, _bleu_score_update
+from torcheval_amd.metrics.text._sum_states import _SumStates
+
+__all__ = ["BLEUScore"]
+
+
+class BLEUScore(_SumStates):
+    """Corpus BLEU with up to 4-gram precision (native C++ n-gram counting)."""
+
+    _names = ("input_len", "target_len", "matches_by_order", "possible_matches_by_order")
+
+    def __init__(self, *, n_gram: int, weights: Optional[torch.Tensor] = None, device: Optional[torch.device] = None) -> None:
+        super().__init__(device=device)
+        if n_gram not in [1, 2, 3, 4]:
+            raise ValueError(f"n_gram should be 1, 2, 3, or 4, got {n_gram}.")
+        if weights is not None and n_gram != len(weights):
+            raise ValueError(
+                f"the length of weights should equal n_gram, got len(weights)={len(weights)}, n_gram={n_gram}"
+            )
+        self.weights = weights
+        self.n_gram = n_gram
+        f64 = torch.float64
+        self._add_state("input_len", torch.tensor(0.0, dtype=f64, device=self.device), merge="sum")
+        self._add_state("target_len", torch.tensor(0.0, dtype=f64, device=self.device), merge="sum")
+        self._add_state("matches_by_order", torch.zeros(n_gram, dtype=f64, device=self.device), merge="sum")
+        self._add_state("possible_matches_by_order", torch.zeros(n_gram, dtype=f64, device=self.device), merge="sum")
+
+    @torch.inference_mode()
+    def update(self, input: Union[str, Sequence[str]], target: Sequence[Union[str, Sequence[str]]]) -> "BLEUScore":
+        il, tl, m, p = _bleu_score_update(input, target, self.n_gram, self.device)
+        self.input_len += il
+        self.target_len += tl
+        self.matches_by_order += m
+        self.possible_matches_by_order += p
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        if torch.sum(self.matches_by_order) == 0:
+            return torch.tensor(0.0, dtype=torch.float64, device=self.device)
+        return _bleu_score_compute(
+            self.input_len, self.target_len, self.matches_by_order, self.possible_matches_by_order,
+            self.n_gram, self.weights,
+        )

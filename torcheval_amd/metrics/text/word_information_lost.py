@@ -1,0 +1,33 @@
+"""WordInformationLost class metric (parity: metrics/text/word_information_lost.py)."""
+
+from typing import List, Optional, Union
+
+import torch
+
+from torcheval_amd.metrics.functional.text import _wil_compute, _wil_update
+from torcheval_amd.metrics.text._sum_states import _SumStates
+
+__all__ = ["WordInformationLost"]
+
+
+class WordInformationLost(_SumStates):
+    """Word information lost (native C++ edit distance)."""
+
+    _names = ("correct_total", "target_total", "preds_total")
+
+    def __init__(self, device: Optional[torch.device] = None) -> None:
+        super().__init__(device=device)
+        for n in self._names:
+            self._add_state(n, torch.tensor(0.0, dtype=torch.float64, device=self.device), merge="sum")
+
+    @torch.inference_mode()
+    def update(self, input: Union[str, List[str]], target: Union[str, List[str]]) -> "WordInformationLost":
+        c, t, p = _wil_update(input, target)
+        self.correct_total += c.to(self.device)
+        self.target_total += t.to(self.device)
+        self.preds_total += p.to(self.device)
+        return self
+
+    @torch.inference_mode()
+    def compute(self) -> torch.Tensor:
+        return _wil_compute(self.correct_total, self.target_total, self.preds_total)

@@ -13,7 +13,7 @@ randomly initialised unless ``weights_path`` points to a local ``.safetensors`` 
 """
 
 import warnings
-from typing import List, Optional
+from typing import Optional
 
 import torch
 import torch.nn as nn

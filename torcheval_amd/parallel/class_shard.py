@@ -134,7 +134,7 @@ def class_sharded_compute(metric, *, group: Optional[dist.ProcessGroup] = None) 
     Supported: ``MulticlassBinnedAUPRC``, ``MultilabelBinnedAUPRC`` ([T, C] counts) and
     ``MulticlassConfusionMatrix`` (full matrix; use ``sharded_confusion_matrix`` to keep it
     sharded)."""
-    from torcheval_amd.metrics.classification.binned import MulticlassBinnedAUPRC, MultilabelBinnedAUPRC
+    from torcheval_amd.metrics.classification.binned_auprc import MulticlassBinnedAUPRC, MultilabelBinnedAUPRC
     from torcheval_amd.metrics.classification.confusion_matrix import MulticlassConfusionMatrix
     from torcheval_amd.metrics.functional.classification.binned_auprc import _binned_riemann
 

@@ -232,4 +232,4 @@ def assert_result_close(result: Any, expected_result: Any, atol: float = 1e-8, r
     elif isinstance(result, float):
         torch.testing.assert_close(result, expected_result, atol=atol, rtol=rtol, equal_nan=True)
     else:
-        raise ValueError("Compute result comparision is not supported.")
+        raise ValueError("Compute result comparison is not supported.")
