@@ -124,7 +124,27 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         m = M.BinaryBinnedAUPRC(threshold=200, device=dev)
         return lambda: m.update(x, y)
 
+    def bprc():
+        x, y = rand(N1M), randint(2, N1M)
+        return lambda: F.binary_precision_recall_curve(x, y)
+
+    def brafp():
+        x, y = rand(N1M), randint(2, N1M)
+        return lambda: F.binary_recall_at_fixed_precision(x, y, min_precision=0.5)
+
     N100k, C100 = n(100_000), 100 if s >= 1 else 5
+
+    def mlprc():
+        x, y = rand(N100k, C100), randint(2, N100k, C100)
+        return lambda: F.multilabel_precision_recall_curve(x, y, num_labels=C100)
+
+    def mlrafp():
+        x, y = rand(N100k, C100), randint(2, N100k, C100)
+        return lambda: F.multilabel_recall_at_fixed_precision(x, y, num_labels=C100, min_precision=0.5)
+
+    def mcprc():
+        x, y = rand(N100k, C100), randint(C100, N100k)
+        return lambda: F.multiclass_precision_recall_curve(x, y, num_classes=C100)
 
     def mc_auroc():
         x, y = rand(N100k, C100), randint(C100, N100k)
@@ -224,6 +244,11 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "binary_binned_auroc N=1M T=200": binned_auroc,
         "binary_binned_precision_recall_curve N=1M T=100": binned_prc,
         "BinaryBinnedAUPRC(200).update N=1M": binned_auprc_cls,
+        "binary_precision_recall_curve N=1M": bprc,
+        "binary_recall_at_fixed_precision N=1M p=0.5": brafp,
+        "multilabel_precision_recall_curve 100k x 100": mlprc,
+        "multilabel_recall_at_fixed_precision 100k x 100 p=0.5": mlrafp,
+        "multiclass_precision_recall_curve N=100k C=100": mcprc,
         "multiclass_auroc N=100k C=100": mc_auroc,
         "multiclass_auprc N=100k C=100": mc_auprc,
         "MulticlassBinnedAUPRC(C=100,T=100).update N=100k": mc_binned_auprc_cls,

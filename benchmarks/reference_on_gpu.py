@@ -100,10 +100,28 @@ def main() -> None:
     bo, br = M.BinaryBinnedAUPRC(threshold=200, device=dev), RM.BinaryBinnedAUPRC(threshold=200, device=dev)
     case("BinaryBinnedAUPRC(200).update N=1M", lambda: bo.update(s, t), lambda: br.update(s, t), 200)
 
+    # K3c: PR curves / recall at fixed precision (the reference loops labels in Python)
+    case("binary_precision_recall_curve N=1M", lambda: F.binary_precision_recall_curve(s, t),
+         lambda: RF.binary_precision_recall_curve(s, t), 50)
+    case("binary_recall_at_fixed_precision N=1M p=0.5",
+         lambda: F.binary_recall_at_fixed_precision(s, t, min_precision=0.5),
+         lambda: RF.binary_recall_at_fixed_precision(s, t, min_precision=0.5), 50)
+    xl = torch.rand(100_000, 100, device=dev, generator=g)
+    tl = torch.randint(0, 2, (100_000, 100), device=dev, generator=g)
+    case("multilabel_precision_recall_curve 100k x 100", lambda: F.multilabel_precision_recall_curve(xl, tl, num_labels=100),
+         lambda: RF.multilabel_precision_recall_curve(xl, tl, num_labels=100), 10)
+    case("multilabel_recall_at_fixed_precision 100k x 100 p=0.5",
+         lambda: F.multilabel_recall_at_fixed_precision(xl, tl, num_labels=100, min_precision=0.5),
+         lambda: RF.multilabel_recall_at_fixed_precision(xl, tl, num_labels=100, min_precision=0.5), 10)
+    del xl, tl
+
     xm = torch.rand(100_000, 100, device=dev, generator=g)
     ym = torch.randint(0, 100, (100_000,), device=dev, generator=g)
     case("multiclass_auroc N=100k C=100", lambda: F.multiclass_auroc(xm, ym, num_classes=100),
          lambda: RF.multiclass_auroc(xm, ym, num_classes=100), 20)
+    case("multiclass_precision_recall_curve N=100k C=100",
+         lambda: F.multiclass_precision_recall_curve(xm, ym, num_classes=100),
+         lambda: RF.multiclass_precision_recall_curve(xm, ym, num_classes=100), 10)
     mbo = M.MulticlassBinnedAUPRC(num_classes=100, threshold=100, device=dev)
     mbr = RM.MulticlassBinnedAUPRC(num_classes=100, threshold=100, device=dev)
     case("MulticlassBinnedAUPRC(C=100,T=100).update N=100k", lambda: mbo.update(xm, ym),

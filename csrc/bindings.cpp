@@ -283,19 +283,19 @@ void binary_counts(const Tensor& input, const Tensor& target, const optional<Ten
 // ---------------------------------------------------------------- K3 sort-scan
 // sorted/order: [rows, n] (descending scores and their permutation); target: [rows, n] binary
 // targets or (class_mode) [n] labels; weight: optional [rows, n]; outputs float64 [rows].
-void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
-              const optional<Tensor>& weight, bool class_mode, const optional<Tensor>& out_auroc,
-              const optional<Tensor>& out_auprc, const optional<Tensor>& init,
-              const optional<Tensor>& out_raw, int64_t payload_kind) {
+// shared argument set-up of the K3 scans (auc_scan, the K3c curve passes); tg / w keep any
+// contiguous copies alive for the launch
+static tea::AucScanArgs scan_args(const Tensor& sorted, const Tensor& order, const Tensor& target,
+                                  const optional<Tensor>& weight, bool class_mode, int64_t payload_kind,
+                                  Tensor& tg, Tensor& w, const char* who) {
   check_gpu(sorted, "sorted");
   TORCH_CHECK(sorted.dim() == 2 && order.dim() == 2 && sorted.sizes() == order.sizes(),
-              "auc_scan: sorted/order must be [rows, n]");
-  TORCH_CHECK(sorted.stride(1) == 1 && order.stride(1) == 1, "auc_scan: rows must be contiguous");
+              who, ": sorted/order must be [rows, n]");
+  TORCH_CHECK(sorted.stride(1) == 1 && order.stride(1) == 1, who, ": rows must be contiguous");
   TORCH_CHECK(sorted.scalar_type() == at::kFloat || sorted.scalar_type() == at::kDouble,
-              "auc_scan: scores must be float32/float64");
+              who, ": scores must be float32/float64");
   TORCH_CHECK(order.scalar_type() == at::kLong || order.scalar_type() == at::kInt,
-              "auc_scan: order must be int64 or int32");
-  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
+              who, ": order must be int64 or int32");
   const int64_t rows = sorted.size(0), n = sorted.size(1);
   tea::AucScanArgs a;
   a.sorted = sorted.data_ptr();
@@ -304,22 +304,20 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
   if (order.scalar_type() == at::kLong) a.order = order.data_ptr<int64_t>();
   else a.order32 = order.data_ptr<int32_t>();
   a.order_stride = order.stride(0);
-  Tensor tg = target;
+  tg = target;
   if (class_mode) {
-    TORCH_CHECK(tg.dim() == 1 && tg.size(0) == n, "auc_scan: class-mode target must be [n]");
+    TORCH_CHECK(tg.dim() == 1 && tg.size(0) == n, who, ": class-mode target must be [n]");
     tg = tg.contiguous();
   } else {
-    TORCH_CHECK(tg.dim() == 2 && tg.size(0) == rows && tg.size(1) == n,
-                "auc_scan: target must be [rows, n]");
+    TORCH_CHECK(tg.dim() == 2 && tg.size(0) == rows && tg.size(1) == n, who, ": target must be [rows, n]");
     if (tg.stride(1) != 1) tg = tg.contiguous();
     a.target_stride = tg.stride(0);
   }
   a.target = tg.data_ptr();
   a.tg_dt = dt_of(tg);
-  Tensor w;
   if (weight.has_value()) {
     w = *weight;
-    TORCH_CHECK(w.dim() == 2 && w.size(0) == rows && w.size(1) == n, "auc_scan: weight must be [rows, n]");
+    TORCH_CHECK(w.dim() == 2 && w.size(0) == rows && w.size(1) == n, who, ": weight must be [rows, n]");
     if (w.stride(1) != 1) w = w.contiguous();
     a.weight = w.data_ptr();
     a.w_dt = dt_of(w);
@@ -327,10 +325,21 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
   }
   a.class_mode = class_mode ? 1 : 0;
   TORCH_CHECK(payload_kind == 0 || (order.scalar_type() == at::kInt && !weight.has_value()),
-              "auc_scan: a payload order must be int32 and unweighted");
+              who, ": a payload order must be int32 and unweighted");
   a.payload_kind = static_cast<int>(payload_kind);
   a.rows = rows;
   a.n = n;
+  return a;
+}
+
+void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
+              const optional<Tensor>& weight, bool class_mode, const optional<Tensor>& out_auroc,
+              const optional<Tensor>& out_auprc, const optional<Tensor>& init,
+              const optional<Tensor>& out_raw, int64_t payload_kind) {
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
+  Tensor tg, w;
+  tea::AucScanArgs a = scan_args(sorted, order, target, weight, class_mode, payload_kind, tg, w, "auc_scan");
+  const int64_t rows = a.rows, n = a.n;
   auto f64_out = [&](const optional<Tensor>& t, const char* name) -> double* {
     if (!t.has_value()) return nullptr;
     TORCH_CHECK(t->scalar_type() == at::kDouble && t->is_contiguous() && t->numel() == rows &&
@@ -353,6 +362,70 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
   Tensor ws = at::empty({tea::auc_scan_workspace_bytes(rows, n)},
                         at::TensorOptions().dtype(at::kByte).device(sorted.device()));
   check_launch(tea::launch_auc_scan(a, ws.data_ptr(), stream_for(sorted)), "auc_scan");
+}
+
+// ---------------------------------------------------------------- K3c curves
+int64_t curve_workspace_bytes(int64_t rows, int64_t n, bool rafp) {
+  return tea::curve_workspace_bytes(rows, n, rafp);
+}
+
+// passes 1-2: tile totals / tie-group tails and per-row scans into `workspace`; G_r -> sizes
+void curve_count(const Tensor& sorted, const Tensor& order, const Tensor& target, bool class_mode,
+                 int64_t payload_kind, const Tensor& workspace, const Tensor& sizes) {
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
+  Tensor tg, w;
+  tea::AucScanArgs a = scan_args(sorted, order, target, c10::nullopt, class_mode, payload_kind, tg, w, "curve_count");
+  TORCH_CHECK(workspace.is_contiguous() && workspace.scalar_type() == at::kByte &&
+                  workspace.numel() >= tea::curve_workspace_bytes(a.rows, a.n, false),
+              "curve_count: workspace too small");
+  TORCH_CHECK(sizes.scalar_type() == at::kLong && sizes.is_contiguous() && sizes.numel() == a.rows,
+              "curve_count: sizes must be contiguous int64 [rows]");
+  a.sizes = sizes.data_ptr<int64_t>();
+  check_launch(tea::launch_curve_count(a, workspace.data_ptr(), false, stream_for(sorted)), "curve_count");
+}
+
+// pass 3: ascending curves into the exact outputs (row_off: int64 [rows] threshold offsets)
+void curve_emit(const Tensor& sorted, const Tensor& order, const Tensor& target, bool class_mode,
+                int64_t payload_kind, const Tensor& workspace, const Tensor& sizes, const Tensor& row_off,
+                const Tensor& out_prec, const Tensor& out_rec, const Tensor& out_thr) {
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
+  Tensor tg, w;
+  tea::AucScanArgs a = scan_args(sorted, order, target, c10::nullopt, class_mode, payload_kind, tg, w, "curve_emit");
+  TORCH_CHECK(workspace.is_contiguous() && workspace.numel() >= tea::curve_workspace_bytes(a.rows, a.n, false),
+              "curve_emit: workspace too small");
+  TORCH_CHECK(sizes.scalar_type() == at::kLong && sizes.numel() == a.rows && row_off.scalar_type() == at::kLong &&
+                  row_off.numel() == a.rows && row_off.is_contiguous() && row_off.device() == sorted.device(),
+              "curve_emit: sizes / row_off must be int64 [rows] on the device");
+  TORCH_CHECK(out_prec.scalar_type() == at::kFloat && out_rec.scalar_type() == at::kFloat &&
+                  out_prec.is_contiguous() && out_rec.is_contiguous() && out_thr.is_contiguous() &&
+                  out_thr.scalar_type() == sorted.scalar_type() && out_prec.numel() == out_thr.numel() + a.rows &&
+                  out_rec.numel() == out_prec.numel(),
+              "curve_emit: outputs must be contiguous f32 [sum G + rows] x2 and key-dtype [sum G]");
+  a.sizes = sizes.data_ptr<int64_t>();
+  a.row_off = row_off.data_ptr<int64_t>();
+  a.out_prec = out_prec.data_ptr<float>();
+  a.out_rec = out_rec.data_ptr<float>();
+  a.out_thr = out_thr.data_ptr();
+  check_launch(tea::launch_curve_emit(a, workspace.data_ptr(), false, stream_for(sorted)), "curve_emit");
+}
+
+// recall at fixed precision per row, no host synchronisation
+void rafp(const Tensor& sorted, const Tensor& order, const Tensor& target, bool class_mode,
+          int64_t payload_kind, double min_precision, const Tensor& out_max_recall, const Tensor& out_best_thr) {
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
+  Tensor tg, w;
+  tea::AucScanArgs a = scan_args(sorted, order, target, c10::nullopt, class_mode, payload_kind, tg, w, "rafp");
+  TORCH_CHECK(out_max_recall.scalar_type() == at::kFloat && out_max_recall.is_contiguous() &&
+                  out_max_recall.numel() == a.rows && out_best_thr.scalar_type() == sorted.scalar_type() &&
+                  out_best_thr.is_contiguous() && out_best_thr.numel() == a.rows,
+              "rafp: outputs must be contiguous f32 [rows] and key-dtype [rows]");
+  Tensor sizes = at::empty({a.rows}, sorted.options().dtype(at::kLong));
+  Tensor ws = at::empty({tea::curve_workspace_bytes(a.rows, a.n, true)}, sorted.options().dtype(at::kByte));
+  a.sizes = sizes.data_ptr<int64_t>();
+  a.min_precision = static_cast<float>(min_precision);
+  a.out_max_recall = out_max_recall.data_ptr<float>();
+  a.out_best_thr = out_best_thr.data_ptr();
+  check_launch(tea::launch_rafp(a, ws.data_ptr(), stream_for(sorted)), "rafp");
 }
 
 // ---------------------------------------------------------------- K4 binned histograms
@@ -788,6 +861,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("order"), py::arg("target"), py::arg("weight"), py::arg("class_mode"),
         py::arg("out_auroc"), py::arg("out_auprc"), py::arg("init") = py::none(),
         py::arg("out_raw") = py::none(), py::arg("payload_kind") = 0);
+  m.def("curve_workspace_bytes", &curve_workspace_bytes, "K3c workspace bytes", py::arg("rows"), py::arg("n"),
+        py::arg("rafp"));
+  m.def("curve_count", &curve_count, "K3c tile totals + tie-group tails + per-row scans (G_r -> sizes)",
+        py::arg("sorted"), py::arg("order"), py::arg("target"), py::arg("class_mode"), py::arg("payload_kind"),
+        py::arg("workspace"), py::arg("sizes"));
+  m.def("curve_emit", &curve_emit, "K3c ascending precision / recall / threshold curves", py::arg("sorted"),
+        py::arg("order"), py::arg("target"), py::arg("class_mode"), py::arg("payload_kind"), py::arg("workspace"),
+        py::arg("sizes"), py::arg("row_off"), py::arg("out_prec"), py::arg("out_rec"), py::arg("out_thr"));
+  m.def("rafp", &rafp, "K3c recall at fixed precision per row (sync-free)", py::arg("sorted"), py::arg("order"),
+        py::arg("target"), py::arg("class_mode"), py::arg("payload_kind"), py::arg("min_precision"),
+        py::arg("out_max_recall"), py::arg("out_best_thr"));
   m.def("binned_counts", &binned_counts, "K4 binned TP/FP/FN per (threshold, class)",
         py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("mode"), py::arg("tp"),
         py::arg("fp"), py::arg("fn"), py::arg("uniform") = 0);

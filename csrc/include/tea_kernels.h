@@ -106,9 +106,31 @@ struct AucScanArgs {
   void* tstart = nullptr;
   void* tarea = nullptr;
   void* totals = nullptr;
+  // K3c curve emission (PR curves / recall at fixed precision)
+  int32_t* tcnt = nullptr;    // [rows, ntiles] tie-group tails per tile
+  int32_t* cstart = nullptr;  // [rows, ntiles] exclusive scan of tcnt
+  int64_t* sizes = nullptr;   // out [rows]: tie groups G_r (curve points without the final one)
+  const int64_t* row_off = nullptr;  // [rows] threshold offset of row r (precision / recall: + r)
+  float* out_prec = nullptr;  // [sum G_r + rows], ascending thresholds, final (1, 0) point per row
+  float* out_rec = nullptr;
+  void* out_thr = nullptr;    // [sum G_r], key dtype
+  float min_precision = 0.f;  // RAFP mode
+  float* s_rec = nullptr;     // [rows, n] recall per group (descending group order)
+  void* s_thr = nullptr;      // [rows, n] threshold per group (key dtype)
+  int32_t* gstar = nullptr;   // [rows] last group with precision >= min_precision (-1: none)
+  int32_t* glo = nullptr;     // [rows] first group whose recall equals the maximum
+  float* out_max_recall = nullptr;  // [rows]
+  void* out_best_thr = nullptr;     // [rows], key dtype
 };
 int64_t auc_scan_workspace_bytes(int64_t rows, int64_t n);
 int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream);
+// K3c: workspace for the curve passes; count (tile sums + tie-group tails, per-row scan, G_r
+// into a.sizes), emit (the compact ascending curves; a.row_off from the host after reading
+// sizes) and the sync-free recall-at-fixed-precision chain (count + emit + search + finalize).
+int64_t curve_workspace_bytes(int64_t rows, int64_t n, bool rafp);
+int launch_curve_count(AucScanArgs& a, void* workspace, bool rafp, hipStream_t stream);
+int launch_curve_emit(AucScanArgs a, void* workspace, bool rafp, hipStream_t stream);
+int launch_rafp(AucScanArgs a, void* workspace, hipStream_t stream);
 
 }  // namespace tea
 

@@ -120,31 +120,59 @@ def multiclass_areas(
     return binary_areas(input.t(), onehot, None, roc=roc, pr=pr)
 
 
-def pr_curve_row(
-    s: torch.Tensor, a: torch.Tensor, b: torch.Tensor, out_dtype: torch.dtype = torch.float32
-) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Precision, recall, thresholds of one sorted row in the reference's layout: ascending
-    thresholds, plus the final (precision=1, recall=0) point; recall is 1 when P == 0."""
-    thr, tp, fp = _row_points(s, a, b)
-    precision = (tp / (tp + fp)).flip(0).to(out_dtype)
-    P = tp[-1]
-    recall = (tp / P).flip(0).to(out_dtype)
-    precision = torch.cat([precision, precision.new_ones(1)])
-    recall = torch.cat([recall, recall.new_zeros(1)])
-    if torch.isnan(recall[0]):
-        recall = torch.nan_to_num(recall, 1.0)
-    return precision, recall, thr.flip(0)
+def _tie_tails(s: torch.Tensor) -> torch.Tensor:
+    """Tie-group tails of descending-sorted rows with the reference's ``diff != 0`` test (so
+    adjacent infinities and NaNs end their own groups, exactly as in precision_recall_curve.py)."""
+    return F.pad(s.diff(dim=-1) != 0, (0, 1), value=True)
 
 
-def pr_curves(
-    x: torch.Tensor, t: torch.Tensor
-) -> Tuple[List[torch.Tensor], List[torch.Tensor], List[torch.Tensor]]:
-    """Per-row PR curves of [rows, n] scores and {0,1} targets."""
-    s, a, b = _sorted_ab(x, t, None)
-    out_p, out_r, out_t = [], [], []
-    for r in range(s.shape[0]):
-        p, rc, th = pr_curve_row(s[r], a[r], b[r])
-        out_p.append(p)
-        out_r.append(rc)
-        out_t.append(th)
-    return out_p, out_r, out_t
+def _curve_tables(x: torch.Tensor, pos: torch.Tensor):
+    """Per-row descending sort -> (sorted keys, tails mask, precision, recall) over every
+    sample of [rows, n]; precision / recall are the reference's int64 / int64 float32 values
+    (recall 1 for a row without positives, the reference's nan_to_num)."""
+    s, idx = torch.sort(x, dim=-1, descending=True)
+    hit = pos.gather(-1, idx)
+    tp = hit.cumsum(-1)
+    fp = (~hit).cumsum(-1)
+    precision = tp / (tp + fp)
+    recall = (tp / tp[..., -1:]).nan_to_num_(1.0)
+    return s, _tie_tails(s), precision, recall
+
+
+def pr_curves(x: torch.Tensor, pos: torch.Tensor) -> Tuple[List[torch.Tensor], List[torch.Tensor], List[torch.Tensor]]:
+    """Per-row PR curves of [rows, n] scores and boolean positives, reference layout: ascending
+    thresholds, then the final (precision 1, recall 0) point.  All rows in one vectorised pass,
+    one host read of the per-row sizes (ATen path; ROCm tensors take K3c, ops/curves.py)."""
+    s, tails, precision, recall = _curve_tables(x, pos)
+    tails = tails.flip(-1)
+    rows = s.shape[0]
+    sizes = tails.sum(-1).tolist()
+    thr = s.flip(-1)[tails].split(sizes)
+    keep = F.pad(tails, (0, 1), value=True)
+    one = precision.new_ones(rows, 1)
+    prec = torch.cat([precision.flip(-1), one], -1)[keep].split([g + 1 for g in sizes])
+    rec = torch.cat([recall.flip(-1), one.zero_()], -1)[keep].split([g + 1 for g in sizes])
+    return list(prec), list(rec), list(thr)
+
+
+def recall_at_precision_rows(
+    x: torch.Tensor, pos: torch.Tensor, min_precision: float
+) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per row of [rows, n]: (max recall over curve points with precision >= min_precision,
+    |highest threshold among the points reaching it|), the appended (1, 0) point included with
+    threshold -1 (recall_at_fixed_precision.py:131-141 semantics), vectorised over rows with no
+    host synchronisation."""
+    s, tails, precision, recall = _curve_tables(x, pos)
+    if not s.is_floating_point():  # the reference's cat with the float -1 promotes
+        s = s.float()
+    rows = s.shape[0]
+    p = torch.tensor(min_precision, dtype=precision.dtype)
+    qual = tails & (precision >= p)
+    zero = recall.new_zeros(rows, 1)
+    max_recall = torch.cat([torch.where(qual, recall, recall.new_full((), -1.0)), zero], -1).amax(-1)
+    hit = tails & (recall == max_recall[:, None])
+    neg_inf = torch.tensor(float("-inf"), dtype=s.dtype)
+    cand = torch.where(hit, s, neg_inf)
+    best = cand.amax(-1)  # a NaN candidate propagates, as in the reference's torch.max
+    best = torch.where(max_recall == 0, torch.maximum(best, torch.full_like(best, -1.0)), best)
+    return max_recall, best.abs()

@@ -1,8 +1,11 @@
 """Precision-recall curves, functional API (parity: precision_recall_curve.py:19-333).
 
-Curves are variable length (one point per distinct threshold), so they are assembled with
-device sort + cumsum + compaction (one per row); the reference's per-label Python loop of
-TorchScript calls (:296-310) becomes a single batched sort over all rows.
+Curves are variable length (one point per distinct threshold).  ROCm tensors run K3c
+(csrc/kernels/curves.hip via ``ops/curves.py``): one batched payload sort over all rows, count
++ scan, one host read of the per-row sizes, emission straight into the exact outputs.  Other
+devices take the vectorised ATen form in ``_curve.pr_curves`` (all rows at once, one size
+read).  The reference's per-label Python loop of TorchScript calls (:296-310) and its per-row
+``torch.isnan(recall[0])`` host read (:226) have no counterpart here.
 """
 
 from typing import List, Optional, Tuple
@@ -12,6 +15,7 @@ import torch
 from torcheval_amd.metrics.functional.tensor_utils import _require_samples
 
 from torcheval_amd.metrics.functional.classification._curve import pr_curves
+from torcheval_amd.ops import use_native
 
 
 @torch.inference_mode()
@@ -32,8 +36,7 @@ def _binary_precision_recall_curve_update(input: torch.Tensor, target: torch.Ten
 def _binary_precision_recall_curve_compute(
     input: torch.Tensor, target: torch.Tensor
 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    p, r, t = pr_curves(input.unsqueeze(0), (target == 1).unsqueeze(0))
-    return p[0], r[0], t[0]
+    return _compute_for_each_class(input, target, 1)
 
 
 def _binary_precision_recall_curve_update_input_check(input: torch.Tensor, target: torch.Tensor) -> None:
@@ -70,6 +73,10 @@ def _multiclass_precision_recall_curve_compute(
 ) -> Tuple[List[torch.Tensor], List[torch.Tensor], List[torch.Tensor]]:
     if num_classes is None:
         num_classes = input.shape[1]
+    if use_native(input) and target.is_cuda and input.shape[0] > 0:
+        from torcheval_amd.ops.curves import multiclass_pr_curves
+
+        return multiclass_pr_curves(input, target)
     onehot = target[None, :] == torch.arange(num_classes, device=target.device)[:, None]
     return pr_curves(input.t(), onehot)
 
@@ -93,6 +100,10 @@ def _multiclass_precision_recall_curve_update_input_check(
 def _compute_for_each_class(
     input: torch.Tensor, target: torch.Tensor, pos_label: int
 ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    if use_native(input) and target.is_cuda and input.numel() > 0:
+        from torcheval_amd.ops.curves import binary_pr_curve
+
+        return binary_pr_curve(input, target, pos_label)
     p, r, t = pr_curves(input.unsqueeze(0), (target == pos_label).unsqueeze(0))
     return p[0], r[0], t[0]
 
@@ -119,6 +130,10 @@ def _multilabel_precision_recall_curve_update(
 def _multilabel_precision_recall_curve_compute(
     input: torch.Tensor, target: torch.Tensor, num_labels: int
 ) -> Tuple[List[torch.Tensor], List[torch.Tensor], List[torch.Tensor]]:
+    if use_native(input) and target.is_cuda and input.shape[0] > 0:
+        from torcheval_amd.ops.curves import multilabel_pr_curves
+
+        return multilabel_pr_curves(input, target)
     return pr_curves(input.t(), target.t() == 1)
 
 
