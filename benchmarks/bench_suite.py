@@ -198,6 +198,24 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
 
     D = 2048 if s >= 1 else 64
 
+    def k5b(cls, kind):
+        def make():
+            x = rand(B, C)
+            if kind == "sum":
+                m = cls(device=dev)
+                return lambda: m.update(x)
+            if kind == "psnr":
+                t = rand(B, C)
+                m = cls(device=dev)
+                return lambda: m.update(x, t)
+            clicks = (rand(64, B * C // 64) < 0.3).float()
+            w = rand(64, B * C // 64)
+            m = cls(num_tasks=64, device=dev)
+            if kind == "ctr":
+                return lambda: m.update(clicks, w)
+            return lambda: m.update(w, clicks, w)
+        return make
+
     def fid_update():
         from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
 
@@ -259,6 +277,12 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "perplexity (4,1024,32000)": ppl,
         "mean_squared_error 8192x1000": mse,
         "r2_score 8192x1000": r2,
+        "Sum.update 8192x1000 (K5b)": k5b(M.Sum, "sum"),
+        "Mean.update 8192x1000 (K5b)": k5b(M.Mean, "sum"),
+        "PeakSignalNoiseRatio.update 8192x1000 (K5b)": k5b(M.PeakSignalNoiseRatio, "psnr"),
+        "ClickThroughRate(64 tasks).update 8192x1000 (K5b)": k5b(M.ClickThroughRate, "ctr"),
+        "WeightedCalibration(64 tasks).update 8192x1000 (K5b)": k5b(M.WeightedCalibration, "wc"),
+        "WindowedClickThroughRate(64 tasks).update 8192x1000 (K5b)": k5b(M.WindowedClickThroughRate, "ctr"),
         "FID update 1000x2048 activations": fid_update,
         "FID compute D=2048": fid_compute,
     }

@@ -51,6 +51,16 @@ def main() -> None:
     ym = torch.randint(0, 100, (100_000,), device=dev, generator=g)
     mb = M.MulticlassBinnedAUPRC(num_classes=100, threshold=100, device=dev)
     work.append(("K4 dense multiclass 100k x 100 T=100", lambda: mb.update(xm, ym)))
+    xs = torch.rand(8192, 1000, device=dev, generator=g)
+    ts = torch.rand(8192, 1000, device=dev, generator=g)
+    msum = M.Sum(device=dev)
+    work.append(("K5b sum 8192x1000", lambda: msum.update(xs)))
+    mpsnr = M.PeakSignalNoiseRatio(device=dev)
+    work.append(("K5b psnr 8192x1000", lambda: mpsnr.update(xs, ts)))
+    clicks = (torch.rand(64, 128000, device=dev, generator=g) < 0.3).float()
+    wts = torch.rand(64, 128000, device=dev, generator=g)
+    mctr = M.ClickThroughRate(num_tasks=64, device=dev)
+    work.append(("K5b ctr 64x128000", lambda: mctr.update(clicks, wts)))
     only = os.environ.get("PMC_ONLY")
     if only:
         work = [w for w in work if only in w[0]]

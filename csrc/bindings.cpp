@@ -428,6 +428,74 @@ void rafp(const Tensor& sorted, const Tensor& order, const Tensor& target, bool 
   check_launch(tea::launch_rafp(a, ws.data_ptr(), stream_for(sorted)), "rafp");
 }
 
+// ---------------------------------------------------------------- K5b per-row weighted sums
+// x: [rows, n] view (t, w: the same shape, any strides; w may be absent -> w_scalar).
+// outs[k] receives stat codes[k] / 8 with op codes[k] % 4 (see tea::RowStat / tea::RowOp), bit 2
+// of the code = row 0 only (a scalar state): f32 / f64 tensors of `rows` elements (any stride:
+// a ring-buffer column works), or of one element for row-0-only outputs.  CUDA tensors
+// run K5b (one launch, two for rows > 64K elements); CPU tensors the host twin.
+void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<Tensor>& w_in, double w_scalar,
+              const std::vector<Tensor>& outs, const std::vector<int64_t>& codes, int64_t rows) {
+  // any shape: a [rows, n] view is used as is, anything else is viewed as rows x (numel / rows)
+  auto as_rows = [&](const Tensor& v) -> Tensor {
+    if (v.dim() == 2 && v.size(0) == rows) return v;
+    TORCH_CHECK(rows > 0 && v.numel() % rows == 0, "row_sums: numel not divisible by rows");
+    return v.reshape({rows, v.numel() / rows});
+  };
+  const Tensor x = as_rows(x_in);
+  const optional<Tensor> t = t_in.has_value() ? optional<Tensor>(as_rows(*t_in)) : c10::nullopt;
+  const optional<Tensor> w = w_in.has_value() ? optional<Tensor>(as_rows(*w_in)) : c10::nullopt;
+  TORCH_CHECK(outs.size() == codes.size() && outs.size() <= static_cast<size_t>(tea::kRowSumsMaxOut),
+              "row_sums: outs / codes mismatch");
+  const bool gpu = x.is_cuda();
+  tea::RowSumsArgs a;
+  a.rows = x.size(0);
+  a.n = x.size(1);
+  auto bind_in = [&](const Tensor& v, const void*& p, tea::DType& dt, int64_t& rs, int64_t& cs, const char* nm) {
+    TORCH_CHECK(v.dim() == 2 && v.size(0) == a.rows && v.size(1) == a.n, "row_sums: ", nm, " must match x");
+    TORCH_CHECK(v.is_cuda() == gpu && (!gpu || v.device() == x.device()), "row_sums: ", nm, " on another device");
+    p = v.data_ptr();
+    dt = dt_of(v);
+    rs = v.stride(0);
+    cs = v.stride(1);
+  };
+  bind_in(x, a.x, a.x_dt, a.x_rs, a.x_cs, "x");
+  if (t.has_value()) bind_in(*t, a.t, a.t_dt, a.t_rs, a.t_cs, "t");
+  if (w.has_value()) bind_in(*w, a.w, a.w_dt, a.w_rs, a.w_cs, "w");
+  a.w_scalar = w_scalar;
+  a.nout = static_cast<int>(outs.size());
+  int need = 0;
+  for (size_t k = 0; k < outs.size(); ++k) {
+    const Tensor& o = outs[k];
+    TORCH_CHECK(o.scalar_type() == at::kFloat || o.scalar_type() == at::kDouble, "row_sums: outputs must be f32/f64");
+    const bool first = (codes[k] & 4) != 0;
+    TORCH_CHECK((o.numel() == a.rows || (first && o.numel() == 1)) && o.is_cuda() == gpu,
+                "row_sums: output ", k, " must hold rows elements");
+    TORCH_CHECK(o.dim() <= 1, "row_sums: outputs must be 0-d or 1-d");
+    a.out[k].p = o.data_ptr();
+    a.out[k].dt = o.scalar_type() == at::kFloat ? tea::DType::f32 : tea::DType::f64;
+    a.out[k].stride = o.dim() == 1 ? o.stride(0) : 0;
+    a.out[k].stat = static_cast<int>(codes[k] / 8);
+    a.out[k].op = static_cast<int>(codes[k] % 4);
+    a.out[k].first_row_only = first ? 1 : 0;
+    TORCH_CHECK(a.out[k].stat >= 0 && a.out[k].stat <= tea::kRANGE, "row_sums: bad stat");
+    if (a.out[k].stat < tea::kCOUNT) need |= 1 << a.out[k].stat;
+    if (a.out[k].stat == tea::kRANGE) need |= (1 << tea::kTMIN) | (1 << tea::kTMAX);
+  }
+  a.need = need;
+  if (!gpu) {
+    tea::row_sums_host(a);
+    return;
+  }
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  a.blocks = tea::row_sums_blocks(a.rows, a.n);
+  if (a.blocks > 1) {  // stream-ordered scratch, fully rewritten by every call: cached, no allocation
+    a.ws = static_cast<double*>(zeroed_workspace(x, stream_for(x), a.rows * a.blocks * tea::kRowRaw * 8, 3));
+  }
+  if (a.n == 0 && a.rows > 0) a.blocks = 1;
+  check_launch(tea::launch_row_sums(a, stream_for(x)), "row_sums");
+}
+
 // ---------------------------------------------------------------- K4 binned histograms
 // input: [n, c] view (any strides); target: [n, c] view (mode 0) or [n] labels (mode 1);
 // thr: float32 [T] sorted; tp/fp/fn: float32 [T, c] views sharing strides (accumulated).
@@ -872,6 +940,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rafp", &rafp, "K3c recall at fixed precision per row (sync-free)", py::arg("sorted"), py::arg("order"),
         py::arg("target"), py::arg("class_mode"), py::arg("payload_kind"), py::arg("min_precision"),
         py::arg("out_max_recall"), py::arg("out_best_thr"));
+  m.def("row_sums", &row_sums, "K5b per-row weighted sums merged into state tensors (GPU kernel / host twin)",
+        py::arg("x"), py::arg("t"), py::arg("w"), py::arg("w_scalar"), py::arg("outs"), py::arg("codes"),
+        py::arg("rows") = 1);
   m.def("binned_counts", &binned_counts, "K4 binned TP/FP/FN per (threshold, class)",
         py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("mode"), py::arg("tp"),
         py::arg("fp"), py::arg("fn"), py::arg("uniform") = 0);

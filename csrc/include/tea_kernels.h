@@ -215,6 +215,54 @@ struct MomentsArgs {
 int column_moments_blocks(int64_t n, int64_t d);
 int launch_column_moments(const MomentsArgs& a, hipStream_t stream);
 
+// ------------------------------------------------------------------ K5b per-row weighted sums
+// One pass over [rows, n] x (and t, w) producing per row, in FP64, any of
+//   WX = sum w x   WT = sum w t   W = sum w   SSE = sum (x - t)^2   WSSE = sum w (x - t)^2
+//   WTT = sum w t^2   TMIN / TMAX = min / max t
+//   COUNT = n      RANGE = (merged TMAX output) - (merged TMIN output)
+// (w: an elementwise weight tensor, or the scalar w_scalar), merged straight into state tensors:
+// each output applies op (= / += / min / max) in its own dtype, so a single launch (two for
+// long rows) is the whole update of Sum / Mean / PSNR / ClickThroughRate / WeightedCalibration,
+// including a windowed metric's ring-slot write and its lifetime accumulation.
+enum RowStat : int {
+  kWX = 0, kWT = 1, kW = 2, kSSE = 3, kWSSE = 4, kWTT = 5,  // sums
+  kTMIN = 6, kTMAX = 7,                                      // extrema
+  kCOUNT = 8, kRANGE = 9                                     // derived
+};
+constexpr int kRowSums = 6, kRowRaw = 8;
+enum RowOp : int { kSet = 0, kAdd = 1, kMin = 2, kMax = 3 };
+constexpr int kRowSumsMaxOut = 10;
+struct RowSumsOut {
+  void* p = nullptr;  // element r at r * stride
+  DType dt = DType::f64;
+  int64_t stride = 0;
+  int stat = 0;
+  int op = 0;
+  int first_row_only = 0;  // a scalar state fed by row 0 only (e.g. a shared count)
+};
+struct RowSumsArgs {
+  const void* x = nullptr;  // element (r, i) at r * x_rs + i * x_cs
+  DType x_dt = DType::f32;
+  int64_t x_rs = 0, x_cs = 1;
+  const void* t = nullptr;
+  DType t_dt = DType::f32;
+  int64_t t_rs = 0, t_cs = 1;
+  const void* w = nullptr;
+  DType w_dt = DType::f32;
+  int64_t w_rs = 0, w_cs = 1;
+  double w_scalar = 1.0;
+  int64_t rows = 0, n = 0;
+  int need = 0;  // bit mask of the raw stats to reduce (WX .. TMAX)
+  int nout = 0;
+  RowSumsOut out[kRowSumsMaxOut];
+  double* ws = nullptr;  // [rows, blocks, kRowRaw] partials when blocks > 1
+  int blocks = 1;        // blocks per row
+};
+int row_sums_blocks(int64_t rows, int64_t n);
+int launch_row_sums(const RowSumsArgs& a, hipStream_t stream);
+// the same update on host memory (CPU tensors): the small-batch twin of the kernel
+void row_sums_host(const RowSumsArgs& a);
+
 // ------------------------------------------------------------------ K6 normalized entropy
 struct NeArgs {
   const void* x = nullptr;

@@ -4,6 +4,8 @@ from typing import Optional, Tuple
 
 import torch
 
+from torcheval_amd.ops import rowsums as _rs
+
 __all__ = ["peak_signal_noise_ratio"]
 
 
@@ -14,6 +16,9 @@ def peak_signal_noise_ratio(
     """PSNR = 10 log10(range^2 / MSE); ``data_range`` defaults to target max - min.
     Class version: ``PeakSignalNoiseRatio``."""
     _psnr_param_check(data_range)
+    fused = _psnr_fused(input, target, data_range)
+    if fused is not None:
+        return fused
     if data_range is None:
         data_range_tensor = torch.max(target) - torch.min(target)
     else:
@@ -45,3 +50,20 @@ def _psnr_update(input: torch.Tensor, target: torch.Tensor) -> Tuple[torch.Tenso
 def _psnr_compute(sum_square_error: torch.Tensor, num_observations: torch.Tensor, data_range: torch.Tensor) -> torch.Tensor:
     mse = sum_square_error / num_observations
     return 10 * torch.log10(torch.pow(data_range, 2) / mse)
+
+
+def _psnr_fused(input: torch.Tensor, target: torch.Tensor, data_range: Optional[float]) -> Optional[torch.Tensor]:
+    """K5b: SSE, count and (auto range) target min / max in one launch, then the reference's
+    compute.  Only where every intermediate keeps the reference's dtype (f32 / f64 inputs of
+    one dtype); anything else returns None (ATen path)."""
+    if input.dtype != target.dtype or input.dtype not in (torch.float32, torch.float64):
+        return None
+    if input.shape != target.shape or not _rs.supported(input, target):
+        return None
+    buf = torch.empty(4, dtype=input.dtype, device=input.device)
+    outs = [(buf[0], _rs.SSE, _rs.SET), (buf[1], _rs.COUNT, _rs.SET)]
+    if data_range is None:
+        outs += [(buf[2], _rs.TMIN, _rs.SET), (buf[3], _rs.TMAX, _rs.SET)]
+    _rs.update_states(input, target, None, outs)
+    rng = buf[3] - buf[2] if data_range is None else torch.tensor(data=data_range, device=target.device)
+    return _psnr_compute(buf[0], buf[1], rng)

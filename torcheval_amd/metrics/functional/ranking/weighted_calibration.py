@@ -5,6 +5,7 @@ from typing import Tuple, Union
 import torch
 
 from torcheval_amd.metrics.functional.ranking._rank_common import _num_tasks_check
+from torcheval_amd.ops import rowsums as _rs
 
 __all__ = ["weighted_calibration"]
 
@@ -18,6 +19,15 @@ def weighted_calibration(
     num_tasks: int = 1,
 ) -> torch.Tensor:
     """sum(w * input) / sum(w * target) per task.  Class: ``WeightedCalibration``."""
+    if (input.dtype in (torch.float32, torch.float64) and target.dtype == input.dtype and input.shape == target.shape
+            and _rs.weight_ok(input, weight) and (not isinstance(weight, torch.Tensor) or weight.dtype == input.dtype)
+            and _rs.supported(input, target, weight if isinstance(weight, torch.Tensor) else None)):
+        _num_tasks_check(input, num_tasks)
+        rows = input.shape[0] if input.ndim == 2 else 1
+        buf = torch.empty(2, rows, dtype=input.dtype, device=input.device)
+        _rs.update_states(input, target, weight, [(buf[0], _rs.WX, _rs.SET), (buf[1], _rs.WT, _rs.SET)], rows=rows)
+        wi, wt = (buf[0], buf[1]) if input.ndim == 2 else (buf[0, 0], buf[1, 0])
+        return wi / wt  # K5b sums + one divide
     wi, wt = _weighted_calibration_update(input, target, weight, num_tasks=num_tasks)
     return wi / wt
 

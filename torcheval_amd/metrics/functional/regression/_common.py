@@ -22,3 +22,58 @@ def _update(
     if squared_error.ndim == 2:
         sample_weight = sample_weight.unsqueeze(-1)
     return (squared_error * sample_weight).sum(dim=0), sample_weight.sum(dim=0).squeeze()
+
+
+def _promote_lazy(metric, names, input: torch.Tensor) -> bool:
+    """The reference's lazy shape promotion of 0-d states to [d] on the first 2-D update
+    (done here up front so the fused kernels can accumulate in place).  False when the states
+    and the batch disagree in shape (the ATen path then reproduces the reference's broadcast)."""
+    d = input.shape[1] if input.ndim == 2 else 1
+    states = [getattr(metric, n) for n in names]
+    if input.ndim == 2 and all(s.ndim == 0 for s in states):
+        for n, s in zip(names, states):
+            setattr(metric, n, torch.zeros(d, dtype=s.dtype, device=s.device) + s)
+        return True
+    return all(s.numel() == d and s.ndim == (1 if input.ndim == 2 else 0) for s in states)
+
+
+def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w: Optional[torch.Tensor],
+                            sums, scalars) -> bool:
+    """One-call update of per-column regression sums straight into ``metric``'s f32 states.
+
+    ``sums``: (state name, K5b stat) of the [d] states; ``scalars``: (state name, stat) of the
+    0-d ones (a count or a weight total).  ROCm [n, d] batches run K5 column moments
+    (coalesced over d) accumulating into the states; ROCm [n] batches and small CPU batches
+    run K5b (``ops/rowsums.py``) over the transposed view.  False: take the ATen path."""
+    from torcheval_amd.ops import rowsums as _rs
+
+    if input.dtype != torch.float32 or target.dtype != torch.float32:
+        return False
+    if w is not None and (w.dtype != torch.float32 or w.ndim != 1):
+        return False
+    names = [n for n, _ in sums] + [n for n, _ in scalars]
+    if not all(getattr(metric, n).dtype == torch.float32 and getattr(metric, n).device == input.device for n in names):
+        return False
+    if input.is_cuda and input.ndim == 2:
+        if not _native(input, target, w) or not _promote_lazy(metric, [n for n, _ in sums], input):
+            return False
+        from torcheval_amd.ops.reductions import column_moments
+
+        kw = {"sse": None, "st": None, "stt": None, "sw": None}
+        key = {_rs.WSSE: "sse", _rs.SSE: "sse", _rs.WT: "st", _rs.WTT: "stt", _rs.W: "sw", _rs.COUNT: "sw"}
+        for n, stat in list(sums) + list(scalars):
+            kw[key[stat]] = getattr(metric, n)
+        column_moments(input, target, w, **kw)
+        return True
+    if not _rs.supported(input, target, w) or input.numel() == 0:
+        return False
+    if not _promote_lazy(metric, [n for n, _ in sums], input):
+        return False
+    rows = input.shape[1] if input.ndim == 2 else 1
+    x2 = input.t() if input.ndim == 2 else input.reshape(1, -1)
+    t2 = target.t() if target.ndim == 2 else target.reshape(1, -1)
+    w2 = None if w is None else w.reshape(1, -1).expand(rows, -1)
+    outs = [(getattr(metric, n).reshape(-1), stat, _rs.ADD) for n, stat in sums]
+    outs += [(getattr(metric, n), stat, _rs.ADD | _rs.FIRST_ROW) for n, stat in scalars]
+    _rs.update_states(x2, t2, w2, outs, rows=rows)
+    return True

@@ -6,9 +6,11 @@ import torch
 
 from torcheval_amd.metrics.functional.ranking import (
     _click_through_rate_compute,
+    _click_through_rate_input_check,
     _click_through_rate_update,
 )
 from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.ops import rowsums as _rs
 
 __all__ = ["ClickThroughRate"]
 
@@ -26,12 +28,19 @@ class ClickThroughRate(Metric[torch.Tensor]):
         for name in ("click_total", "weight_total"):
             self._add_state(name, torch.zeros(num_tasks, dtype=torch.float64, device=self.device), merge="sum")
 
-    @torch.inference_mode()
     def update(self, input: torch.Tensor, weights: Union[torch.Tensor, float, int] = 1.0) -> "ClickThroughRate":
-        click_total, weight_total = _click_through_rate_update(input, weights, num_tasks=self.num_tasks)
-        self.click_total = self.click_total + click_total
-        self.weight_total = self.weight_total + weight_total
-        return self
+        if _rs.weight_ok(input, weights) and _rs.supported(
+            input, weights if isinstance(weights, torch.Tensor) else None, states=(self.click_total, self.weight_total)
+        ):
+            _click_through_rate_input_check(input, weights, num_tasks=self.num_tasks)
+            _rs.update_states(input, None, weights, [(self.click_total, _rs.WX, _rs.ADD),
+                                                     (self.weight_total, _rs.W, _rs.ADD)], rows=self.num_tasks)
+            return self
+        with torch.inference_mode():  # the ATen path (the native op records no autograd)
+            click_total, weight_total = _click_through_rate_update(input, weights, num_tasks=self.num_tasks)
+            self.click_total = self.click_total + click_total
+            self.weight_total = self.weight_total + weight_total
+            return self
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:

@@ -8,7 +8,10 @@ from torcheval_amd.metrics.functional.regression import (
     _r2_score_compute,
     _r2_score_param_check,
     _r2_score_update,
+    _r2_score_update_input_check,
 )
+from torcheval_amd.metrics.functional.regression._common import fused_regression_update
+from torcheval_amd.ops import rowsums as _rs
 from torcheval_amd.metrics.metric import Metric
 
 __all__ = ["R2Score"]
@@ -27,17 +30,24 @@ class R2Score(Metric[torch.Tensor]):
         for name in ("sum_squared_obs", "sum_obs", "sum_squared_residual", "num_obs"):
             self._add_state(name, torch.tensor(0.0, device=self.device))
 
-    @torch.inference_mode()
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "R2Score":
-        sso, so, ssr, n = _r2_score_update(input, target)
-        if self.sum_squared_obs.ndim == 0 and sso.ndim == 1:
-            self.sum_squared_obs, self.sum_obs, self.sum_squared_residual = sso, so, ssr
-        else:
-            self.sum_squared_obs += sso
-            self.sum_obs += so
-            self.sum_squared_residual += ssr
-        self.num_obs += n
-        return self
+        _r2_score_update_input_check(input, target)
+        if fused_regression_update(
+            self, input, target, None,
+            [("sum_squared_obs", _rs.WTT), ("sum_obs", _rs.WT), ("sum_squared_residual", _rs.SSE)],
+            [("num_obs", _rs.COUNT)],
+        ):
+            return self
+        with torch.inference_mode():  # the ATen path (the native op records no autograd)
+            sso, so, ssr, n = _r2_score_update(input, target)
+            if self.sum_squared_obs.ndim == 0 and sso.ndim == 1:
+                self.sum_squared_obs, self.sum_obs, self.sum_squared_residual = sso, so, ssr
+            else:
+                self.sum_squared_obs += sso
+                self.sum_obs += so
+                self.sum_squared_residual += ssr
+            self.num_obs += n
+            return self
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:

@@ -71,8 +71,17 @@ class _WindowedSums(Metric):
         slot = self.next_inserted
         for (name, _), v in zip(self._WINDOW, values):
             getattr(self, name)[:, slot] = v
+        self._advance()
+
+    def _slot_views(self) -> List[torch.Tensor]:
+        """The [num_tasks] column views the next update writes (for fused kernels that write the
+        slot themselves and then call ``_advance``)."""
+        slot = self.next_inserted
+        return [getattr(self, name)[:, slot] for name, _ in self._WINDOW]
+
+    def _advance(self) -> None:
         width = getattr(self, self._WINDOW[0][0]).shape[1]
-        self.next_inserted = (slot + 1) % width
+        self.next_inserted = (self.next_inserted + 1) % width
         self._filled = min(self._filled + 1, width)
         self.total_updates += 1
 

@@ -6,9 +6,11 @@ import torch
 
 from torcheval_amd.metrics.functional.ranking import (
     _click_through_rate_compute,
+    _click_through_rate_input_check,
     _click_through_rate_update,
 )
 from torcheval_amd.metrics.window._ring import _WindowedSums
+from torcheval_amd.ops import rowsums as _rs
 
 
 class WindowedClickThroughRate(_WindowedSums):
@@ -32,14 +34,26 @@ class WindowedClickThroughRate(_WindowedSums):
             enable_lifetime=enable_lifetime, device=device,
         )
 
-    @torch.inference_mode()
     def update(self, input: torch.Tensor, weights: Union[torch.Tensor, float, int] = 1.0):
-        click_total, weight_total = _click_through_rate_update(input, weights, num_tasks=self.num_tasks)
-        if self.enable_lifetime:
-            self.click_total += click_total
-            self.weight_total += weight_total
-        self._push((click_total, weight_total))
-        return self
+        slot_c, slot_w = self._slot_views()
+        if _rs.weight_ok(input, weights) and _rs.supported(
+            input, weights if isinstance(weights, torch.Tensor) else None, states=(slot_c, slot_w)
+        ):
+            # K5b: the ring-slot write and the lifetime accumulation in one launch
+            _click_through_rate_input_check(input, weights, num_tasks=self.num_tasks)
+            outs = [(slot_c, _rs.WX, _rs.SET), (slot_w, _rs.W, _rs.SET)]
+            if self.enable_lifetime:
+                outs += [(self.click_total, _rs.WX, _rs.ADD), (self.weight_total, _rs.W, _rs.ADD)]
+            _rs.update_states(input, None, weights, outs, rows=self.num_tasks)
+            self._advance()
+            return self
+        with torch.inference_mode():  # the ATen path (the native op records no autograd)
+            click_total, weight_total = _click_through_rate_update(input, weights, num_tasks=self.num_tasks)
+            if self.enable_lifetime:
+                self.click_total += click_total
+                self.weight_total += weight_total
+            self._push((click_total, weight_total))
+            return self
 
     @torch.inference_mode()
     def compute(self) -> Union[torch.Tensor, Tuple[torch.Tensor, torch.Tensor]]:
