@@ -216,6 +216,16 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
             return lambda: m.update(w, clicks, w)
         return make
 
+    def rp_queries():
+        Q = 1000 if s >= 1 else 10
+        x, y, q = rand(N1M), randint(2, N1M), randint(Q, N1M)
+
+        def run():
+            m = M.RetrievalPrecision(k=10, num_queries=Q, device=dev)
+            m.update(x, y, indexes=q)
+            return m.compute()
+        return run
+
     def fid_update():
         from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
 
@@ -283,6 +293,7 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "ClickThroughRate(64 tasks).update 8192x1000 (K5b)": k5b(M.ClickThroughRate, "ctr"),
         "WeightedCalibration(64 tasks).update 8192x1000 (K5b)": k5b(M.WeightedCalibration, "wc"),
         "WindowedClickThroughRate(64 tasks).update 8192x1000 (K5b)": k5b(M.WindowedClickThroughRate, "ctr"),
+        "RetrievalPrecision(k=10, 1000 queries) update+compute N=1M": rp_queries,
         "FID update 1000x2048 activations": fid_update,
         "FID compute D=2048": fid_compute,
     }

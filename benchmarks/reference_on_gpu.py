@@ -115,6 +115,15 @@ def main() -> None:
          lambda: RF.multilabel_recall_at_fixed_precision(xl, tl, num_labels=100, min_precision=0.5), 10)
     del xl, tl
 
+    qidx = torch.randint(0, 1000, (1_000_000,), device=dev, generator=g)
+
+    def rp_run(mod):
+        m = mod.RetrievalPrecision(k=10, num_queries=1000, device=dev)
+        m.update(s, t, indexes=qidx)
+        return m.compute()
+
+    case("RetrievalPrecision(k=10, 1000 queries) update+compute N=1M", lambda: rp_run(M), lambda: rp_run(RM), 20)
+
     xm = torch.rand(100_000, 100, device=dev, generator=g)
     ym = torch.randint(0, 100, (100_000,), device=dev, generator=g)
     case("multiclass_auroc N=100k C=100", lambda: F.multiclass_auroc(xm, ym, num_classes=100),

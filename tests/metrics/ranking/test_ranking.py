@@ -113,7 +113,7 @@ class TestRankingClasses(MetricClassTester):
         x, t = torch.rand(8, 10), torch.randint(0, 2, (8, 10))
         fx, ft = x.flatten(), t.flatten()
         self.run_class_implementation_tests(
-            metric=RetrievalPrecision(k=5), state_names={"topk", "target"},
+            metric=RetrievalPrecision(k=5), state_names={"topk", "target", "count"},
             update_kwargs={"input": x, "target": t},
             compute_result=retrieval_precision(fx, ft, k=5).reshape(1),
         )
@@ -128,3 +128,66 @@ class TestRankingClasses(MetricClassTester):
         assert torch.isnan(out[2])
         with pytest.raises(ValueError, match="no positive value found"):
             RetrievalPrecision(empty_target_action="err").update(torch.rand(3), torch.zeros(3)).compute()
+
+
+def _rp_oracle(batches, k, num_queries, limit_k_to_size, action):
+    """The reference's algorithm: per-query lists of streaming top-k, then precision@k."""
+    tops = [(torch.empty(0), torch.empty(0)) for _ in range(num_queries)]
+    for x, t, idx in batches:
+        for i in range(num_queries):
+            sel = idx == i
+            if not bool(sel.any()):
+                continue
+            v = torch.cat([tops[i][0], x[sel]])
+            tt = torch.cat([tops[i][1], t[sel].float()])
+            kk = v.numel() if k is None else min(k, v.numel())
+            vv, j = v.topk(kk)
+            tops[i] = (vv, tt[j])
+    out = []
+    for v, t in tops:
+        if not len(t):
+            out.append(float("nan"))
+        elif not bool((t == 1).any()):
+            out.append({"pos": 1.0, "neg": 0.0, "skip": float("nan")}[action])
+        else:
+            total = v.numel() if k is None else (min(k, v.numel()) if limit_k_to_size else k)
+            out.append(float(t.sum()) / total)
+    return torch.tensor(out)
+
+
+@pytest.mark.parametrize("k", [None, 1, 3, 7])
+@pytest.mark.parametrize("limit", [False, True])
+@pytest.mark.parametrize("action", ["neg", "pos", "skip"])
+def test_retrieval_precision_dense_state_matches_oracle(k, limit, action):
+    if limit and k is None:
+        return
+    g = torch.Generator().manual_seed((k or 0) * 7 + int(limit))
+    Q = 6
+    m = RetrievalPrecision(k=k, limit_k_to_size=limit, num_queries=Q, empty_target_action=action)
+    batches = []
+    for n in (13, 0, 40, 5):
+        x = (torch.randint(0, 20, (n,), generator=g) / 20.0)
+        t = torch.randint(0, 2, (n,), generator=g)
+        idx = torch.randint(-1, Q, (n,), generator=g)  # -1: ignored
+        idx[idx == 4] = 5  # query 4 never appears
+        m.update(x, t, indexes=idx)
+        batches.append((x, t, idx))
+    want = _rp_oracle(batches, k, Q, limit, action)
+    torch.testing.assert_close(m.compute(), want, equal_nan=True)
+    # merge two halves == one metric over everything
+    a = RetrievalPrecision(k=k, limit_k_to_size=limit, num_queries=Q, empty_target_action=action)
+    b = RetrievalPrecision(k=k, limit_k_to_size=limit, num_queries=Q, empty_target_action=action)
+    for x, t, idx in batches[:2]:
+        a.update(x, t, indexes=idx)
+    for x, t, idx in batches[2:]:
+        b.update(x, t, indexes=idx)
+    torch.testing.assert_close(a.merge_state([b]).compute(), want, equal_nan=True)
+
+
+def test_retrieval_precision_loads_reference_state_dict():
+    ref_sd = {"topk": [torch.tensor([0.9, 0.5]), torch.empty(0)], "target": [torch.tensor([1.0, 0.0]), torch.empty(0)]}
+    m = RetrievalPrecision(k=2, num_queries=2)
+    m.load_state_dict(ref_sd)
+    out = m.compute()
+    torch.testing.assert_close(out[0], torch.tensor(0.5))
+    assert torch.isnan(out[1])
