@@ -6,6 +6,7 @@
 // not assume, so no kernel ever runs with a mismatched grid.
 #include <torch/extension.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <unordered_map>
 
@@ -488,9 +489,18 @@ void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<T
     return;
   }
   c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  a.blocks = tea::row_sums_blocks(a.rows, a.n);
+  // long rows: partials + ordered combine (two launches) by default; TORCHEVAL_AMD_K5B_FOLD=1
+  // selects the one-launch fold (half the host cost, same device time at 8192 x 1000:
+  // 18.0 vs 11.2 + 5.7 us; profiles/k5b_rowsums_r2.md)
+  static const bool two_launch = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K5B_FOLD");
+    return !(e != nullptr && e[0] == '1');
+  }();
+  a.blocks = two_launch ? tea::row_sums_blocks(a.rows, a.n) : tea::row_sums_fold_blocks(a.rows, a.n);
   if (a.blocks > 1) {  // stream-ordered scratch, fully rewritten by every call: cached, no allocation
     a.ws = static_cast<double*>(zeroed_workspace(x, stream_for(x), a.rows * a.blocks * tea::kRowRaw * 8, 3));
+    if (!two_launch)  // self-cleaning arrival tickets
+      a.ticket = static_cast<unsigned*>(zeroed_workspace(x, stream_for(x), a.rows * 4, 4));
   }
   if (a.n == 0 && a.rows > 0) a.blocks = 1;
   check_launch(tea::launch_row_sums(a, stream_for(x)), "row_sums");

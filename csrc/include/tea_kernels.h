@@ -256,9 +256,11 @@ struct RowSumsArgs {
   int nout = 0;
   RowSumsOut out[kRowSumsMaxOut];
   double* ws = nullptr;  // [rows, blocks, kRowRaw] partials when blocks > 1
+  unsigned* ticket = nullptr;  // [rows] zeroed arrival counters: one-launch fold (left zeroed)
   int blocks = 1;        // blocks per row
 };
-int row_sums_blocks(int64_t rows, int64_t n);
+int row_sums_blocks(int64_t rows, int64_t n);       // two-launch grid (partials + combine)
+int row_sums_fold_blocks(int64_t rows, int64_t n);  // one-launch fold (needs a ticket)
 int launch_row_sums(const RowSumsArgs& a, hipStream_t stream);
 // the same update on host memory (CPU tensors): the small-batch twin of the kernel
 void row_sums_host(const RowSumsArgs& a);

@@ -17,6 +17,8 @@
 // at the end (sum w x = w sum x) instead of per element.  Every input is read once, in 16-B
 // vectors when rows are unit-stride f32.  Each output applies its own op (= / += / min / max)
 // in its own dtype.  Deterministic: fixed partition and combine order.
+#include <algorithm>
+
 #include "tea_common.h"
 #include "tea_kernels.h"
 
@@ -90,9 +92,9 @@ __device__ __forceinline__ Acc wave_merge(Acc a) {
 }
 
 // block reduction; the result is valid in thread 0
-template <int NEED>
+template <int NEED, int BS = kB>
 __device__ Acc block_merge(Acc a) {
-  __shared__ double lds[kB / kWave][kNStat];
+  __shared__ double lds[BS / kWave][kNStat];
   a = wave_merge<NEED>(a);
   const int w = threadIdx.x >> 6;
   if (lane_id() == 0) {
@@ -101,7 +103,7 @@ __device__ Acc block_merge(Acc a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int j = 1; j < kB / kWave; ++j) {
+    for (int j = 1; j < BS / kWave; ++j) {
       Acc b;
 #pragma unroll
       for (int k = 0; k < kNStat; ++k) b.v[k] = lds[j][k];
@@ -112,8 +114,9 @@ __device__ Acc block_merge(Acc a) {
 }
 
 // [lo, hi) of row r; VEC: f32 rows with unit stride, 16-B aligned (x, t, w as present)
-template <int NEED, bool HAS_W, bool VEC>
+template <int NEED, bool HAS_W, bool VEC, int BS = kB>
 __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t hi) {
+  constexpr int64_t kChunk = static_cast<int64_t>(BS) * kVecPerThread * 4;
   constexpr bool HAS_T = (NEED & kNeedT) != 0;
   Acc a;
   acc_init(a);
@@ -124,12 +127,12 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
     const float* wr = HAS_W ? static_cast<const float*>(g.w) + r * g.w_rs : nullptr;
     const int64_t vlo = (lo + 3) / 4 * 4, vhi = hi / 4 * 4;
     // every float4 of the chunk is issued before any arithmetic: one memory round trip
-    for (int64_t base = vlo; base < vhi; base += kPerBlock) {
+    for (int64_t base = vlo; base < vhi; base += kChunk) {
       float4 xv[kVecPerThread], tv[kVecPerThread], wv[kVecPerThread];
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int u = 0; u < kVecPerThread; ++u) {
-        const int64_t i = base + 4 * (static_cast<int64_t>(u) * kB + threadIdx.x);
+        const int64_t i = base + 4 * (static_cast<int64_t>(u) * BS + threadIdx.x);
         const bool ok = i < vhi;
         xv[u] = ok ? *reinterpret_cast<const float4*>(xr + i) : z;
         tv[u] = (HAS_T && ok) ? *reinterpret_cast<const float4*>(tr + i) : z;
@@ -137,7 +140,7 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
       }
 #pragma unroll
       for (int u = 0; u < kVecPerThread; ++u) {
-        const int64_t i = base + 4 * (static_cast<int64_t>(u) * kB + threadIdx.x);
+        const int64_t i = base + 4 * (static_cast<int64_t>(u) * BS + threadIdx.x);
         if (i < vhi) {
           acc_elem<NEED, HAS_W>(a, need, xv[u].x, tv[u].x, wv[u].x);
           acc_elem<NEED, HAS_W>(a, need, xv[u].y, tv[u].y, wv[u].y);
@@ -147,12 +150,12 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
       }
     }
     // ragged head / tail (< 4 elements each side)
-    for (int64_t i = lo + threadIdx.x; i < min(vlo, hi); i += kB)
+    for (int64_t i = lo + threadIdx.x; i < min(vlo, hi); i += BS)
       acc_elem<NEED, HAS_W>(a, need, xr[i], HAS_T ? tr[i] : 0.f, HAS_W ? wr[i] : 0.f);
-    for (int64_t i = max(vhi, vlo) + threadIdx.x; i < hi; i += kB)
+    for (int64_t i = max(vhi, vlo) + threadIdx.x; i < hi; i += BS)
       acc_elem<NEED, HAS_W>(a, need, xr[i], HAS_T ? tr[i] : 0.f, HAS_W ? wr[i] : 0.f);
   } else {
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kB) {
+    for (int64_t i = lo + threadIdx.x; i < hi; i += BS) {
       const double x = load_as_f64(g.x, g.x_dt, r * g.x_rs + i * g.x_cs);
       const double t = HAS_T ? load_as_f64(g.t, g.t_dt, r * g.t_rs + i * g.t_cs) : 0.0;
       const double w = HAS_W ? load_as_f64(g.w, g.w_dt, r * g.w_rs + i * g.w_cs) : 0.0;
@@ -255,6 +258,55 @@ __global__ __launch_bounds__(kB) void row_sums_combine_kernel(RowSumsArgs g) {
   if (threadIdx.x == 0) finish_row<HAS_W>(g, r, m);
 }
 
+// one launch for long rows: <= 256 fat blocks (1024 threads, ~one per CU) each fold a span
+// of the row; each publishes its FP64 partial (plain store -> agent release -> ticket), and
+// the block that draws the row's last ticket acquires, combines the partials in block order
+// (deterministic) and applies the outputs.  With one block per CU the release costs one
+// L2 write-back per CU (the 2000-block variant of this protocol paid 2000 and took 46 us).
+// The ticket resets itself, so the zeroed workspace stays zeroed between calls.
+constexpr int kFB = 1024;
+constexpr int64_t kFoldChunk = static_cast<int64_t>(kFB) * kVecPerThread * 4;
+
+template <int NEED, bool HAS_W, bool VEC>
+__global__ __launch_bounds__(kFB) void row_sums_fold_kernel(RowSumsArgs g, int64_t span) {
+  const int64_t r = blockIdx.y;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * span;
+  const int64_t hi = min(g.n, lo + span);
+  const Acc a = block_merge<NEED, kFB>(reduce_range<NEED, HAS_W, VEC, kFB>(g, r, lo, hi));
+  __shared__ int s_last;
+  if (threadIdx.x == 0) {
+    double* p = g.ws + (r * g.blocks + blockIdx.x) * kNStat;
+#pragma unroll
+    for (int k = 0; k < kNStat; ++k) p[k] = a.v[k];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the partial reached L2 ...
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // ... is written back chip-wide ...
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(g.ticket + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (t == static_cast<unsigned>(g.blocks - 1)) ? 1 : 0;  // ... before the ticket
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  Acc m;
+  acc_init(m);
+  for (int b = threadIdx.x; b < g.blocks; b += kFB) {
+    Acc q;
+    const double* src = g.ws + (r * g.blocks + b) * kNStat;
+#pragma unroll
+    for (int k = 0; k < kNStat; ++k) q.v[k] = src[k];
+    acc_merge<NEED>(m, q);
+  }
+  m = block_merge<NEED, kFB>(m);
+  if (threadIdx.x == 0) {
+    finish_row<HAS_W>(g, r, m);
+    __hip_atomic_store(g.ticket + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 bool vec_ok(const void* p, DType dt, int64_t rs, int64_t cs) {
   return p == nullptr || (dt == DType::f32 && cs == 1 && rs % 4 == 0 && reinterpret_cast<uintptr_t>(p) % 16 == 0);
 }
@@ -264,6 +316,12 @@ int launch_need(const RowSumsArgs& a, bool vec, hipStream_t stream) {
   if (a.blocks <= 1) {
     if (vec) hipLaunchKernelGGL((row_sums_single_kernel<NEED, HAS_W, true>), dim3(a.rows), dim3(kB), 0, stream, a);
     else hipLaunchKernelGGL((row_sums_single_kernel<NEED, HAS_W, false>), dim3(a.rows), dim3(kB), 0, stream, a);
+  } else if (a.ticket) {  // one launch: fat blocks + last-block combine
+    const int64_t span = (a.n + a.blocks - 1) / a.blocks;
+    const int64_t span_c = (span + kFoldChunk - 1) / kFoldChunk * kFoldChunk;
+    const dim3 grid(static_cast<unsigned>(a.blocks), static_cast<unsigned>(a.rows));
+    if (vec) hipLaunchKernelGGL((row_sums_fold_kernel<NEED, HAS_W, true>), grid, dim3(kFB), 0, stream, a, span_c);
+    else hipLaunchKernelGGL((row_sums_fold_kernel<NEED, HAS_W, false>), grid, dim3(kFB), 0, stream, a, span_c);
   } else {
     const dim3 grid(static_cast<unsigned>(a.blocks), static_cast<unsigned>(a.rows));
     if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true>), grid, dim3(kB), 0, stream, a);
@@ -286,9 +344,16 @@ int row_sums_blocks(int64_t rows, int64_t n) {
   return static_cast<int>((n + kPerBlock - 1) / kPerBlock);
 }
 
+int row_sums_fold_blocks(int64_t rows, int64_t n) {
+  if (n <= kSingle) return 1;
+  const int64_t per_row = std::max<int64_t>(2, 256 / std::max<int64_t>(rows, 1));
+  return static_cast<int>(std::min<int64_t>(per_row, (n + kFoldChunk - 1) / kFoldChunk));
+}
+
 int launch_row_sums(const RowSumsArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
   if (a.x == nullptr || (a.blocks > 1 && !a.ws)) return -2;
+  if (a.ticket && a.blocks < 2) return -2;
   const bool vec = vec_ok(a.x, a.x_dt, a.x_rs, a.x_cs) && vec_ok(a.t, a.t_dt, a.t_rs, a.t_cs) &&
                    vec_ok(a.w, a.w_dt, a.w_rs, a.w_cs);
   // the statistic sets the metrics use; W is derived when the weight is a scalar
