@@ -31,6 +31,7 @@ PAGES: Dict[str, Tuple[str, str, List[str]]] = {
         "Metrics",
         "Stateful metric classes (``update`` / ``compute`` / ``merge_state`` / ``state_dict``).",
         [
+            "torcheval_amd.metrics.metric",
             "torcheval_amd.metrics.aggregation",
             "torcheval_amd.metrics.classification",
             "torcheval_amd.metrics.image",

@@ -33,6 +33,8 @@ TSelf = TypeVar("TSelf", bound="Metric")
 TComputeReturn = TypeVar("TComputeReturn")
 TState = Union[torch.Tensor, List[torch.Tensor], Dict[Any, torch.Tensor], int, float]
 
+__doc_name__ = "Metric Base"
+
 MERGE_KINDS = ("sum", "max", "min", "cat", None)
 
 
