@@ -352,7 +352,7 @@ int row_sums_fold_blocks(int64_t rows, int64_t n) {
 
 int launch_row_sums(const RowSumsArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
-  if (a.x == nullptr || (a.blocks > 1 && !a.ws)) return -2;
+  if ((a.n > 0 && a.x == nullptr) || (a.blocks > 1 && !a.ws)) return -2;  // empty rows: outputs only
   if (a.ticket && a.blocks < 2) return -2;
   const bool vec = vec_ok(a.x, a.x_dt, a.x_rs, a.x_cs) && vec_ok(a.t, a.t_dt, a.t_rs, a.t_cs) &&
                    vec_ok(a.w, a.w_dt, a.w_rs, a.w_cs);

@@ -156,6 +156,20 @@ def test_graphed_update_rejects_rebinding_metric():
 
     with pytest.raises(RuntimeError, match="rebinds its states"):
         GraphedUpdate(Rebinding(), torch.rand(8, device="cuda"))
+    class HostCopy(Rebinding):
+        def update(self, x):
+            self.total += torch.tensor(float(x.numel()), device="cuda")  # host -> device copy
+            return self
+
     # an update that copies host data to the device cannot be recorded at all
     with pytest.raises(RuntimeError, match="cannot be captured"):
-        GraphedUpdate(PeakSignalNoiseRatio(device="cuda"), torch.rand(8, device="cuda"), torch.rand(8, device="cuda"))
+        GraphedUpdate(HostCopy(), torch.rand(8, device="cuda"))
+    # PSNR's update is one K5b launch into its states: it records and replays like the eager path
+    x, t = torch.rand(4, 3, 8, 8, device="cuda"), torch.rand(4, 3, 8, 8, device="cuda")
+    graphed_m, eager_m = PeakSignalNoiseRatio(device="cuda"), PeakSignalNoiseRatio(device="cuda")
+    step = GraphedUpdate(graphed_m, x, t)
+    for _ in range(3):
+        x.copy_(torch.rand_like(x))
+        step(x, t)
+        eager_m.update(x, t)
+    torch.testing.assert_close(graphed_m.compute(), eager_m.compute())
