@@ -226,6 +226,18 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
             return m.compute()
         return run
 
+    def fid_50k():
+        # BASELINE config 5 shape: activations streamed into FID's covariance states in batches
+        # of 1000 (50 updates = 50k x 2048), real and fake
+        d = 2048 if s >= 1 else 16
+        acts = [torch.randn(1000 if s >= 1 else 8, d, device=dev, generator=g) for _ in range(4)]
+        m = M.FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=d, device=dev)
+
+        def run():
+            for i in range(50):
+                m.update_activations(acts[i % 4], i % 2 == 0)
+        return run
+
     def fid_update():
         from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
 
@@ -295,6 +307,7 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "WindowedClickThroughRate(64 tasks).update 8192x1000 (K5b)": k5b(M.WindowedClickThroughRate, "ctr"),
         "RetrievalPrecision(k=10, 1000 queries) update+compute N=1M": rp_queries,
         "FID update 1000x2048 activations": fid_update,
+        "FID 50k x 2048 activations (50 updates of 1000)": fid_50k,
         "FID compute D=2048": fid_compute,
     }
 

@@ -983,3 +983,85 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   tea_register_runtime(m);
   tea_register_cpu_metrics(m);
 }
+
+// ---------------------------------------------------------------- torch dispatcher registration
+// The same kernels as schema'd operators, ``torch.ops.torcheval_amd.<name>``: visible to the
+// dispatcher (device routing, torch.compile graphs via the Meta kernels, profiler names,
+// custom-op tooling).  The metric classes keep calling the pybind entry points above directly:
+// one dispatcher hop costs a few us of host time per call, which the per-batch updates avoid.
+// Every op mutates its outputs in place and returns nothing, so the Meta kernels are no-ops.
+namespace {
+
+void op_row_sums(const Tensor& x, const optional<Tensor>& t, const optional<Tensor>& w, double w_scalar,
+                 at::TensorList outs, at::IntArrayRef codes, int64_t rows) {
+  row_sums(x, t, w, w_scalar, outs.vec(), codes.vec(), rows);
+}
+void op_sort_desc(const Tensor& x, const Tensor& s, const Tensor& o, const optional<Tensor>& p, int64_t kind) {
+  sort_desc(x, s, o, p, kind);
+}
+void op_auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target, const optional<Tensor>& weight,
+                 bool class_mode, const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc,
+                 const optional<Tensor>& init, const optional<Tensor>& out_raw, int64_t payload_kind) {
+  auc_scan(sorted, order, target, weight, class_mode, out_auroc, out_auprc, init, out_raw, payload_kind);
+}
+void op_rafp(const Tensor& sorted, const Tensor& order, const Tensor& target, bool class_mode, int64_t kind,
+             double p, const Tensor& out_rec, const Tensor& out_thr) {
+  rafp(sorted, order, target, class_mode, kind, p, out_rec, out_thr);
+}
+void op_fid_cov_update(const Tensor& act, const Tensor& cov, const optional<Tensor>& colsum) {
+  fid_cov_update(act, cov, colsum);
+}
+void op_perplexity_sums(const Tensor& input, const Tensor& target, optional<int64_t> ignore_index,
+                        const Tensor& out, const optional<Tensor>& err, bool deterministic) {
+  perplexity_sums(input, target, ignore_index, out, err, deterministic);
+}
+void op_transpose_f32(const Tensor& x, const Tensor& out) { transpose_f32(x, out); }
+void op_cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t num_classes,
+                   const optional<Tensor>& micro_correct, const optional<Tensor>& micro_total,
+                   const optional<Tensor>& cls_correct, const optional<Tensor>& cls_label,
+                   const optional<Tensor>& cls_pred, const optional<Tensor>& confusion,
+                   const optional<Tensor>& err) {
+  cls_counts(input, target, k, num_classes, micro_correct, micro_total, cls_correct, cls_label, cls_pred,
+             confusion, err, 0, c10::nullopt, c10::nullopt, c10::nullopt);
+}
+
+}  // namespace
+
+TORCH_LIBRARY(torcheval_amd, m) {
+  m.def("row_sums(Tensor x, Tensor? t, Tensor? w, float w_scalar, Tensor(a!)[] outs, int[] codes, int rows) -> ()");
+  m.def("sort_desc(Tensor x, Tensor(a!) sorted, Tensor(b!) order, Tensor? payload, int payload_kind) -> ()");
+  m.def("auc_scan(Tensor sorted, Tensor order, Tensor target, Tensor? weight, bool class_mode, "
+        "Tensor(a!)? out_auroc, Tensor(b!)? out_auprc, Tensor? init, Tensor(c!)? out_raw, int payload_kind) -> ()");
+  m.def("rafp(Tensor sorted, Tensor order, Tensor target, bool class_mode, int payload_kind, float min_precision, "
+        "Tensor(a!) out_max_recall, Tensor(b!) out_best_thr) -> ()");
+  m.def("fid_cov_update(Tensor act, Tensor(a!) cov, Tensor(b!)? colsum) -> ()");
+  m.def("perplexity_sums(Tensor input, Tensor target, int? ignore_index, Tensor(a!) out, Tensor(b!)? err, "
+        "bool deterministic) -> ()");
+  m.def("transpose_f32(Tensor x, Tensor(a!) out) -> ()");
+  m.def("cls_counts(Tensor input, Tensor target, int k, int num_classes, Tensor(a!)? micro_correct, "
+        "Tensor(b!)? micro_total, Tensor(c!)? cls_correct, Tensor(d!)? cls_label, Tensor(e!)? cls_pred, "
+        "Tensor(f!)? confusion, Tensor(g!)? err) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(torcheval_amd, CUDA, m) {
+  m.impl("row_sums", &op_row_sums);
+  m.impl("sort_desc", &op_sort_desc);
+  m.impl("auc_scan", &op_auc_scan);
+  m.impl("rafp", &op_rafp);
+  m.impl("fid_cov_update", &op_fid_cov_update);
+  m.impl("perplexity_sums", &op_perplexity_sums);
+  m.impl("transpose_f32", &op_transpose_f32);
+  m.impl("cls_counts", &op_cls_counts);
+}
+
+TORCH_LIBRARY_IMPL(torcheval_amd, CPU, m) {
+  m.impl("row_sums", &op_row_sums);  // the C++ host twin
+}
+
+TORCH_LIBRARY_IMPL(torcheval_amd, Meta, m) {
+  m.impl("row_sums", [](const Tensor&, const optional<Tensor>&, const optional<Tensor>&, double, at::TensorList,
+                        at::IntArrayRef, int64_t) {});
+  m.impl("sort_desc", [](const Tensor&, const Tensor&, const Tensor&, const optional<Tensor>&, int64_t) {});
+  m.impl("fid_cov_update", [](const Tensor&, const Tensor&, const optional<Tensor>&) {});
+  m.impl("transpose_f32", [](const Tensor&, const Tensor&) {});
+}
