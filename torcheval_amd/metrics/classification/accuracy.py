@@ -34,10 +34,9 @@ from torcheval_amd.metrics.metric import Metric
 import torcheval_amd.ops as _ops
 from torcheval_amd.ops import native, native_loaded, use_native
 
-# K1 micro-accuracy entry of the loaded extension (None when unbuilt or HIP is disabled)
-_FAST_MICRO = (
-    getattr(_ops._C, "micro_accuracy_update", None) if native_loaded() and not _ops.DISABLE_HIP else None
-)
+# K1 micro-accuracy entry of the loaded extension (None when unbuilt); metrics built while
+# ``torcheval_amd.ops.DISABLE_HIP`` is set do not use it (checked per metric, at construction)
+_FAST_MICRO = getattr(_ops._C, "micro_accuracy_update", None) if native_loaded() else None
 from torcheval_amd.ops.classification import (
     binary_counts,
     cls_counts,
@@ -98,6 +97,7 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         # precondition itself and returns False for anything it does not handle
         self._fast = (
             _FAST_MICRO is not None
+            and not _ops.DISABLE_HIP
             and self.average == "micro"
             and self.k == 1
             and type(self) is MulticlassAccuracy
