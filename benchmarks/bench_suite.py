@@ -238,6 +238,18 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
                 m.update_activations(acts[i % 4], i % 2 == 0)
         return run
 
+    def merge_runs():
+        # the receiver side of a sorted-run sync: 8 ranks x 1M samples (K3m merge + K3 scan)
+        from torcheval_amd.metrics.functional.classification._curve import merged_areas, sort_run
+
+        R, per = (8, n(1_000_000))
+        runs = [sort_run(rand(per), randint(2, per), None) for _ in range(R)]
+        return lambda: merged_areas([r[0] for r in runs], [r[1] for r in runs], None, roc=True, pr=False)
+
+    def union_auroc():
+        x, y = rand(8 * n(1_000_000)), randint(2, 8 * n(1_000_000))
+        return lambda: F.binary_auroc(x, y)
+
     def fid_update():
         from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
 
@@ -306,6 +318,8 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "WeightedCalibration(64 tasks).update 8192x1000 (K5b)": k5b(M.WeightedCalibration, "wc"),
         "WindowedClickThroughRate(64 tasks).update 8192x1000 (K5b)": k5b(M.WindowedClickThroughRate, "ctr"),
         "RetrievalPrecision(k=10, 1000 queries) update+compute N=1M": rp_queries,
+        "sorted-run AUROC of 8 x 1M synced samples (K3m merge + K3)": merge_runs,
+        "binary_auroc of the 8M union (K3a sort + K3)": union_auroc,
         "FID update 1000x2048 activations": fid_update,
         "FID 50k x 2048 activations (50 updates of 1000)": fid_50k,
         "FID compute D=2048": fid_compute,

@@ -429,6 +429,79 @@ void rafp(const Tensor& sorted, const Tensor& order, const Tensor& target, bool 
   check_launch(tea::launch_rafp(a, ws.data_ptr(), stream_for(sorted)), "rafp");
 }
 
+// ---------------------------------------------------------------- K3m sorted-run merge
+// scores: 1-D float32, the concatenation of len(lengths) runs each sorted descending (NaN
+// first).  Returns (merged scores, int32 positions into `scores`): log2(R) pairwise merge
+// rounds - the merge-path kernel on ROCm tensors, std::merge on CPU tensors.
+std::vector<Tensor> merge_sorted_runs(const Tensor& scores, const std::vector<int64_t>& lengths) {
+  TORCH_CHECK(scores.dim() == 1 && scores.scalar_type() == at::kFloat && scores.is_contiguous(),
+              "merge_sorted_runs: scores must be contiguous float32 [n]");
+  int64_t n = 0;
+  for (int64_t l : lengths) {
+    TORCH_CHECK(l >= 0, "merge_sorted_runs: negative run length");
+    n += l;
+  }
+  TORCH_CHECK(n == scores.numel() && n < (int64_t{1} << 31), "merge_sorted_runs: lengths must sum to numel < 2^31");
+  Tensor k0 = scores.clone();
+  Tensor v0 = at::arange(n, scores.options().dtype(at::kInt));
+  if (lengths.size() <= 1) return {k0, v0};
+  Tensor k1 = at::empty_like(k0), v1 = at::empty_like(v0);
+  std::vector<int64_t> runs(lengths.begin(), lengths.end());
+  const bool gpu = scores.is_cuda();
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(gpu ? c10::optional<c10::Device>(scores.device()) : c10::nullopt);
+  auto lt = [](float x, float y) {  // descending, NaN first: x goes before y
+    const bool xn = x != x, yn = y != y;
+    if (xn || yn) return xn && !yn;
+    return x > y;
+  };
+  while (runs.size() > 1) {
+    std::vector<int64_t> next;
+    int64_t off = 0;
+    float* ki = k0.data_ptr<float>();
+    uint32_t* vi = reinterpret_cast<uint32_t*>(v0.data_ptr<int32_t>());
+    float* ko = k1.data_ptr<float>();
+    uint32_t* vo = reinterpret_cast<uint32_t*>(v1.data_ptr<int32_t>());
+    for (size_t r = 0; r < runs.size(); r += 2) {
+      const int64_t na = runs[r], nb = r + 1 < runs.size() ? runs[r + 1] : 0;
+      if (gpu) {
+        if (nb == 0) {  // odd run out: carry it over
+          check_launch(hipMemcpyAsync(ko + off, ki + off, na * 4, hipMemcpyDeviceToDevice, stream_for(scores)),
+                       "merge_sorted_runs copy");
+          check_launch(hipMemcpyAsync(vo + off, vi + off, na * 4, hipMemcpyDeviceToDevice, stream_for(scores)),
+                       "merge_sorted_runs copy");
+        } else {
+          check_launch(tea::launch_merge_desc(ki + off, vi + off, na, ki + off + na, vi + off + na, nb, ko + off,
+                                              vo + off, stream_for(scores)), "merge_sorted_runs");
+        }
+      } else {
+        // stable two-run merge on the host (ties: the first run first)
+        int64_t i = 0, j = 0, o = off;
+        const float* A = ki + off;
+        const float* B = ki + off + na;
+        while (i < na || j < nb) {
+          const bool take_a = j >= nb || (i < na && !lt(B[j], A[i]));
+          if (take_a) {
+            ko[o] = A[i];
+            vo[o] = vi[off + i];
+            ++i;
+          } else {
+            ko[o] = B[j];
+            vo[o] = vi[off + na + j];
+            ++j;
+          }
+          ++o;
+        }
+      }
+      next.push_back(na + nb);
+      off += na + nb;
+    }
+    std::swap(k0, k1);
+    std::swap(v0, v1);
+    runs.swap(next);
+  }
+  return {k0, v0};
+}
+
 // ---------------------------------------------------------------- K5b per-row weighted sums
 // x: [rows, n] view (t, w: the same shape, any strides; w may be absent -> w_scalar).
 // outs[k] receives stat codes[k] / 8 with op codes[k] % 4 (see tea::RowStat / tea::RowOp), bit 2
@@ -950,6 +1023,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rafp", &rafp, "K3c recall at fixed precision per row (sync-free)", py::arg("sorted"), py::arg("order"),
         py::arg("target"), py::arg("class_mode"), py::arg("payload_kind"), py::arg("min_precision"),
         py::arg("out_max_recall"), py::arg("out_best_thr"));
+  m.def("merge_sorted_runs", &merge_sorted_runs, "K3m merge of descending-sorted runs -> (scores, int32 positions)",
+        py::arg("scores"), py::arg("lengths"));
   m.def("row_sums", &row_sums, "K5b per-row weighted sums merged into state tensors (GPU kernel / host twin)",
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("w_scalar"), py::arg("outs"), py::arg("codes"),
         py::arg("rows") = 1);

@@ -128,6 +128,9 @@ int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream);
 // into a.sizes), emit (the compact ascending curves; a.row_off from the host after reading
 // sizes) and the sync-free recall-at-fixed-precision chain (count + emit + search + finalize).
 int64_t curve_workspace_bytes(int64_t rows, int64_t n, bool rafp);
+// K3m: merge two descending-sorted (score, u32 payload) runs into ko / vo (merge path)
+int launch_merge_desc(const float* ka, const uint32_t* va, int64_t na, const float* kb, const uint32_t* vb, int64_t nb,
+                      float* ko, uint32_t* vo, hipStream_t stream);
 int launch_curve_count(AucScanArgs& a, void* workspace, bool rafp, hipStream_t stream);
 int launch_curve_emit(AucScanArgs a, void* workspace, bool rafp, hipStream_t stream);
 int launch_rafp(AucScanArgs a, void* workspace, hipStream_t stream);

@@ -218,3 +218,23 @@ def test_sample_sharded_auc_rccl(pg):
         torch.testing.assert_close(rocw, binary_auroc(x, t, weight=w).double(), rtol=1e-9, atol=1e-12)
         m = BinaryAUROC(device=DEV).update(x, t)
         torch.testing.assert_close(sharded_compute(m, group=pg), m.compute().double(), rtol=1e-9, atol=1e-12)
+
+
+def test_sorted_run_sync_rccl(pg):
+    """The synced BinaryAUROC / BinaryAUPRC arrive as sorted runs and merge (K3m) on HBM."""
+    from torcheval_amd.metrics import BinaryAUPRC, BinaryAUROC
+    from torcheval_amd.metrics.toolkit import get_synced_metric
+
+    x = torch.randint(0, 300, (50_000,), device=DEV).float() / 300
+    t = torch.randint(0, 2, (50_000,), device=DEV)
+    roc = BinaryAUROC(device=DEV)
+    pr = BinaryAUPRC(device=DEV)
+    for lo in range(0, 50_000, 10_000):
+        roc.update(x[lo:lo + 10_000], t[lo:lo + 10_000])
+        pr.update(x[lo:lo + 10_000], t[lo:lo + 10_000])
+    want_roc, want_pr = roc.compute(), pr.compute()
+    with collectives_at_world_size_1():
+        s_roc, s_pr = get_synced_metric(roc), get_synced_metric(pr)
+    assert s_roc._sorted_runs and s_pr._sorted_runs
+    torch.testing.assert_close(s_roc.compute(), want_roc, rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(s_pr.compute(), want_pr, rtol=1e-6, atol=1e-6)

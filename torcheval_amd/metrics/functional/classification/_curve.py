@@ -176,3 +176,54 @@ def recall_at_precision_rows(
     best = cand.amax(-1)  # a NaN candidate propagates, as in the reference's torch.max
     best = torch.where(max_recall == 0, torch.maximum(best, torch.full_like(best, -1.0)), best)
     return max_recall, best.abs()
+
+
+# ---------------------------------------------------------------- sorted runs
+def sort_run(x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor]):
+    """One 1-D sample set sorted descending (NaN first, as K3a / torch.sort): (scores, targets,
+    weights) permuted together - the form a rank ships to a distributed sync, so the receiver
+    merges sorted runs instead of sorting the union."""
+    if use_native(x) and x.dtype == torch.float32 and x.numel() > 0:
+        from torcheval_amd.ops.sortscan import _sort_rows
+
+        s, idx, _ = _sort_rows(x.reshape(1, -1))
+        perm = idx[0].long()
+        s = s[0]
+    else:
+        s, perm = torch.sort(x, descending=True, stable=True)
+    return s, t[perm], (None if w is None else w[perm])
+
+
+def merged_areas(runs_x, runs_t, runs_w, *, roc: bool, pr: bool):
+    """float64 (AUROC, AUPRC) of the union of 1-D runs that are each sorted descending: the
+    runs are merged (K3m merge path on ROCm, a host merge on CPU; log2(R) passes) and the
+    merged order feeds the K3 scan directly - no sort of the union."""
+    from torcheval_amd.ops import native
+
+    x = torch.cat([r.reshape(-1) for r in runs_x])
+    t = torch.cat([r.reshape(-1) for r in runs_t])
+    w = None if runs_w is None else torch.cat([r.reshape(-1) for r in runs_w])
+    s, order = native().merge_sorted_runs(x.contiguous(), [r.numel() for r in runs_x])
+    if use_native(x) and t.is_cuda:
+        tt = t if t.dtype != torch.bool else t.to(torch.uint8)
+        out_roc = torch.empty(1, dtype=torch.float64, device=x.device) if roc else None
+        out_pr = torch.empty(1, dtype=torch.float64, device=x.device) if pr else None
+        native().auc_scan(s[None], order[None], tt[None], None if w is None else w[None], False,
+                          out_roc, out_pr, None, None, 0)
+        return out_roc, out_pr
+    o = order.long()
+    tt = t[o].to(torch.float64)
+    ww = torch.ones_like(tt) if w is None else w[o].to(torch.float64)
+    _, tp, fp = _row_points(s, ww * tt, ww * (1 - tt))
+    ar, ap = _areas_from_points(tp, fp) if tp.numel() else (
+        torch.tensor(0.5, dtype=torch.float64), torch.tensor(0.0, dtype=torch.float64))
+    return (ar.reshape(1) if roc else None, ap.reshape(1) if pr else None)
+
+
+def runs_mergeable(metric, inputs) -> bool:
+    """Whether a sample-store metric's list states are sorted runs the merge path can take."""
+    return (
+        getattr(metric, "_sorted_runs", False)
+        and len(inputs) >= 1
+        and all(x.dim() == 1 and x.dtype == torch.float32 for x in inputs)
+    )
