@@ -11,6 +11,7 @@ Usage: python benchmarks/bench_suite.py [--only NAME] [--out profiles/bench_suit
 """
 
 import argparse
+import re
 import json
 import os
 import sys
@@ -338,7 +339,7 @@ def main() -> None:
     scale = 0.001 if args.smoke else 1.0
     rows: List[Dict[str, object]] = []
     for name, make in cases(dev, scale).items():
-        if args.only and args.only not in name:
+        if args.only and not re.search(args.only, name):
             continue
         row: Dict[str, object] = {"case": name}
         for mode in ("native", "aten"):
