@@ -1,19 +1,25 @@
-"""K8 (FID covariance SYRK) vs the library GEMM over batch sizes, D = 2048, fp32.
+"""K8 (FID covariance SYRK) vs the library GEMM over batch sizes / feature dims / split-K.
 
-Prints one JSON line per K: K8 time, rocBLAS/hipBLASLt ``act.T @ act`` time, and the
-effective FP32-MFMA rate of K8 on the upper-triangle FLOPs it actually does."""
+    python benchmarks/k8_sweep.py [--d 2048 768] [--k 1000 50000] [--splits 0 1 2 3]
 
+split 0 = the launcher's own choice.  Prints one JSON line per (D, K, split): K8 time, the
+rocBLAS/hipBLASLt ``act.T @ act`` time, the effective FP32-MFMA rate of K8 on the
+upper-triangle FLOPs it does (96 x 96 tiles, diagonal tiles full), and the max relative error
+against an fp64 product of the same activations."""
+
+import argparse
 import json
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, __file__.rsplit("/benchmarks/", 1)[0])
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from torcheval_amd.ops import native  # noqa: E402
 
 
-def timeit(fn, iters=50):
-    for _ in range(5):
+def timeit(fn, iters=30):
+    for _ in range(3):
         fn()
     torch.cuda.synchronize()
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -26,19 +32,40 @@ def timeit(fn, iters=50):
 
 
 def main():
-    D = 2048
-    T = D // 64
-    for K in [int(a) for a in (sys.argv[1:] or ["128", "512", "1000", "2048", "4096", "8192"])]:
-        act = torch.randn(K, D, device="cuda")
-        cov = torch.zeros(D, D, device="cuda")
-        cs = torch.zeros(D, device="cuda")
-        t_k8 = timeit(lambda: native().fid_cov_update(act, cov, cs))
-        out = torch.empty(D, D, device="cuda")
-        t_mm = timeit(lambda: torch.mm(act.T, act, out=out))
-        flops_tri = 2.0 * K * 64 * 64 * T * (T + 1) / 2
-        print(json.dumps({"K": K, "k8_us": round(t_k8, 2), "gemm_us": round(t_mm, 2),
-                          "k8_tflops_tri": round(flops_tri / t_k8 / 1e6, 1),
-                          "gemm_tflops": round(2.0 * K * D * D / t_mm / 1e6, 1)}), flush=True)
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--d", type=int, nargs="+", default=[2048])
+    ap.add_argument("--k", type=int, nargs="+", default=[128, 1000, 4096, 50000])
+    ap.add_argument("--splits", type=int, nargs="+", default=[0])
+    ap.add_argument("--out", default=None)
+    args = ap.parse_args()
+    rows = []
+    for D in args.d:
+        T = (D + 95) // 96
+        for K in args.k:
+            act = torch.randn(K, D, device="cuda")
+            out = torch.empty(D, D, device="cuda")
+            t_mm = timeit(lambda: torch.mm(act.T, act, out=out))
+            ref = act.double().T @ act.double()
+            for sp in args.splits:
+                if sp > 0:
+                    os.environ["TORCHEVAL_AMD_K8_SPLIT"] = str(sp)
+                else:
+                    os.environ.pop("TORCHEVAL_AMD_K8_SPLIT", None)
+                cov = torch.zeros(D, D, device="cuda")
+                cs = torch.zeros(D, device="cuda")
+                native().fid_cov_update(act, cov, cs)
+                err = float(((cov.double() - ref).abs().max() / ref.abs().max()).item())
+                t_k8 = timeit(lambda: native().fid_cov_update(act, cov, cs))
+                flops_tri = 2.0 * K * 96 * 96 * T * (T + 1) / 2
+                row = {"D": D, "K": K, "split": sp, "k8_us": round(t_k8, 2), "gemm_us": round(t_mm, 2),
+                       "speedup_vs_gemm": round(t_mm / t_k8, 2), "k8_tflops_tri": round(flops_tri / t_k8 / 1e6, 1),
+                       "gemm_tflops": round(2.0 * K * D * D / t_mm / 1e6, 1), "max_rel_err": err}
+                rows.append(row)
+                print(json.dumps(row), flush=True)
+    os.environ.pop("TORCHEVAL_AMD_K8_SPLIT", None)
+    if args.out:
+        with open(args.out, "w") as f:
+            json.dump(rows, f, indent=1)
 
 
 if __name__ == "__main__":

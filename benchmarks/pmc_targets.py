@@ -47,6 +47,8 @@ def main() -> None:
     act = torch.randn(1000, 2048, device=dev, generator=g)
     fid = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=2048, device=dev)
     work.append(("K8 fid cov 1000x2048", lambda: fid.update_activations(act, True)))
+    act50k = torch.randn(50_000, 2048, device=dev, generator=g)
+    work.append(("K8 fid cov 50000x2048", lambda: fid.update_activations(act50k, False)))
     xm = torch.rand(100_000, 100, device=dev, generator=g)
     ym = torch.randint(0, 100, (100_000,), device=dev, generator=g)
     mb = M.MulticlassBinnedAUPRC(num_classes=100, threshold=100, device=dev)

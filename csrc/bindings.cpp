@@ -95,6 +95,24 @@ void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, in
   return it->second.data_ptr();
 }
 
+// Scratch that kernels overwrite before reading (no zeroing contract): per (device, stream,
+// slot), grown on demand.
+void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot) {
+  static std::mutex mu;
+  static std::unordered_map<uint64_t, Tensor> cache;
+  const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
+                       (static_cast<uint64_t>(slot) << 48) ^ reinterpret_cast<uint64_t>(stream);
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache.find(key);
+  if (it == cache.end() || it->second.numel() < bytes) {
+    Tensor ws = at::empty({std::max<int64_t>(bytes, 1 << 16)},
+                          at::TensorOptions().dtype(at::kByte).device(like.device()));
+    if (it == cache.end()) it = cache.emplace(key, ws).first;
+    else it->second = ws;
+  }
+  return it->second.data_ptr();
+}
+
 void check_launch(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "torcheval_amd._C: ", what, " launch failed (code ", rc, ")");
 }
@@ -816,6 +834,9 @@ void fid_cov_update(const Tensor& act, const Tensor& cov, const optional<Tensor>
                 "fid_cov_update: colsum must be float32 [d]");
     a.colsum = colsum->data_ptr<float>();
   }
+  a.split = tea::fid_cov_split(a.n, d);
+  if (a.split > 1)
+    a.ws = static_cast<float*>(scratch_workspace(act, stream_for(act), tea::fid_cov_workspace_bytes(d, a.split), 0));
   check_launch(tea::launch_fid_cov(a, stream_for(act)), "fid_cov_update");
 }
 

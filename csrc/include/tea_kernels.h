@@ -325,7 +325,13 @@ struct FidCovArgs {
   int64_t n = 0, d = 0, row_stride = 0;
   float* cov = nullptr;     // [d, d] contiguous, += act^T act
   float* colsum = nullptr;  // [d], += column sums (optional)
+  int split = 1;            // K-range items per output tile (> 1: partials + fix-up pass)
+  float* ws = nullptr;      // split > 1: fid_cov_workspace_bytes(d, split) of scratch
 };
+// split-K factor the launcher would pick for [n, d] on this device (env TORCHEVAL_AMD_K8_SPLIT
+// overrides) and the scratch it needs
+int fid_cov_split(int64_t n, int64_t d);
+int64_t fid_cov_workspace_bytes(int64_t d, int split);
 int launch_fid_cov(const FidCovArgs& a, hipStream_t stream);
 
 }  // namespace tea

@@ -137,6 +137,30 @@ def test_k8_cov_matches_fp64(n, d):
     assert torch.equal(c, c.T)
 
 
+@pytest.mark.parametrize("n,d,split", [(5000, 512, 0), (1000, 2048, 3), (333, 300, 2), (70, 2048, 5)])
+def test_k8_split_k_matches_fp64(n, d, split, monkeypatch):
+    """split-K items (partials + fix-up pass): auto split for a small D, forced splits
+    (including one with an empty last K-range) for the others."""
+    if split:
+        monkeypatch.setenv("TORCHEVAL_AMD_K8_SPLIT", str(split))
+    g = torch.Generator().manual_seed(n + d)
+    act = torch.randn(n, d, generator=g)
+    cov0 = torch.randn(d, d, generator=g)
+    cov0 = cov0 + cov0.T
+    s0 = torch.randn(d, generator=g)
+    cov, s = cov0.to(DEV), s0.to(DEV)
+    native().fid_cov_update(act.to(DEV), cov, s)
+    torch.cuda.synchronize()
+    ref = cov0.double() + act.double().T @ act.double()
+    torch.testing.assert_close(cov.cpu().double(), ref, rtol=1e-4, atol=1e-3 * math.sqrt(n))
+    torch.testing.assert_close(s.cpu().double(), s0.double() + act.double().sum(0), rtol=1e-5, atol=1e-3)
+    c = cov.cpu() - cov0
+    assert torch.equal(c, c.T)
+    again = cov0.to(DEV)
+    native().fid_cov_update(act.to(DEV), again, None)
+    assert torch.equal(again.cpu(), cov.cpu())  # deterministic for a given split
+
+
 def test_k8_strided_activations():
     g = torch.Generator().manual_seed(3)
     big = torch.randn(50, 2048 + 32, generator=g)
