@@ -32,6 +32,11 @@ int main(int argc, char** argv) {
     a.cov = cov;
     a.colsum = cs;
     a.split = 1;
+    a.ld = d;
+    float* zeros;
+    CK(hipMalloc(&zeros, 64));
+    CK(hipMemset(zeros, 0, 64));
+    a.zeros = zeros;
     for (int i = 0; i < 3; ++i) CK(static_cast<hipError_t>(tea::launch_fid_cov(a, 0)));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));

@@ -812,13 +812,18 @@ void perplexity_sums(const Tensor& input, const Tensor& target, optional<int64_t
 }
 
 // ---------------------------------------------------------------- K8 FID covariance
-void fid_cov_update(const Tensor& act, const Tensor& cov, const optional<Tensor>& colsum) {
-  check_gpu(act, "activations");
-  TORCH_CHECK(act.dim() == 2 && act.scalar_type() == at::kFloat && act.stride(1) == 1,
+void fid_cov_update(const Tensor& act_in, const Tensor& cov, const optional<Tensor>& colsum) {
+  check_gpu(act_in, "activations");
+  TORCH_CHECK(act_in.dim() == 2 && act_in.scalar_type() == at::kFloat && act_in.stride(1) == 1,
               "fid_cov_update: activations must be float32 [n, d] with unit column stride");
+  const int64_t d = act_in.size(1);
+  // K8 stages 16-byte pieces: rows must start 16-byte aligned and a width that is not a
+  // multiple of 4 is zero-padded (one copy; the FID feature widths 64 / 192 / 768 / 2048 never
+  // need it)
+  Tensor act = act_in;
+  if (d % 4 != 0) act = at::constant_pad_nd(act_in, {0, 4 - d % 4}, 0);
   TORCH_CHECK(act.stride(0) % 4 == 0 && reinterpret_cast<uintptr_t>(act.data_ptr()) % 16 == 0,
               "fid_cov_update: activation rows must be 16-byte aligned");
-  const int64_t d = act.size(1);
   TORCH_CHECK(cov.scalar_type() == at::kFloat && cov.is_contiguous() && cov.numel() == d * d &&
                   cov.device() == act.device(),
               "fid_cov_update: cov must be a contiguous float32 [d, d] on the same device");
@@ -827,8 +832,10 @@ void fid_cov_update(const Tensor& act, const Tensor& cov, const optional<Tensor>
   a.act = act.data_ptr<float>();
   a.n = act.size(0);
   a.d = d;
+  a.ld = act.size(1);
   a.row_stride = act.stride(0);
   a.cov = cov.data_ptr<float>();
+  a.zeros = static_cast<const float*>(zeroed_workspace(act, stream_for(act), 64, 6));
   if (colsum.has_value()) {
     TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->is_contiguous() && colsum->numel() == d,
                 "fid_cov_update: colsum must be float32 [d]");

@@ -321,8 +321,10 @@ namespace tea {
 
 // ------------------------------------------------------------------ K8 FID covariance
 struct FidCovArgs {
-  const float* act = nullptr;  // [n, d] activations (row stride, unit column stride)
+  const float* act = nullptr;  // [n, ld] activations (row stride, unit column stride)
   int64_t n = 0, d = 0, row_stride = 0;
+  int64_t ld = 0;               // loaded width: d rounded up to 4 (columns [d, ld) must be 0)
+  const float* zeros = nullptr;  // >= 16 B of zeros (the source of masked LDS-DMA slots)
   float* cov = nullptr;     // [d, d] contiguous, += act^T act
   float* colsum = nullptr;  // [d], += column sums (optional)
   int split = 1;            // K-range items per output tile (> 1: partials + fix-up pass)

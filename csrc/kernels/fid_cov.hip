@@ -4,26 +4,27 @@
 // symmetric rank-k update that computes only the upper-triangle tiles (half the FLOPs),
 // mirrors them, and fuses the column sums into the diagonal tiles.
 //
-// gfx950 mapping, v3.  Round-1's v2 (64 x 64 tiles, 4 waves each owning one 32 x 32 block)
+// gfx950 mapping, v5.  Round-1's v2 (64 x 64 tiles, 4 waves each owning one 32 x 32 block)
 // ran 82 us at 1000 x 2048 with SQ_VALU_MFMA_BUSY ~33 %: one 32 x 32 accumulator per wave
-// means two LDS operand reads per MFMA and 16 B/clk/CU of L2 operand traffic per block, and
-// D = 2048 gives 528 tiles for 256 CUs (16 CUs run a third tile).  v3 sizes the tile so the
-// upper triangle IS the machine:
+// means two LDS operand reads per MFMA, and D = 2048 gives 528 tiles for 256 CUs (16 CUs run a
+// third tile).  v5 (profiles/k8_fid_cov_r2.md has the measured ladder):
 //  * 96 x 96 output tiles: D = 2048 -> T = 22 tile rows -> 253 upper-triangle tiles, one
 //    workgroup per CU in a single wave of blocks (no quantisation tail).
 //  * 8 waves = 2 per SIMD: wave w owns the 48 x 48 quadrant w & 3 as 3 x 3 blocks of
 //    v_mfma_f32_16x16x4_f32 (exact FP32 products, 9 independent 4-register accumulators), and
 //    the k-steps of parity w >> 2 (in-block 2-way split of K, summed through LDS at the end).
 //    Per 4-k step a wave reads 3 A + 3 B operands (one ds_read_b32 each) for 9 MFMAs - 3x the
-//    operand reuse of v2 - and the next step's operands are read before this step's MFMAs
-//    (register double buffer); the SIMD's second wave covers what LDS latency is left.
-//    (4 waves with one wave per SIMD, measured: 54 TF at 1000 x 2048, 82 TF at 50k x 2048.)
-//  * the K loop streams 64 rows of ``act`` per stage (both operands of sample k are reads of
-//    row k), float4 loads, LDS double buffer (112 KB, dynamic) with a register-staged prefetch
-//    one stage ahead; the loads are branch-free and their consumers are fenced below the
-//    MFMAs with sched_barrier, so the global latency hides behind the matrix work.
-//    LDS rows are padded to 112 floats: the four k-rows one ds_read_b32 touches start 48 banks
-//    apart (mod 64), so the 16-lane row segments never share a bank.
+//    operand reuse of v2 - with the next step's reads pinned ahead of this step's MFMAs
+//    (sched_group_barrier), and the SIMD's second wave covers what LDS latency is left.
+//  * staging by LDS-DMA (global_load_lds_dwordx4): 64 rows of ``act`` per stage, three LDS
+//    stages (144 KB), two stages in flight, counted vmcnt + raw s_barrier.  The operand image
+//    is lane-linear with each row's columns rotated by 16 floats on odd row pairs (rotation
+//    applied to the per-lane source address), so the 4 rows one ds_read_b32 touches hit 4
+//    disjoint 16-bank groups.  Rows past the K range / columns past the width read a zero line.
+//  * diagonal tiles: quadrant (1, 0) is quadrant (0, 1) transposed, so its two waves sum the
+//    tile's columns (the fused colsum) instead of running MFMAs, and the epilogue mirrors it -
+//    the diagonal blocks do no more MFMA-pipe work than the others (a colsum pass on top of
+//    the MFMAs made them the grid's critical path: 112 vs 139 TF/s in the no-load A/B).
 //  * XCD-aware block order: the grid is padded to a multiple of 8 and block b is remapped to
 //    item (b % 8) * (nb / 8) + b / 8, so each XCD owns a contiguous run of row-major tiles
 //    that share their row panel in that XCD's L2.
@@ -53,22 +54,27 @@ namespace {
 #define TEA_K8_SCHED 1
 #endif
 
-constexpr int kT = 96;        // output tile
-constexpr int kBK = 64;       // rows of act per stage
-constexpr int kLD = 112;      // padded LDS row (floats)
+constexpr int kT = 96;         // output tile
+constexpr int kBK = 64;        // rows of act per stage
 constexpr int kThreads = 512;  // 8 waves
 constexpr int kFixThreads = 256;
-constexpr int kStage = kBK * kLD;      // floats per operand per stage
-constexpr int kSegs = kT / 4;          // float4 segments per tile row (24)
-constexpr int kLoads = kBK * kSegs / kThreads;  // float4 loads per thread per operand (3)
+constexpr int kStage = kBK * kT;          // floats per operand per stage (lane-linear image)
+constexpr int kSegs = kT / 4;             // float4 slots per image row (24)
+constexpr int kGlds = kStage / 4 / kThreads;  // global_load_lds_dwordx4 per thread per operand (3)
 constexpr int kCPad = kT + 1;
-static_assert(kBK * kSegs % kThreads == 0, "stage must split evenly over the block");
-static_assert(kT * kCPad <= 4 * kStage, "epilogue tile must fit in the operand buffers");
-constexpr int kSmemBytes = 4 * kStage * 4;  // 112 KB: one block per CU
-static_assert(kCPad * kT + kBK * kT <= 4 * kStage, "epilogue tile + column sums must fit");
-static_assert((kCPad * kT) % 4 == 0, "column-sum partials must stay 16-byte aligned");
+constexpr int kBufs = 3;                    // LDS stages: two LDS-DMA stages in flight
+constexpr int kSmemBytes = 2 * kBufs * kStage * 4;  // 144 KB: one block per CU
+static_assert(kStage % (4 * kThreads) == 0, "stage must split evenly into wave-wide LDS-DMA pieces");
+static_assert(kT * kCPad + 2 * kT <= 2 * kBufs * kStage, "epilogue tile + column sums must fit");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Operand image of one stage: LDS row r (= sample b0 + r) holds the tile's 96 columns rotated
+// by rot(r) floats.  The four rows one ds_read_b32 touches (r = 4q + lk) then start at banks
+// {0, 32, 16, 48} + col (mod 64), so the 16-lane segments never share a bank, and the image
+// stays lane-linear for global_load_lds (whose LDS destination is base + lane x 16 B): the
+// rotation is applied to the per-lane SOURCE address instead.
+__device__ __forceinline__ int rot(int r) { return ((r >> 1) & 1) * 16; }
 
 __device__ __forceinline__ void tile_coords(int t, int T, int& ti, int& tj) {
   // t enumerates the upper triangle (ti <= tj) row by row
@@ -81,18 +87,6 @@ __device__ __forceinline__ void tile_coords(int t, int T, int& ti, int& tj) {
   tj = row + rem;
 }
 
-__device__ __forceinline__ float4 load_seg(const float* row, int64_t c, int64_t d) {
-  if (c + 3 < d) return *reinterpret_cast<const float4*>(row + c);
-  float t[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int e = 0; e < 4; ++e)
-    if (c + e < d) t[e] = row[c + e];
-  return make_float4(t[0], t[1], t[2], t[3]);
-}
-
-// kVec: d % 4 == 0, so every float4 segment of a row is wholly inside or wholly outside [0, d)
-// and the stage loads are branch-free (clamped address + select): no exec-mask branches and no
-// vmcnt waits between the loads of one stage, so all of them overlap the stage's MFMAs.
-template <bool kVec>
 __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T, int tiles, int items, int64_t chunk) {
   const int nb = gridDim.x;
   int item = blockIdx.x;
@@ -106,9 +100,9 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
   const int64_t k0 = ks * chunk;
   const int64_t k1 = min(a.n, k0 + chunk);
 
-  extern __shared__ __attribute__((aligned(16))) float smem[];  // kSmemBytes
-  float* sI = smem;               // [2][kBK][kLD]
-  float* sJ = smem + 2 * kStage;  // [2][kBK][kLD]
+  extern __shared__ __attribute__((aligned(16))) float smem[];  // kSmemBytes, the only LDS object
+  float* sI = smem;                   // [kBufs][kBK][kT] rotated images
+  float* sJ = smem + kBufs * kStage;  // [kBufs][kBK][kT]
   const float* sJr = diag ? sI : sJ;
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -121,91 +115,68 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
   for (int m = 0; m < 3; ++m)
 #pragma unroll
     for (int n = 0; n < 3; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float colsum = 0.f;
 
-  int srow[kLoads], scol[kLoads];
+  // ---- staging: wave w's piece q covers image slots [(3w + q) * 64, +64), lane = slot
+  int prow[kGlds];
+  const float* srcI[kGlds];
+  const float* srcJ[kGlds];
+  bool okI[kGlds], okJ[kGlds];
 #pragma unroll
-  for (int h = 0; h < kLoads; ++h) {
-    const int idx = threadIdx.x + kThreads * h;
-    srow[h] = idx / kSegs;
-    scol[h] = (idx % kSegs) * 4;
+  for (int q = 0; q < kGlds; ++q) {
+    const int p = (w * kGlds + q) * 64 + lane;
+    const int r = p / kSegs;
+    const int c = (4 * (p % kSegs) - rot(r) + kT) % kT;  // source column of this slot
+    prow[q] = r;
+    okI[q] = I0 + c < a.ld;
+    okJ[q] = J0 + c < a.ld;
+    srcI[q] = a.act + static_cast<int64_t>(r) * a.row_stride + I0 + c;
+    srcJ[q] = a.act + static_cast<int64_t>(r) * a.row_stride + J0 + c;
   }
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  // One stage of global loads in registers.  Two sets: the loads of stage s + 2 are issued
-  // at the start of stage s and committed to LDS at the end of stage s + 1, so each load has
-  // two stages of MFMA work (~2 x 4.6k cycles) to land.  fetch issues the loads only; the
-  // zero-masking of out-of-range rows / columns consumes the values, so it is in commit().
-  struct Regs {
-    float4 i[kLoads], j[kLoads];
-    bool vi[kLoads], vj[kLoads];
-  };
-  Regs R0, R1;
-  auto fetch = [&](Regs& R, int64_t b0) {
+  typedef const __attribute__((address_space(1))) void* gptr_t;
+  typedef __attribute__((address_space(3))) void* lptr_t;
+  // rows past the K range and columns past the (4-padded) width read a zero line instead
+  auto issue = [&](int buf, int64_t b0) {
+    const int64_t shift = b0 * a.row_stride;
+    const int64_t rows_left = k1 - b0;
 #pragma unroll
-    for (int h = 0; h < kLoads; ++h) {
-      const int64_t b = b0 + srow[h];
-      const bool vb = b < k1;
-      const float* row = a.act + (vb ? b : k1 - 1) * a.row_stride;  // k1 >= 1: always a real row
-      if constexpr (kVec) {
-        const int64_t ci = I0 + scol[h], cj = J0 + scol[h];
-        R.vi[h] = vb && ci < a.d;
-        R.vj[h] = vb && cj < a.d;
-        R.i[h] = *reinterpret_cast<const float4*>(row + (ci < a.d ? ci : 0));
-        R.j[h] = *reinterpret_cast<const float4*>(row + (cj < a.d ? cj : 0));
-      } else {
-        R.vi[h] = R.vj[h] = true;
-        R.i[h] = vb ? load_seg(row, I0 + scol[h], a.d) : zero4;
-        R.j[h] = vb ? load_seg(row, J0 + scol[h], a.d) : zero4;
+    for (int q = 0; q < kGlds; ++q) {
+      const bool vr = prow[q] < rows_left;
+      const float* gi = vr && okI[q] ? srcI[q] + shift : a.zeros;
+      __builtin_amdgcn_global_load_lds((gptr_t)(gi),
+                                       (lptr_t)(sI + buf * kStage + (w * kGlds + q) * 256), 16, 0, 0);
+      if (!diag) {
+        const float* gj = vr && okJ[q] ? srcJ[q] + shift : a.zeros;
+        __builtin_amdgcn_global_load_lds((gptr_t)(gj),
+                                         (lptr_t)(sJ + buf * kStage + (w * kGlds + q) * 256), 16, 0, 0);
       }
     }
   };
-  // per-component selects: a whole-float4 select gets lowered through a stack slot
-  auto masked = [](const float4& x, bool v) {
-    return make_float4(v ? x.x : 0.f, v ? x.y : 0.f, v ? x.z : 0.f, v ? x.w : 0.f);
-  };
-  // diagonal tiles: column sums ride along in registers (each thread always stages the same
-  // 4 columns), folded through LDS once at the end - a per-stage LDS pass made the diagonal
-  // blocks the slowest blocks of the grid (the no-load loop ran 112 vs 139 TF/s)
-  float4 csum[kLoads];
-#pragma unroll
-  for (int h = 0; h < kLoads; ++h) csum[h] = zero4;
-  auto commit = [&](Regs& R, int buf) {
-    // branch-free (one basic block with the MFMAs, so the scheduler can interleave them):
-    // diagonal tiles also write the unused J buffer, off-diagonal tiles also sum columns
-#pragma unroll
-    for (int h = 0; h < kLoads; ++h) {
-      const int off = buf * kStage + srow[h] * kLD + scol[h];
-      const float4 x = masked(R.i[h], R.vi[h]);
-#ifndef TEA_K8_NO_LDS_WRITE  // (bench variant: loads consumed by the column sums only)
-      *reinterpret_cast<float4*>(sI + off) = x;
-      *reinterpret_cast<float4*>(sJ + off) = masked(R.j[h], R.vj[h]);
-#else
-      csum[h].x += R.j[h].x;
-#endif
-      csum[h].x += x.x;
-      csum[h].y += x.y;
-      csum[h].z += x.z;
-      csum[h].w += x.w;
-    }
-  };
 
+  // ---- operand reads: row r = 8j + 4 par + lk (r % 4 = lk), column c + rot(lk) (mod 96)
+  const int rl = rot(lk);
+  int offA[3], offB[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    offA[m] = (4 * par + lk) * kT + (wr * 48 + 16 * m + li + rl) % kT;
+    offB[m] = (4 * par + lk) * kT + (wc * 48 + 16 * m + li + rl) % kT;
+  }
   auto mma_stage = [&](int buf) {
-    const float* cI = sI + buf * kStage + wr * 48 + li + (4 * par + lk) * kLD;
-    const float* cJ = sJr + buf * kStage + wc * 48 + li + (4 * par + lk) * kLD;
+    const float* cI = sI + buf * kStage;
+    const float* cJ = sJr + buf * kStage;
     float av[2][3], bv[2][3];
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      av[0][m] = cI[16 * m];
-      bv[0][m] = cJ[16 * m];
+      av[0][m] = cI[offA[m]];
+      bv[0][m] = cJ[offB[m]];
     }
 #pragma unroll
-    for (int j = 0; j < kBK / 8; ++j) {  // this wave's k-steps: rows 8j + 4 par + [0, 4)
+    for (int j = 0; j < kBK / 8; ++j) {  // this wave's k-steps
       const int cur = j & 1;
       if (j + 1 < kBK / 8) {
 #pragma unroll
         for (int m = 0; m < 3; ++m) {
-          av[cur ^ 1][m] = cI[(j + 1) * 8 * kLD + 16 * m];
-          bv[cur ^ 1][m] = cJ[(j + 1) * 8 * kLD + 16 * m];
+          av[cur ^ 1][m] = cI[(j + 1) * 8 * kT + offA[m]];
+          bv[cur ^ 1][m] = cJ[(j + 1) * 8 * kT + offB[m]];
         }
       }
 #pragma unroll
@@ -217,56 +188,72 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
 #if TEA_K8_SCHED
     // pin the software pipeline: the first step's operand reads, then per step the next
     // step's reads issued ahead of this step's 9 MFMAs (the default schedule re-reads into
-    // registers that are still feeding MFMAs and waits lgkmcnt(0) right before the next
-    // group), with the stage's LDS commit, global loads and their address / select VALU work
-    // spread over the MFMA gaps instead of forming a serial phase around the barrier
+    // registers that are still feeding MFMAs and waits lgkmcnt(0) right before the next group)
     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
     for (int j = 0; j < kBK / 8; ++j) {
-      if (j < 2 * kLoads) {
-        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
-      }
-      __builtin_amdgcn_sched_group_barrier(0x002, 12, 0);
       if (j + 1 < kBK / 8) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
       __builtin_amdgcn_sched_group_barrier(0x008, 9, 0);
     }
 #endif
   };
 
-  // One K stage, as one basic block: commit stage b0 + BK (loaded during the previous stage,
-  // held in C) into the other LDS buffer - free since the last barrier -, issue the loads of
-  // stage b0 + 2 BK into F, and run the MFMAs on buffer buf, all interleaved; then the
-  // barrier.  Past the end the commits write masked zeros nobody reads and the loads re-read
-  // row k1 - 1, so no branch splits the block.
-  auto stage = [&](int64_t b0, int buf, Regs& F, Regs& C) {
-    __builtin_amdgcn_sched_barrier(0);
-#ifndef TEA_K8_NO_STAGE_LOADS  // (csrc/bench/k8_variants.hip: the loop without its global loads)
-    commit(C, buf ^ 1);
-#ifndef TEA_K8_NO_FETCH
-    fetch(F, b0 + 2 * kBK);
-#endif
-#endif
-    mma_stage(buf);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
+  // ---- diagonal tiles: quadrant (1, 0) is the transpose of quadrant (0, 1), so its two waves
+  // (both on one SIMD) skip their MFMAs and sum the tile's columns instead (wave par: rows of
+  // parity par; lane: columns lane and 64 + lane); the epilogue mirrors (0, 1) into (1, 0).
+  // The diagonal blocks then carry no more MFMA-pipe work than the others, which they would
+  // otherwise add to the kernel's critical path.
+  const bool col_wave = diag && quad == 2;
+  float colsum0 = 0.f, colsum1 = 0.f;
+  auto col_stage = [&](int buf) {
+    const float* img = sI + buf * kStage;
+#pragma unroll 8
+    for (int r = par; r < kBK; r += 2) {
+      colsum0 += img[r * kT + (lane + rot(r)) % kT];
+      if (lane < kT - 64) colsum1 += img[r * kT + (64 + lane + rot(r)) % kT];
+    }
   };
 
-  fetch(R0, k0);
-  commit(R0, 0);
-  fetch(R1, k0 + kBK);
-  __syncthreads();
-  for (int64_t b0 = k0; b0 < k1;) {
-    stage(b0, 0, R0, R1);
-    b0 += kBK;
-    if (b0 >= k1) break;
-    stage(b0, 1, R1, R0);
-    b0 += kBK;
+  // ---- K loop: three LDS stages, two LDS-DMA stages in flight behind the MFMAs.  The end of
+  // stage s waits only for stage s + 1's pieces (a counted vmcnt leaves stage s + 2's in
+  // flight) and meets at a raw s_barrier - __syncthreads() would drain vmcnt to 0.  The buffer
+  // refilled at stage s + 1 is the one stage s read, so that barrier also retires its reads.
+  auto wait_next = [&](bool keep_one) {
+    if (keep_one) {
+      if (diag) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");  // kGlds pieces per stage
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");       // 2 x kGlds
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  };
+  static_assert(kGlds == 3, "the counted waits above assume 3 pieces per operand per stage");
+  issue(0, k0);
+  const bool two = k0 + kBK < k1;
+  if (two) issue(1, k0 + kBK);
+  wait_next(two);
+  int buf = 0;
+  for (int64_t b0 = k0; b0 < k1; b0 += kBK) {
+    const int ahead = buf == 0 ? 2 : buf - 1;  // (buf + 2) % 3
+    const bool more = b0 + 2 * kBK < k1;
+#ifndef TEA_K8_NO_STAGE_LOADS  // (csrc/bench/k8_variants.hip: the loop without its global loads)
+    if (more) issue(ahead, b0 + 2 * kBK);
+#endif
+    if (col_wave) {
+      col_stage(buf);
+    } else {
+      __builtin_amdgcn_sched_barrier(0);
+      mma_stage(buf);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wait_next(more);
+    buf = buf == 2 ? 0 : buf + 1;
   }
 
-  // sum the two k-parity halves of each quadrant in LDS (96 x 97 floats, reusing the operand
-  // buffers; the loop's last barrier retired every operand read)
+  // ---- sum the two k-parity halves of each quadrant in LDS (96 x 97 floats, reusing the
+  // operand buffers; the loop's last barrier retired every operand read)
   float* sC = smem;
+  float* sCol = smem + kCPad * kT;  // [2][kT]: the column-sum waves' partials
   auto to_lds = [&](bool add) {
 #pragma unroll
     for (int m = 0; m < 3; ++m)
@@ -278,19 +265,24 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
           sC[idx] = add ? sC[idx] + acc[m][n][r] : acc[m][n][r];
         }
   };
-  float* sCol = smem + kCPad * kT;  // [kBK][kT] column-sum partials (diagonal tiles)
+  if (col_wave) {
+    sCol[par * kT + lane] = colsum0;
+    if (lane < kT - 64) sCol[par * kT + 64 + lane] = colsum1;
+  }
+  if (par == 1 && !col_wave) to_lds(false);
+  __syncthreads();
+  if (par == 0 && !col_wave) to_lds(true);
+  __syncthreads();
+  float colsum = 0.f;
   if (diag) {
-#pragma unroll
-    for (int h = 0; h < kLoads; ++h) *reinterpret_cast<float4*>(sCol + srow[h] * kT + scol[h]) = csum[h];
+    // quadrant (1, 0) = quadrant (0, 1) transposed; the column sums of the two row parities
+    for (int e = threadIdx.x; e < 48 * 48; e += kThreads) {
+      const int r = 48 + e / 48, c = e % 48;
+      sC[r * kCPad + c] = sC[c * kCPad + r];
+    }
+    if (threadIdx.x < kT) colsum = sCol[threadIdx.x] + sCol[kT + threadIdx.x];
+    __syncthreads();
   }
-  if (par == 1) to_lds(false);
-  __syncthreads();
-  if (par == 0) to_lds(true);
-  if (diag && threadIdx.x < kT) {
-#pragma unroll 8
-    for (int r = 0; r < kBK; ++r) colsum += sCol[r * kT + threadIdx.x];
-  }
-  __syncthreads();
 
   if (a.split > 1) {
     // raw partial tile [kT][kT] (row-major) + diagonal column-sum partial for the fix-up pass
@@ -301,7 +293,7 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
     return;
   }
 
-  // epilogue: coalesced RMW of C[I, J] and the mirrored C[J, I] from the LDS tile
+  // ---- epilogue: coalesced RMW of C[I, J] and the mirrored C[J, I] from the LDS tile
   for (int e = threadIdx.x; e < kT * kT; e += kThreads) {
     const int row = e / kT, col = e % kT;
     const int64_t gi = I0 + row, gj = J0 + col;
@@ -380,8 +372,8 @@ int fid_cov_split(int64_t n, int64_t d) {
   const int64_t cus = cu_count();
   if (tiles * 4 >= cus * 3) return 1;  // the triangle fills >= 3/4 of the CUs already
   const int64_t stages = (n + kBK - 1) / kBK;
-  int64_t s = cus / tiles;            // one item per CU
-  s = std::min<int64_t>(s, stages / 8);  // keep >= 8 stages per item
+  int64_t s = cus / tiles;               // one item per CU
+  s = std::min<int64_t>(s, stages / 2);  // keep >= 2 stages (128 rows) per item
   return static_cast<int>(std::max<int64_t>(s, 1));
 }
 
@@ -403,17 +395,11 @@ int launch_fid_cov(const FidCovArgs& a, hipStream_t stream) {
   const int64_t chunk = ((stages + split - 1) / split) * kBK;
   const int items = tiles * split;
   const int grid = (items + 7) / 8 * 8;
-  static const bool lds_ok = [] {
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel<true>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kSmemBytes) == hipSuccess &&
-           hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel<false>),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, kSmemBytes) == hipSuccess;
-  }();
+  static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel),
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSmemBytes) == hipSuccess;
   if (!lds_ok) return -3;
-  if (a.d % 4 == 0)
-    hipLaunchKernelGGL(fid_syrk_kernel<true>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
-  else
-    hipLaunchKernelGGL(fid_syrk_kernel<false>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
+  if (a.zeros == nullptr || a.ld % 4 != 0 || a.ld < a.d || a.row_stride % 4 != 0) return -1;
+  hipLaunchKernelGGL(fid_syrk_kernel, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
   int rc = static_cast<int>(hipGetLastError());
   if (rc || split == 1) return rc;
   hipLaunchKernelGGL(fid_fixup_kernel, dim3(tiles * 9), dim3(kFixThreads), 0, stream, a, T, tiles);
