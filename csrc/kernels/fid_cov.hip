@@ -18,9 +18,9 @@
 //    (sched_group_barrier), and the SIMD's second wave covers what LDS latency is left.
 //  * staging by LDS-DMA (global_load_lds_dwordx4): 64 rows of ``act`` per stage, three LDS
 //    stages (144 KB), two stages in flight, counted vmcnt + raw s_barrier.  The operand image
-//    is lane-linear with each row's columns rotated by 16 floats on odd row pairs (rotation
-//    applied to the per-lane source address), so the 4 rows one ds_read_b32 touches hit 4
-//    disjoint 16-bank groups.  Rows past the K range / columns past the width read a zero line.
+//    is lane-linear with each row's columns rotated by 0/16/32/48 floats (rotation applied to
+//    the per-lane source address), so the 4 rows one ds_read_b32 touches hit 4 disjoint
+//    16-bank groups.  Rows past the K range / columns past the width read a zero line.
 //  * diagonal tiles: quadrant (1, 0) is quadrant (0, 1) transposed, so its two waves sum the
 //    tile's columns (the fused colsum) instead of running MFMAs, and the epilogue mirrors it -
 //    the diagonal blocks do no more MFMA-pipe work than the others (a colsum pass on top of
@@ -71,10 +71,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // Operand image of one stage: LDS row r (= sample b0 + r) holds the tile's 96 columns rotated
 // by rot(r) floats.  The four rows one ds_read_b32 touches (r = 4q + lk) then start at banks
-// {0, 32, 16, 48} + col (mod 64), so the 16-lane segments never share a bank, and the image
-// stays lane-linear for global_load_lds (whose LDS destination is base + lane x 16 B): the
-// rotation is applied to the per-lane SOURCE address instead.
-__device__ __forceinline__ int rot(int r) { return ((r >> 1) & 1) * 16; }
+// {0, 48, 32, 16} + col (mod 64) - distinct mod 32 within each half-wave too (a rotation of
+// 16 on odd row pairs only gave {0, 32, 16, 48}: 3.8 bank-conflict cycles per LDS instruction
+// measured, as lanes 0-31 then share banks mod 32) - and the image stays lane-linear for
+// global_load_lds (whose LDS destination is base + lane x 16 B): the rotation is applied to
+// the per-lane SOURCE address instead.
+__device__ __forceinline__ int rot(int r) { return (r & 1) * 16 + ((r >> 1) & 1) * 32; }
 
 __device__ __forceinline__ void tile_coords(int t, int T, int& ti, int& tj) {
   // t enumerates the upper triangle (ti <= tj) row by row
@@ -214,6 +216,23 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
     }
   };
 
+  // ---- the C tile (and its mirror) this block read-modify-writes at the end: loaded into
+  // registers now, so the epilogue's reads are not a serial HBM round trip after the loop
+  constexpr int kPer = kT * kT / kThreads;  // 18 elements per thread
+  static_assert(kT * kT % kThreads == 0, "tile must split evenly over the block");
+  float cpre[kPer], mpre[kPer];
+  if (a.split == 1) {
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int e = threadIdx.x + kThreads * q;
+      const int row = e / kT, col = e % kT;
+      const bool in = I0 + row < a.d && J0 + col < a.d;
+      cpre[q] = in ? a.cov[(I0 + row) * a.d + J0 + col] : 0.f;
+      const bool min_ = !diag && J0 + row < a.d && I0 + col < a.d;
+      mpre[q] = min_ ? a.cov[(J0 + row) * a.d + I0 + col] : 0.f;
+    }
+  }
+
   // ---- K loop: three LDS stages, two LDS-DMA stages in flight behind the MFMAs.  The end of
   // stage s waits only for stage s + 1's pieces (a counted vmcnt leaves stage s + 2's in
   // flight) and meets at a raw s_barrier - __syncthreads() would drain vmcnt to 0.  The buffer
@@ -293,15 +312,17 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
     return;
   }
 
-  // ---- epilogue: coalesced RMW of C[I, J] and the mirrored C[J, I] from the LDS tile
-  for (int e = threadIdx.x; e < kT * kT; e += kThreads) {
+  // ---- epilogue: coalesced C[I, J] += tile and mirrored C[J, I] += tile^T (C read up front)
+#pragma unroll
+  for (int q = 0; q < kPer; ++q) {
+    const int e = threadIdx.x + kThreads * q;
     const int row = e / kT, col = e % kT;
     const int64_t gi = I0 + row, gj = J0 + col;
-    if (gi < a.d && gj < a.d) a.cov[gi * a.d + gj] += sC[row * kCPad + col];
+    if (gi < a.d && gj < a.d) a.cov[gi * a.d + gj] = cpre[q] + sC[row * kCPad + col];
     if (!diag) {
       // mirrored tile: C[J0 + row][I0 + col] = tile[col][row]
       const int64_t mi = J0 + row, mj = I0 + col;
-      if (mi < a.d && mj < a.d) a.cov[mi * a.d + mj] += sC[col * kCPad + row];
+      if (mi < a.d && mj < a.d) a.cov[mi * a.d + mj] = mpre[q] + sC[col * kCPad + row];
     }
   }
   if (diag && a.colsum && threadIdx.x < kT && I0 + threadIdx.x < a.d) a.colsum[I0 + threadIdx.x] += colsum;
