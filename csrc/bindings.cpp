@@ -448,68 +448,99 @@ void rafp(const Tensor& sorted, const Tensor& order, const Tensor& target, bool 
 }
 
 // ---------------------------------------------------------------- K3m sorted-run merge
-// scores: 1-D float32, the concatenation of len(lengths) runs each sorted descending (NaN
-// first).  Returns (merged scores, int32 positions into `scores`): log2(R) pairwise merge
-// rounds - the merge-path kernel on ROCm tensors, std::merge on CPU tensors.
-std::vector<Tensor> merge_sorted_runs(const Tensor& scores, const std::vector<int64_t>& lengths) {
-  TORCH_CHECK(scores.dim() == 1 && scores.scalar_type() == at::kFloat && scores.is_contiguous(),
-              "merge_sorted_runs: scores must be contiguous float32 [n]");
+// keys: R 1-D float32 runs, each sorted descending (NaN first).  payloads: optional R 32-bit
+// runs carried with their keys (e.g. the f32 target of each sample, so K3 needs no gather);
+// without them the payload is each sample's position in the concatenation of the runs.
+// Returns (merged keys, merged int32 payload): log2(R) pairwise merge rounds - the merge-path
+// kernel on ROCm tensors, a stable host merge on CPU tensors.  The first round reads the runs
+// in place (no concatenation copy) and positions are generated there (no arange).
+std::vector<Tensor> merge_sorted_runs(const std::vector<Tensor>& keys, const optional<std::vector<Tensor>>& payloads) {
+  TORCH_CHECK(!keys.empty(), "merge_sorted_runs: no runs");
+  const bool carry = payloads.has_value();
+  TORCH_CHECK(!carry || payloads->size() == keys.size(), "merge_sorted_runs: one payload per run");
+  const auto dev = keys[0].device();
+  const bool gpu = keys[0].is_cuda();
   int64_t n = 0;
-  for (int64_t l : lengths) {
-    TORCH_CHECK(l >= 0, "merge_sorted_runs: negative run length");
-    n += l;
+  std::vector<int64_t> len;
+  for (size_t r = 0; r < keys.size(); ++r) {
+    const Tensor& k = keys[r];
+    TORCH_CHECK(k.dim() == 1 && k.scalar_type() == at::kFloat && k.is_contiguous() && k.device() == dev,
+                "merge_sorted_runs: keys must be contiguous float32 [n] runs on one device");
+    if (carry) {
+      const Tensor& v = (*payloads)[r];
+      TORCH_CHECK(v.dim() == 1 && v.numel() == k.numel() && v.is_contiguous() && v.element_size() == 4 &&
+                      v.device() == dev,
+                  "merge_sorted_runs: payloads must be contiguous 32-bit runs matching the keys");
+    }
+    len.push_back(k.numel());
+    n += k.numel();
   }
-  TORCH_CHECK(n == scores.numel() && n < (int64_t{1} << 31), "merge_sorted_runs: lengths must sum to numel < 2^31");
-  Tensor k0 = scores.clone();
-  Tensor v0 = at::arange(n, scores.options().dtype(at::kInt));
-  if (lengths.size() <= 1) return {k0, v0};
-  Tensor k1 = at::empty_like(k0), v1 = at::empty_like(v0);
-  std::vector<int64_t> runs(lengths.begin(), lengths.end());
-  const bool gpu = scores.is_cuda();
-  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(gpu ? c10::optional<c10::Device>(scores.device()) : c10::nullopt);
+  TORCH_CHECK(n < (int64_t{1} << 31), "merge_sorted_runs: fewer than 2^31 samples");
+  const auto fopt = keys[0].options();
+  Tensor k0 = at::empty({n}, fopt), v0 = at::empty({n}, fopt.dtype(at::kInt));
+  Tensor k1 = at::empty({n}, fopt), v1 = at::empty({n}, fopt.dtype(at::kInt));
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(gpu ? c10::optional<c10::Device>(dev) : c10::nullopt);
+  hipStream_t st = gpu ? stream_for(keys[0]) : nullptr;
+  // split scratch for the largest pair (every pair of a round is stream-ordered after the last)
+  Tensor splits = gpu ? at::empty({tea::merge_splits_count(n)}, fopt.dtype(at::kLong)) : Tensor();
   auto lt = [](float x, float y) {  // descending, NaN first: x goes before y
     const bool xn = x != x, yn = y != y;
     if (xn || yn) return xn && !yn;
     return x > y;
   };
+  // one stable two-run merge; va / vb null: payload = base + index
+  auto merge2 = [&](const float* ka, const uint32_t* va, int64_t na, uint32_t base_a, const float* kb,
+                    const uint32_t* vb, int64_t nb, uint32_t base_b, float* ko, uint32_t* vo) {
+    if (gpu) {
+      check_launch(tea::launch_merge_desc(ka, va, na, base_a, kb, vb, nb, base_b, ko, vo, splits.data_ptr<int64_t>(), st),
+                   "merge_sorted_runs");
+      return;
+    }
+    int64_t i = 0, j = 0, o = 0;
+    while (i < na || j < nb) {
+      const bool take_a = j >= nb || (i < na && !lt(kb[j], ka[i]));
+      if (take_a) {
+        ko[o] = ka[i];
+        vo[o] = va ? va[i] : base_a + static_cast<uint32_t>(i);
+        ++i;
+      } else {
+        ko[o] = kb[j];
+        vo[o] = vb ? vb[j] : base_b + static_cast<uint32_t>(j);
+        ++j;
+      }
+      ++o;
+    }
+  };
+  auto pay = [&](size_t r) -> const uint32_t* {
+    return carry ? static_cast<const uint32_t*>((*payloads)[r].data_ptr()) : nullptr;
+  };
+  // round 1: from the runs in place into (k0, v0)
+  std::vector<int64_t> runs;
+  {
+    float* ko = k0.data_ptr<float>();
+    uint32_t* vo = reinterpret_cast<uint32_t*>(v0.data_ptr<int32_t>());
+    int64_t off = 0;
+    for (size_t r = 0; r < keys.size(); r += 2) {
+      const int64_t na = len[r], nb = r + 1 < keys.size() ? len[r + 1] : 0;
+      const float* ka = keys[r].data_ptr<float>();
+      const float* kb = nb ? keys[r + 1].data_ptr<float>() : ka;
+      merge2(ka, pay(r), na, static_cast<uint32_t>(off), kb, nb ? pay(r + 1) : nullptr, nb,
+             static_cast<uint32_t>(off + na), ko + off, vo + off);
+      runs.push_back(na + nb);
+      off += na + nb;
+    }
+  }
   while (runs.size() > 1) {
     std::vector<int64_t> next;
     int64_t off = 0;
-    float* ki = k0.data_ptr<float>();
-    uint32_t* vi = reinterpret_cast<uint32_t*>(v0.data_ptr<int32_t>());
+    const float* ki = k0.data_ptr<float>();
+    const uint32_t* vi = reinterpret_cast<const uint32_t*>(v0.data_ptr<int32_t>());
     float* ko = k1.data_ptr<float>();
     uint32_t* vo = reinterpret_cast<uint32_t*>(v1.data_ptr<int32_t>());
     for (size_t r = 0; r < runs.size(); r += 2) {
       const int64_t na = runs[r], nb = r + 1 < runs.size() ? runs[r + 1] : 0;
-      if (gpu) {
-        if (nb == 0) {  // odd run out: carry it over
-          check_launch(hipMemcpyAsync(ko + off, ki + off, na * 4, hipMemcpyDeviceToDevice, stream_for(scores)),
-                       "merge_sorted_runs copy");
-          check_launch(hipMemcpyAsync(vo + off, vi + off, na * 4, hipMemcpyDeviceToDevice, stream_for(scores)),
-                       "merge_sorted_runs copy");
-        } else {
-          check_launch(tea::launch_merge_desc(ki + off, vi + off, na, ki + off + na, vi + off + na, nb, ko + off,
-                                              vo + off, stream_for(scores)), "merge_sorted_runs");
-        }
-      } else {
-        // stable two-run merge on the host (ties: the first run first)
-        int64_t i = 0, j = 0, o = off;
-        const float* A = ki + off;
-        const float* B = ki + off + na;
-        while (i < na || j < nb) {
-          const bool take_a = j >= nb || (i < na && !lt(B[j], A[i]));
-          if (take_a) {
-            ko[o] = A[i];
-            vo[o] = vi[off + i];
-            ++i;
-          } else {
-            ko[o] = B[j];
-            vo[o] = vi[off + na + j];
-            ++j;
-          }
-          ++o;
-        }
-      }
+      // (an odd run out is "merged" with an empty run: one pass-through copy)
+      merge2(ki + off, vi + off, na, 0, ki + off + na, vi + off + na, nb, 0, ko + off, vo + off);
       next.push_back(na + nb);
       off += na + nb;
     }
@@ -1051,8 +1082,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rafp", &rafp, "K3c recall at fixed precision per row (sync-free)", py::arg("sorted"), py::arg("order"),
         py::arg("target"), py::arg("class_mode"), py::arg("payload_kind"), py::arg("min_precision"),
         py::arg("out_max_recall"), py::arg("out_best_thr"));
-  m.def("merge_sorted_runs", &merge_sorted_runs, "K3m merge of descending-sorted runs -> (scores, int32 positions)",
-        py::arg("scores"), py::arg("lengths"));
+  m.def("merge_sorted_runs", &merge_sorted_runs,
+        "K3m merge of descending-sorted runs -> (keys, int32 payload: carried or positions)", py::arg("keys"),
+        py::arg("payloads") = py::none());
   m.def("row_sums", &row_sums, "K5b per-row weighted sums merged into state tensors (GPU kernel / host twin)",
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("w_scalar"), py::arg("outs"), py::arg("codes"),
         py::arg("rows") = 1);

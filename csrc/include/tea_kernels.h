@@ -129,8 +129,13 @@ int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream);
 // sizes) and the sync-free recall-at-fixed-precision chain (count + emit + search + finalize).
 int64_t curve_workspace_bytes(int64_t rows, int64_t n, bool rafp);
 // K3m: merge two descending-sorted (score, u32 payload) runs into ko / vo (merge path)
-int launch_merge_desc(const float* ka, const uint32_t* va, int64_t na, const float* kb, const uint32_t* vb, int64_t nb,
-                      float* ko, uint32_t* vo, hipStream_t stream);
+// va / vb may be null: the payload is then base_a + i (base_b + j), the sample's position.
+// splits: merge_splits_count(na + nb) int64 of scratch.
+constexpr int kMergeTile = 2048;
+int64_t merge_splits_count(int64_t n);
+int launch_merge_desc(const float* ka, const uint32_t* va, int64_t na, uint32_t base_a, const float* kb,
+                      const uint32_t* vb, int64_t nb, uint32_t base_b, float* ko, uint32_t* vo, int64_t* splits,
+                      hipStream_t stream);
 int launch_curve_count(AucScanArgs& a, void* workspace, bool rafp, hipStream_t stream);
 int launch_curve_emit(AucScanArgs a, void* workspace, bool rafp, hipStream_t stream);
 int launch_rafp(AucScanArgs a, void* workspace, hipStream_t stream);

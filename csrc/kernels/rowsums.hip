@@ -18,6 +18,7 @@
 // vectors when rows are unit-stride f32.  Each output applies its own op (= / += / min / max)
 // in its own dtype.  Deterministic: fixed partition and combine order.
 #include <algorithm>
+#include <cstdlib>
 
 #include "tea_common.h"
 #include "tea_kernels.h"
@@ -31,6 +32,7 @@ constexpr int kNStat = kRowRaw;        // raw stats (6 sums, 2 extrema)
 constexpr int kVecPerThread = 4;       // float4 loads in flight per operand per thread
 constexpr int64_t kPerBlock = kB * kVecPerThread * 4;  // 4096 elements per grid block
 constexpr int64_t kSingle = 32768;     // rows up to this long: one block per row
+constexpr int kCB = 1024;              // combine block
 
 constexpr int bit(int s) { return 1 << s; }
 constexpr int kNeedT = bit(kWT) | bit(kSSE) | bit(kWSSE) | bit(kWTT) | bit(kTMIN) | bit(kTMAX);
@@ -130,22 +132,35 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
     for (int64_t base = vlo; base < vhi; base += kChunk) {
       float4 xv[kVecPerThread], tv[kVecPerThread], wv[kVecPerThread];
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      // unconditional loads from a clamped (always valid) address: a per-lane `ok ? load : 0`
+      // makes hipcc branch around each load and wait vmcnt(0) after it - one serial memory
+      // round trip per float4 (the consumers below skip the out-of-range lanes)
 #pragma unroll
       for (int u = 0; u < kVecPerThread; ++u) {
         const int64_t i = base + 4 * (static_cast<int64_t>(u) * BS + threadIdx.x);
-        const bool ok = i < vhi;
-        xv[u] = ok ? *reinterpret_cast<const float4*>(xr + i) : z;
-        tv[u] = (HAS_T && ok) ? *reinterpret_cast<const float4*>(tr + i) : z;
-        wv[u] = (HAS_W && ok) ? *reinterpret_cast<const float4*>(wr + i) : z;
+        const int64_t ic = i < vhi ? i : vlo;
+        xv[u] = *reinterpret_cast<const float4*>(xr + ic);
+        tv[u] = HAS_T ? *reinterpret_cast<const float4*>(tr + ic) : z;
+        wv[u] = HAS_W ? *reinterpret_cast<const float4*>(wr + ic) : z;
       }
+      if (base + kChunk <= vhi) {  // whole chunk in range (block-uniform): no per-lane branch
 #pragma unroll
-      for (int u = 0; u < kVecPerThread; ++u) {
-        const int64_t i = base + 4 * (static_cast<int64_t>(u) * BS + threadIdx.x);
-        if (i < vhi) {
+        for (int u = 0; u < kVecPerThread; ++u) {
           acc_elem<NEED, HAS_W>(a, need, xv[u].x, tv[u].x, wv[u].x);
           acc_elem<NEED, HAS_W>(a, need, xv[u].y, tv[u].y, wv[u].y);
           acc_elem<NEED, HAS_W>(a, need, xv[u].z, tv[u].z, wv[u].z);
           acc_elem<NEED, HAS_W>(a, need, xv[u].w, tv[u].w, wv[u].w);
+        }
+      } else {
+#pragma unroll
+        for (int u = 0; u < kVecPerThread; ++u) {
+          const int64_t i = base + 4 * (static_cast<int64_t>(u) * BS + threadIdx.x);
+          if (i < vhi) {
+            acc_elem<NEED, HAS_W>(a, need, xv[u].x, tv[u].x, wv[u].x);
+            acc_elem<NEED, HAS_W>(a, need, xv[u].y, tv[u].y, wv[u].y);
+            acc_elem<NEED, HAS_W>(a, need, xv[u].z, tv[u].z, wv[u].z);
+            acc_elem<NEED, HAS_W>(a, need, xv[u].w, tv[u].w, wv[u].w);
+          }
         }
       }
     }
@@ -225,36 +240,41 @@ __global__ __launch_bounds__(kB) void row_sums_single_kernel(RowSumsArgs g) {
   if (threadIdx.x == 0) finish_row<HAS_W>(g, r, a);
 }
 
-// grid blocks: FP64 partials -> ws (combined by row_sums_combine_kernel in block order:
-// deterministic).  A last-block-combines variant (agent release per block + ticket) was
-// measured at 46 us for 8192 x 1000 (2000 release fences) against 14.6 + 10 us for two launches.
+// grid blocks: each folds `span` elements (whole 4096-element chunks) of its row into FP64
+// partials -> ws, stored stat-major ([row][stat][block]) so the combine reads only the NEEDed
+// stats, contiguously (combined by row_sums_combine_kernel in block order: deterministic).
+// A last-block-combines variant (agent release per block + ticket) was measured at 46 us for
+// 8192 x 1000 (2000 release fences) against 14.6 + 10 us for two launches.
 template <int NEED, bool HAS_W, bool VEC>
-__global__ __launch_bounds__(kB) void row_sums_grid_kernel(RowSumsArgs g) {
+__global__ __launch_bounds__(kB) void row_sums_grid_kernel(RowSumsArgs g, int64_t span) {
   const int64_t r = blockIdx.y;
-  const int64_t lo = static_cast<int64_t>(blockIdx.x) * kPerBlock;
-  const int64_t hi = min(g.n, lo + kPerBlock);
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * span;
+  const int64_t hi = min(g.n, lo + span);
   const Acc a = block_merge<NEED>(reduce_range<NEED, HAS_W, VEC>(g, r, lo, hi));
   if (threadIdx.x == 0) {
-    double* p = g.ws + (r * g.blocks + blockIdx.x) * kNStat;
+    double* p = g.ws + r * kNStat * g.blocks + blockIdx.x;
 #pragma unroll
-    for (int k = 0; k < kNStat; ++k) p[k] = a.v[k];
+    for (int k = 0; k < kNStat; ++k)
+      if (NEED & bit(k)) p[k * g.blocks] = a.v[k];
   }
 }
 
 // one block per row: every thread folds a strided subset of the partials, then a block merge
 template <int NEED, bool HAS_W>
-__global__ __launch_bounds__(kB) void row_sums_combine_kernel(RowSumsArgs g) {
+__global__ __launch_bounds__(kCB) void row_sums_combine_kernel(RowSumsArgs g) {
   const int64_t r = blockIdx.x;
   Acc m;
   acc_init(m);
-  for (int b = threadIdx.x; b < g.blocks; b += kB) {
+  const double* src = g.ws + r * kNStat * g.blocks;
+  for (int b = threadIdx.x; b < g.blocks; b += kCB) {
     Acc q;
-    const double* src = g.ws + (r * g.blocks + b) * kNStat;
+    acc_init(q);
 #pragma unroll
-    for (int k = 0; k < kNStat; ++k) q.v[k] = src[k];
+    for (int k = 0; k < kNStat; ++k)
+      if (NEED & bit(k)) q.v[k] = src[k * g.blocks + b];
     acc_merge<NEED>(m, q);
   }
-  m = block_merge<NEED>(m);
+  m = block_merge<NEED, kCB>(m);
   if (threadIdx.x == 0) finish_row<HAS_W>(g, r, m);
 }
 
@@ -323,10 +343,12 @@ int launch_need(const RowSumsArgs& a, bool vec, hipStream_t stream) {
     if (vec) hipLaunchKernelGGL((row_sums_fold_kernel<NEED, HAS_W, true>), grid, dim3(kFB), 0, stream, a, span_c);
     else hipLaunchKernelGGL((row_sums_fold_kernel<NEED, HAS_W, false>), grid, dim3(kFB), 0, stream, a, span_c);
   } else {
+    const int64_t chunks = (a.n + kPerBlock - 1) / kPerBlock;
+    const int64_t span = (chunks + a.blocks - 1) / a.blocks * kPerBlock;
     const dim3 grid(static_cast<unsigned>(a.blocks), static_cast<unsigned>(a.rows));
-    if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true>), grid, dim3(kB), 0, stream, a);
-    else hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, false>), grid, dim3(kB), 0, stream, a);
-    hipLaunchKernelGGL((row_sums_combine_kernel<NEED, HAS_W>), dim3(a.rows), dim3(kB), 0, stream, a);
+    if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true>), grid, dim3(kB), 0, stream, a, span);
+    else hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, false>), grid, dim3(kB), 0, stream, a, span);
+    hipLaunchKernelGGL((row_sums_combine_kernel<NEED, HAS_W>), dim3(a.rows), dim3(kCB), 0, stream, a);
   }
   return static_cast<int>(hipGetLastError());
 }
@@ -339,9 +361,15 @@ int launch_w(const RowSumsArgs& a, bool vec, hipStream_t stream) {
 }  // namespace
 
 int row_sums_blocks(int64_t rows, int64_t n) {
-  (void)rows;
   if (n <= kSingle) return 1;
-  return static_cast<int>((n + kPerBlock - 1) / kPerBlock);
+  // about 512 blocks over all rows (each folds whole 4096-element chunks): enough bytes in
+  // flight per CU without thousands of one-chunk blocks and partials (csrc/bench/
+  // k5b_variants.hip, Sum 8192 x 1000: 2000 blocks 9.1 us, 1024 8.4, 512 7.95, 256 9.1)
+  int64_t cap = 512;
+  if (const char* e = std::getenv("TORCHEVAL_AMD_K5B_GRID")) cap = std::max(1, std::atoi(e));
+  const int64_t chunks = (n + kPerBlock - 1) / kPerBlock;
+  const int64_t per_row = std::max<int64_t>(2, cap / std::max<int64_t>(rows, 1));
+  return static_cast<int>(std::min(chunks, per_row));
 }
 
 int row_sums_fold_blocks(int64_t rows, int64_t n) {

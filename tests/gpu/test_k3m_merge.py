@@ -28,12 +28,17 @@ def _runs(sizes, levels, seed, nan=False):
 def test_merge_matches_stable_sort(sizes, levels):
     runs = _runs(sizes, levels, sum(sizes), nan=True)
     x = torch.cat(runs)
-    s, o = native().merge_sorted_runs(x.to(DEV), list(sizes))
-    s_cpu, o_cpu = native().merge_sorted_runs(x, list(sizes))
+    s, o = native().merge_sorted_runs([r.to(DEV) for r in runs])
+    s_cpu, o_cpu = native().merge_sorted_runs(runs)
     torch.testing.assert_close(s.cpu(), s_cpu, equal_nan=True, rtol=0, atol=0)
     assert torch.equal(o.cpu(), o_cpu)  # same stable order as the host merge
-    want = torch.sort(x, descending=True, stable=True).values
+    want, perm = torch.sort(x, descending=True, stable=True)
     torch.testing.assert_close(s.cpu(), want, equal_nan=True, rtol=0, atol=0)
+    assert torch.equal(o.cpu().long(), perm)  # positions = the stable permutation
+    # a carried payload comes out in the same order
+    pays = [torch.arange(r.numel(), dtype=torch.int32) * 3 + i for i, r in enumerate(runs)]
+    _, p = native().merge_sorted_runs([r.to(DEV) for r in runs], [q.to(DEV) for q in pays])
+    assert torch.equal(p.cpu(), torch.cat(pays)[perm])
 
 
 @pytest.mark.parametrize("R,n", [(2, 100_000), (8, 125_000), (3, 7)])

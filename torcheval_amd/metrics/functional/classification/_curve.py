@@ -182,10 +182,19 @@ def recall_at_precision_rows(
 def sort_run(x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor]):
     """One 1-D sample set sorted descending (NaN first, as K3a / torch.sort): (scores, targets,
     weights) permuted together - the form a rank ships to a distributed sync, so the receiver
-    merges sorted runs instead of sorting the union."""
+    merges sorted runs instead of sorting the union.  Unweighted ROCm runs with bool / integer /
+    f32 targets carry the target through the K3a sort as its f32 value (no permutation gather;
+    the shipped targets are then f32 - exact for every 0/1 label), which is also the payload
+    the receiver's merge carries."""
     if use_native(x) and x.dtype == torch.float32 and x.numel() > 0:
-        from torcheval_amd.ops.sortscan import _sort_rows
+        from torcheval_amd.ops.sortscan import PAYLOAD_TARGET, _sort_rows
 
+        if w is None and x.is_cuda and t.dtype in (torch.bool, torch.uint8, torch.int32, torch.int64, torch.float32):
+            tp = t.to(torch.uint8) if t.dtype == torch.bool else t
+            s, idx, kind = _sort_rows(x.reshape(1, -1), tp.reshape(1, -1), PAYLOAD_TARGET)
+            if kind == PAYLOAD_TARGET:
+                return s[0], idx[0].view(torch.float32), None
+            return s[0], t[idx[0].long()], None
         s, idx, _ = _sort_rows(x.reshape(1, -1))
         perm = idx[0].long()
         s = s[0]
@@ -196,18 +205,29 @@ def sort_run(x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor]):
 
 def merged_areas(runs_x, runs_t, runs_w, *, roc: bool, pr: bool):
     """float64 (AUROC, AUPRC) of the union of 1-D runs that are each sorted descending: the
-    runs are merged (K3m merge path on ROCm, a host merge on CPU; log2(R) passes) and the
-    merged order feeds the K3 scan directly - no sort of the union."""
+    runs are merged (K3m merge path on ROCm, a host merge on CPU; log2(R) passes, the first
+    reading the runs in place) and the merged order feeds the K3 scan directly - no sort of
+    the union.  Unweighted ROCm runs carry their targets (as f32) through the merge, so K3
+    reads them in order without a gather (the K3a ``PAYLOAD_TARGET`` convention)."""
     from torcheval_amd.ops import native
+    from torcheval_amd.ops.sortscan import PAYLOAD_TARGET
 
-    x = torch.cat([r.reshape(-1) for r in runs_x])
+    xs = [r.reshape(-1).contiguous() for r in runs_x]
+    if xs[0].is_cuda and use_native(xs[0]) and runs_w is None:
+        pays = [r.reshape(-1).to(torch.float32).contiguous() for r in runs_t]
+        s, p = native().merge_sorted_runs(xs, pays)
+        out_roc = torch.empty(1, dtype=torch.float64, device=s.device) if roc else None
+        out_pr = torch.empty(1, dtype=torch.float64, device=s.device) if pr else None
+        native().auc_scan(s[None], p[None], p.view(torch.float32)[None], None, False, out_roc, out_pr, None, None,
+                          PAYLOAD_TARGET)
+        return out_roc, out_pr
     t = torch.cat([r.reshape(-1) for r in runs_t])
     w = None if runs_w is None else torch.cat([r.reshape(-1) for r in runs_w])
-    s, order = native().merge_sorted_runs(x.contiguous(), [r.numel() for r in runs_x])
-    if use_native(x) and t.is_cuda:
+    s, order = native().merge_sorted_runs(xs)
+    if use_native(s) and t.is_cuda:
         tt = t if t.dtype != torch.bool else t.to(torch.uint8)
-        out_roc = torch.empty(1, dtype=torch.float64, device=x.device) if roc else None
-        out_pr = torch.empty(1, dtype=torch.float64, device=x.device) if pr else None
+        out_roc = torch.empty(1, dtype=torch.float64, device=s.device) if roc else None
+        out_pr = torch.empty(1, dtype=torch.float64, device=s.device) if pr else None
         native().auc_scan(s[None], order[None], tt[None], None if w is None else w[None], False,
                           out_roc, out_pr, None, None, 0)
         return out_roc, out_pr
