@@ -119,7 +119,7 @@ def test_k7_invalid_target_raises():
 
 
 # ----------------------------------------------------------------------------- K8
-@pytest.mark.parametrize("n,d", [(1, 8), (37, 100), (64, 128), (200, 300), (256, 2048), (1000, 2048)])
+@pytest.mark.parametrize("n,d", [(1, 8), (37, 100), (64, 128), (200, 300), (256, 2048), (1000, 2048), (50, 37), (300, 1001)])
 def test_k8_cov_matches_fp64(n, d):
     g = torch.Generator().manual_seed(n * 7 + d)
     act = torch.randn(n, d, generator=g)

@@ -36,10 +36,15 @@ def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
         from torcheval_amd.ops import native
 
         a = act
-        if not (a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0):
+        # K8 stages 16-B row pieces: rows 16-B aligned (a width that is not a multiple of 4 is
+        # zero-padded by the op itself when the tensor is contiguous)
+        def _ok(t: Tensor) -> bool:
+            return t.stride(1) == 1 and t.data_ptr() % 16 == 0 and (t.stride(0) % 4 == 0 or t.is_contiguous())
+
+        if not _ok(a):
             # a fresh allocation: contiguous() would return a contiguous but misaligned view as is
             a = act.clone(memory_format=torch.contiguous_format)
-        if a.stride(1) == 1 and a.stride(0) % 4 == 0 and a.data_ptr() % 16 == 0:  # K8 streams 16-B row segments
+        if _ok(a):
             native().fid_cov_update(a, cov_sum, col_sum)
             return
     col_sum += torch.sum(act, dim=0)
