@@ -551,6 +551,50 @@ std::vector<Tensor> merge_sorted_runs(const std::vector<Tensor>& keys, const opt
   return {k0, v0};
 }
 
+// ---------------------------------------------------------------- K10b retrieval top-k
+// Merges a batch into RetrievalPrecision's [Q, k] top-k state rows in place (see
+// retrieval.hip).  x, t: float32 [n]; q: int64 [n] query ids or None (all query 0).
+void retrieval_topk_update(const Tensor& x, const Tensor& t, const optional<Tensor>& q, const Tensor& topk,
+                           const Tensor& target, const Tensor& count) {
+  check_gpu(x, "scores");
+  const int64_t n = x.numel();
+  TORCH_CHECK(x.dim() == 1 && x.scalar_type() == at::kFloat && x.is_contiguous(), "retrieval_topk: x must be f32 [n]");
+  TORCH_CHECK(t.dim() == 1 && t.numel() == n && t.scalar_type() == at::kFloat && t.is_contiguous() &&
+                  t.device() == x.device(), "retrieval_topk: t must be f32 [n]");
+  TORCH_CHECK(topk.dim() == 2 && topk.scalar_type() == at::kFloat && topk.is_contiguous() &&
+                  target.sizes() == topk.sizes() && target.scalar_type() == at::kFloat && target.is_contiguous() &&
+                  topk.device() == x.device() && target.device() == x.device(),
+              "retrieval_topk: state rows must be contiguous f32 [Q, k]");
+  const int64_t Q = topk.size(0), k = topk.size(1);
+  TORCH_CHECK(count.dim() == 1 && count.numel() == Q && count.scalar_type() == at::kLong && count.is_contiguous() &&
+                  count.device() == x.device(), "retrieval_topk: count must be int64 [Q]");
+  TORCH_CHECK(k >= 1 && k <= 64 && 2 * Q * 4 <= tea::kRetrievalMaxLds && n < (int64_t{1} << 31),
+              "retrieval_topk: needs 1 <= k <= 64, Q <= 8192, n < 2^31");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  tea::RetrievalArgs a;
+  a.x = x.data_ptr<float>();
+  a.t = t.data_ptr<float>();
+  if (q.has_value()) {
+    TORCH_CHECK(q->dim() == 1 && q->numel() == n && q->scalar_type() == at::kLong && q->is_contiguous() &&
+                    q->device() == x.device(), "retrieval_topk: q must be int64 [n]");
+    a.q = q->data_ptr<int64_t>();
+  }
+  a.n = n;
+  a.Q = Q;
+  a.k = static_cast<int>(k);
+  a.topk = topk.data_ptr<float>();
+  a.target_state = target.data_ptr<float>();
+  a.count = count.data_ptr<int64_t>();
+  hipStream_t st = stream_for(x);
+  a.counts = static_cast<int*>(zeroed_workspace(x, st, Q * 4, 7));
+  auto* ws = static_cast<char*>(scratch_workspace(x, st, (2 * Q + 2) * 4 + 2 * n * 4, 1));
+  a.offsets = reinterpret_cast<int*>(ws);
+  a.cursor = a.offsets + Q + 1;
+  a.rec_key = reinterpret_cast<uint32_t*>(a.cursor + Q + 1);
+  a.rec_idx = a.rec_key + n;
+  check_launch(tea::launch_retrieval_topk(a, st), "retrieval_topk_update");
+}
+
 // ---------------------------------------------------------------- K5b per-row weighted sums
 // x: [rows, n] view (t, w: the same shape, any strides; w may be absent -> w_scalar).
 // outs[k] receives stat codes[k] / 8 with op codes[k] % 4 (see tea::RowStat / tea::RowOp), bit 2
@@ -1085,6 +1129,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("merge_sorted_runs", &merge_sorted_runs,
         "K3m merge of descending-sorted runs -> (keys, int32 payload: carried or positions)", py::arg("keys"),
         py::arg("payloads") = py::none());
+  m.def("retrieval_topk_update", &retrieval_topk_update,
+        "K10b segmented streaming top-k merge into RetrievalPrecision state rows", py::arg("x"), py::arg("t"),
+        py::arg("q"), py::arg("topk"), py::arg("target"), py::arg("count"));
   m.def("row_sums", &row_sums, "K5b per-row weighted sums merged into state tensors (GPU kernel / host twin)",
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("w_scalar"), py::arg("outs"), py::arg("codes"),
         py::arg("rows") = 1);

@@ -400,4 +400,23 @@ int64_t radix_sort_tiles(int64_t rows, int64_t n);
 int64_t radix_sort_groups(int64_t tiles);
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream);
 int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream);
+// ------------------------------------------------------------------ K10b retrieval top-k
+struct RetrievalArgs {
+  const float* x = nullptr;        // [n] scores
+  const float* t = nullptr;        // [n] targets
+  const int64_t* q = nullptr;      // [n] query ids (null: every sample is query 0)
+  int64_t n = 0, Q = 0;
+  int k = 0;                        // 1..64
+  float* topk = nullptr;            // [Q, k] state (best first, -inf padded)
+  float* target_state = nullptr;    // [Q, k]
+  int64_t* count = nullptr;         // [Q] valid entries (<= k)
+  int* counts = nullptr;            // [Q] zeroed scratch (left zeroed)
+  int* offsets = nullptr;           // [Q + 1] scratch
+  int* cursor = nullptr;            // [Q] scratch
+  uint32_t* rec_key = nullptr;      // [n] scratch
+  uint32_t* rec_idx = nullptr;      // [n] scratch
+};
+constexpr int kRetrievalMaxLds = 64 * 1024;  // 2 x Q int32 of LDS: Q <= 8192
+int launch_retrieval_topk(const RetrievalArgs& a, hipStream_t stream);
+
 }  // namespace tea

@@ -7,11 +7,13 @@ gather per query); compute loops again with a ``1 in target`` host check per que
 Here the state is dense and device-resident, and neither update nor compute synchronises:
 
 * ``k`` given: ``topk`` / ``target`` are ``[num_queries, k]`` (score-descending, padded with
-  -inf / 0) plus ``count`` (valid entries per query, <= k).  One update = one composite-key
-  sort of the batch by (query, score desc) - a single int64 radix sort - segment starts from
-  an index_add histogram, a gather of every query's best k batch items, and one row-wise
-  ``topk`` of [num_queries, 2k] candidates (old top-k + batch top-k).  O(N log N + Q k) work in
-  ~12 launches whatever the number of queries.
+  -inf / 0) plus ``count`` (valid entries per query, <= k).  On ROCm (f32 state, k <= 64,
+  num_queries <= 8192) one update is the K10b kernel chain (csrc/kernels/retrieval.hip):
+  per-query histogram, scan, a scatter of the batch into per-query segments, and one wave
+  per query selecting the top-k of old row + segment - 4 launches, no sort.  Otherwise: one
+  composite-key sort of the batch by (query, score desc) - a single int64 radix sort -
+  segment starts from an index_add histogram, a gather of every query's best k batch items,
+  and one row-wise ``topk`` of [num_queries, 2k] candidates (old top-k + batch top-k).
 * ``k=None`` (every item is retrieved): the top-"all" is the whole history, so the state is the
   per-query sums it reduces to - ``relevant`` (sum of targets), ``positives`` (count of
   target == 1) and ``items`` - merged with ``merge="sum"`` (one RCCL all-reduce when synced).
@@ -91,6 +93,8 @@ class RetrievalPrecision(Metric[torch.Tensor]):
         if Q > 1 and indexes is None:
             raise ValueError("`indexes` must be passed during update() when num_queries > 1.")
         dev = self._state_device()
+        if self.k is not None and self._native_topk(input, target, indexes):
+            return self
         input, target = input.to(dev), target.to(dev)
         if Q == 1:
             q = torch.zeros(input.shape[0], dtype=torch.int64, device=dev)
@@ -116,6 +120,25 @@ class RetrievalPrecision(Metric[torch.Tensor]):
         self.relevant += stats[0, :Q]
         self.positives += stats[1, :Q]
         self.items += stats[2, :Q]
+
+    def _native_topk(self, input: torch.Tensor, target: torch.Tensor, indexes: Optional[torch.Tensor]) -> bool:
+        """K10b path: f32 state on ROCm, 1 <= k <= 64, num_queries <= 8192."""
+        from torcheval_amd.ops import native, use_native
+
+        if not (use_native(input) and self.topk.is_cuda and self.topk.dtype == torch.float32
+                and self.target.dtype == torch.float32 and 1 <= self.k <= 64 and self.num_queries <= 8192
+                and input.dtype in (torch.float32, torch.float16, torch.bfloat16)
+                and input.shape[0] < 2**31
+                and target.dtype in (torch.float32, torch.float16, torch.bfloat16, torch.int64, torch.int32, torch.uint8, torch.bool)):
+            return False
+        x = input.to(self.topk.device, torch.float32).contiguous()
+        t = target.to(self.topk.device, torch.float32).contiguous()
+        q = None
+        if self.num_queries > 1:
+            q = indexes.to(self.topk.device, torch.int64).contiguous()
+        self.topk, self.target, self.count = self.topk.contiguous(), self.target.contiguous(), self.count.contiguous()
+        native().retrieval_topk_update(x, t, q, self.topk, self.target, self.count)
+        return True
 
     def _update_topk(self, input: torch.Tensor, target: torch.Tensor, q: torch.Tensor) -> None:
         Q, k, n = self.num_queries, self.k, input.shape[0]
