@@ -67,3 +67,35 @@ def test_error_flags_raise_on_every_rank(ws):
     assert all(r[0] for r in res), res
     assert res[-1][1] == 9  # the flagged rank's own metric still holds its flag
     assert all(not r[1] for r in res[:-1])  # None, or a clean (zero) flag
+
+
+def _fast_vs_general_job(rank, ws):
+    from torcheval_amd.metrics import Max, Mean, MulticlassAccuracy, MulticlassPrecision
+    from torcheval_amd.parallel import state_sync
+
+    g = torch.Generator().manual_seed(10 + rank)
+    coll = {
+        "acc": MulticlassAccuracy(num_classes=5, average="macro").update(torch.randn(40, 5, generator=g),
+                                                                       torch.randint(0, 5, (40,), generator=g)),
+        "prec": MulticlassPrecision(num_classes=5, average=None).update(torch.randn(40, 5, generator=g),
+                                                                      torch.randint(0, 5, (40,), generator=g)),
+        "mean": Mean().update(torch.randn(17, generator=g)),
+        "max": Max().update(torch.randn(9, generator=g)),
+    }
+    fast = state_sync._fast_small_sync(coll, None, ws)
+    assert fast is not None
+    again = state_sync._fast_small_sync(coll, None, ws)  # cached plan
+    general = state_sync.start_sync_collection(coll, None, ws, snapshot=False, blocking=True).finish()
+    out = []
+    for key in coll:
+        for name in coll[key]._state_merge_kinds():
+            a, b, c = getattr(fast[key], name), getattr(again[key], name), getattr(general[key], name)
+            assert torch.equal(a, b) and torch.equal(a, c), (key, name)
+        out.append(float(fast[key].compute().float().sum()))
+    return out
+
+
+@pytest.mark.parametrize("ws", [2, 3])
+def test_fast_small_sync_matches_general_path(ws):
+    res = run_distributed(_fast_vs_general_job, ws)
+    assert all(r == res[0] for r in res), res  # bit-identical on every rank
