@@ -42,7 +42,7 @@ def main() -> int:
         t0 = time.perf_counter()
         p = subprocess.run(["bash", "-o", "pipefail", "-c", cmd], capture_output=True, text=True)
         dt = time.perf_counter() - t0
-        tail = (p.stdout + p.stderr).strip().splitlines()[-3:]
+        tail = (p.stdout.strip() or p.stderr.strip()).splitlines()[-3:]
         record["steps"].append({"name": name, "cmd": cmd, "rc": p.returncode, "seconds": round(dt, 1), "tail": tail})
         print(f"[{p.returncode}] {name} ({dt:.1f}s): {tail[-1] if tail else ''}", flush=True)
         if p.returncode != 0:

@@ -215,7 +215,10 @@ def merged_areas(runs_x, runs_t, runs_w, *, roc: bool, pr: bool):
     xs = [r.reshape(-1).contiguous() for r in runs_x]
     if xs[0].is_cuda and use_native(xs[0]) and runs_w is None:
         pays = [r.reshape(-1).to(torch.float32).contiguous() for r in runs_t]
-        s, p = native().merge_sorted_runs(xs, pays)
+        if len(xs) == 1:  # one run is already merged
+            s, p = xs[0], pays[0].view(torch.int32)
+        else:
+            s, p = native().merge_sorted_runs(xs, pays)
         out_roc = torch.empty(1, dtype=torch.float64, device=s.device) if roc else None
         out_pr = torch.empty(1, dtype=torch.float64, device=s.device) if pr else None
         native().auc_scan(s[None], p[None], p.view(torch.float32)[None], None, False, out_roc, out_pr, None, None,
