@@ -54,15 +54,26 @@ __global__ __launch_bounds__(kT) void curve_count_kernel(AucScanArgs a) {
   float2* ab = reinterpret_cast<float2*>(a.ab) + static_cast<int64_t>(r) * a.n;
   double sa = 0.0, sb = 0.0;
   int tails = 0;
+  // clamped unconditional loads, masked after (a per-lane `if (i < n)` around loads compiles
+  // to a branch + vmcnt(0) per element)
+  float2 vv[kPer];
+  K kc[kPer], kn[kPer];
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int64_t i = base + k * kT + threadIdx.x;  // coalesced
+    const int64_t ic = i < a.n ? i : a.n - 1;
+    vv[k] = sample_ab(a, r, ic);
+    kc[k] = key_at<K>(a, r, ic);
+    kn[k] = key_at<K>(a, r, ic + 1 < a.n ? ic + 1 : ic);
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t i = base + k * kT + threadIdx.x;
     if (i < a.n) {
-      const float2 v = sample_ab(a, r, i);
-      if constexpr (!DIRECT) ab[i] = v;
-      sa += v.x;
-      sb += v.y;
-      tails += (i == a.n - 1 || !same_key<K>(key_at<K>(a, r, i + 1), key_at<K>(a, r, i))) ? 1 : 0;
+      if constexpr (!DIRECT) ab[i] = vv[k];
+      sa += vv[k].x;
+      sb += vv[k].y;
+      tails += (i == a.n - 1 || !same_key<K>(kn[k], kc[k])) ? 1 : 0;
     }
   }
   __shared__ double lds[2][kT / 64];
@@ -141,18 +152,21 @@ __global__ __launch_bounds__(kT) void curve_emit_kernel(AucScanArgs a) {
   const int64_t i0 = base + j0;
   K key[kPer];
   float2 v[kPer];
+  // clamped unconditional loads, masked after
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int64_t i = i0 + k;
-    if (i < a.n) {
-      key[k] = key_at<K>(a, r, i);
-      v[k] = load_ab<DIRECT>(a, ab, r, i);
-    } else {
-      key[k] = K(0);
-      v[k] = make_float2(0.f, 0.f);
-    }
+    const int64_t i = i0 + k < a.n ? i0 + k : a.n - 1;
+    key[k] = key_at<K>(a, r, i);
+    v[k] = load_ab<DIRECT>(a, ab, r, i);
   }
-  const K next_key = (i0 + kPer < a.n) ? key_at<K>(a, r, i0 + kPer) : K(0);
+  K next_key = key_at<K>(a, r, i0 + kPer < a.n ? i0 + kPer : a.n - 1);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const bool ok = i0 + k < a.n;
+    key[k] = ok ? key[k] : K(0);
+    v[k] = ok ? v[k] : make_float2(0.f, 0.f);
+  }
+  next_key = (i0 + kPer < a.n) ? next_key : K(0);
   const D2 t0 = reinterpret_cast<const D2*>(a.tstart)[tile];
   const int g0 = a.cstart[tile];
   const D2 tot_row = reinterpret_cast<const D2*>(a.totals)[r];

@@ -93,15 +93,21 @@ __device__ __forceinline__ void load_tile(const RadixArgs& a, const uint32_t* ke
                                           uint32_t (&v)[kRounds], bool want_vals) {
   constexpr int kRTile = kRT * kRounds;
   const int64_t t0 = static_cast<int64_t>(tile) * kRTile + threadIdx.x;
+  // every load from a clamped (valid) index, the tail masked afterwards: a per-lane
+  // `if (i < n) load` compiled to a branch and a vmcnt(0) per round - kRounds serial round
+  // trips instead of one
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
     const int64_t i = t0 + j * kRT;
-    k[j] = 0u;
-    v[j] = 0u;
-    if (i < a.n) {
-      k[j] = load_key(a, keys_in, pass, row, i);
-      if (want_vals) v[j] = vals_in[row * a.n + i];
-    }
+    const int64_t ic = i < a.n ? i : a.n - 1;
+    k[j] = load_key(a, keys_in, pass, row, ic);
+    v[j] = want_vals ? vals_in[row * a.n + ic] : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const bool ok = t0 + j * kRT < a.n;
+    k[j] = ok ? k[j] : 0u;
+    v[j] = ok ? v[j] : 0u;
   }
 }
 
@@ -171,17 +177,21 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
   const int64_t tbase = static_cast<int64_t>(tile) * kRTile;
   const int64_t wbase = tbase + static_cast<int64_t>(w) * kSub;
   uint32_t k[kRounds], v[kRounds], r[kRounds];
+  // clamped unconditional loads, tail masked afterwards (see load_tile)
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
     const int64_t i = wbase + j * 64 + lane;
-    k[j] = 0u;
-    v[j] = 0u;
-    if (i < a.n) {
-      k[j] = load_key(a, keys_in, pass, row, i);
-      if constexpr (VMODE == 0) v[j] = vals_in[row * a.n + i];
-      else if constexpr (VMODE == 1) v[j] = static_cast<uint32_t>(i);
-      else v[j] = first_payload<PT, KIND>(a, row, i);
-    }
+    const int64_t ic = i < a.n ? i : a.n - 1;
+    k[j] = load_key(a, keys_in, pass, row, ic);
+    if constexpr (VMODE == 0) v[j] = vals_in[row * a.n + ic];
+    else if constexpr (VMODE == 1) v[j] = static_cast<uint32_t>(i);
+    else v[j] = first_payload<PT, KIND>(a, row, ic);
+  }
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const bool ok = wbase + j * 64 + lane < a.n;
+    k[j] = ok ? k[j] : 0u;
+    v[j] = ok ? v[j] : 0u;
   }
 #pragma unroll
   for (int q = 0; q < kBins / 64; ++q) wc[w][lane + 64 * q] = 0;
@@ -195,7 +205,9 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     for (int g0 = 0; g0 < a.ngroups; g0 += 16) {
       uint32_t v[16];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) v[q] = g0 + q < a.ngroups ? G[static_cast<int64_t>(g0 + q) * kBins] : 0u;
+      for (int q = 0; q < 16; ++q) v[q] = G[static_cast<int64_t>(min(g0 + q, a.ngroups - 1)) * kBins];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) v[q] = g0 + q < a.ngroups ? v[q] : 0u;
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         tot += v[q];
@@ -205,8 +217,11 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     const uint32_t* H = a.hist + (row * a.tiles + static_cast<int64_t>(mg) * kGroup) * kBins + threadIdx.x;
     const int in_group = tile - mg * kGroup;  // tiles of this group before this one
     uint32_t hv[kGroup];
+    const int qmax = min(kGroup, a.tiles - mg * kGroup) - 1;  // last tile of this group
 #pragma unroll
-    for (int q = 0; q < kGroup; ++q) hv[q] = q < in_group ? H[static_cast<int64_t>(q) * kBins] : 0u;
+    for (int q = 0; q < kGroup; ++q) hv[q] = H[static_cast<int64_t>(min(q, qmax)) * kBins];
+#pragma unroll
+    for (int q = 0; q < kGroup; ++q) hv[q] = q < in_group ? hv[q] : 0u;
 #pragma unroll
     for (int q = 0; q < kGroup; ++q) pre += hv[q];
     uint32_t inc = tot;

@@ -37,15 +37,23 @@ __global__ __launch_bounds__(kT) void tile_sums_kernel(AucScanArgs a) {
   const int64_t base = static_cast<int64_t>(blockIdx.x) * kTile;
   double sa = 0.0, sb = 0.0;
   float2* ab = reinterpret_cast<float2*>(a.ab) + static_cast<int64_t>(r) * a.n;
-#pragma unroll 4
+  // clamped unconditional loads, the tail masked after (a per-lane `if (i < n)` around the
+  // loads compiled to a branch + vmcnt(0) per element)
+  float2 vv[kPer];
+#pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int64_t i = base + k * kT + threadIdx.x;  // coalesced gather order
-    if (i < a.n) {
-      const float2 v = sample_ab(a, r, i);
-      if constexpr (!DIRECT) ab[i] = v;
-      sa += v.x;
-      sb += v.y;
+    vv[k] = sample_ab(a, r, i < a.n ? i : a.n - 1);
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int64_t i = base + k * kT + threadIdx.x;
+    const bool ok = i < a.n;
+    if constexpr (!DIRECT) {
+      if (ok) ab[i] = vv[k];
     }
+    sa += ok ? vv[k].x : 0.f;
+    sb += ok ? vv[k].y : 0.f;
   }
   __shared__ double lds[2][kT / 64];
   sa = wave_sum(sa);
@@ -194,20 +202,26 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   const int64_t i0 = base + j0;
   K key[kPer];
   float2 v[kPer];
+  // clamped unconditional loads (the tile has >= 1 sample, so base + tile_n - 1 is valid),
+  // masked after: one round trip instead of one per element
+  const int64_t ilast = base + tile_n - 1;
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
-    const int64_t i = i0 + k;
-    if (j0 + k < tile_n) {
-      key[k] = key_at<K>(a, r, i);
-      v[k] = load_ab<DIRECT>(a, ab, r, i);
-    } else {
-      key[k] = K(0);
-      v[k] = make_float2(0.f, 0.f);
-    }
+    const int64_t i = i0 + k < ilast ? i0 + k : ilast;
+    key[k] = key_at<K>(a, r, i);
+    v[k] = load_ab<DIRECT>(a, ab, r, i);
   }
   const bool live = j0 < tile_n;
-  const K pk0 = (live && i0 > 0) ? key_at<K>(a, r, i0 - 1) : K(0);
-  const K nk_last = (live && i0 + kPer < a.n) ? key_at<K>(a, r, i0 + kPer) : K(0);
+  K pk0 = key_at<K>(a, r, i0 > 0 ? (i0 - 1 < ilast ? i0 - 1 : ilast) : 0);
+  K nk_last = key_at<K>(a, r, i0 + kPer < a.n ? i0 + kPer : a.n - 1);
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const bool ok = j0 + k < tile_n;
+    key[k] = ok ? key[k] : K(0);
+    v[k] = ok ? v[k] : make_float2(0.f, 0.f);
+  }
+  pk0 = (live && i0 > 0) ? pk0 : K(0);
+  nk_last = (live && i0 + kPer < a.n) ? nk_last : K(0);
   double pa = 0.0, pb = 0.0;
   if constexpr (FUSED) {
     const D2* ts = reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
