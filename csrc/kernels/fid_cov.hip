@@ -218,18 +218,25 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
 
   // ---- the C tile (and its mirror) this block read-modify-writes at the end: loaded into
   // registers now, so the epilogue's reads are not a serial HBM round trip after the loop
-  constexpr int kPer = kT * kT / kThreads;  // 18 elements per thread
-  static_assert(kT * kT % kThreads == 0, "tile must split evenly over the block");
-  float cpre[kPer], mpre[kPer];
-  if (a.split == 1) {
+  // C is read as float4 rows when d % 4 == 0 (every 4-column group then lies wholly inside or
+  // outside [0, d)): 96 x 24 float4 per tile, <= 5 per thread, clamped addresses + selects so
+  // the loads issue back to back (a guarded load per element compiled to a branch + wait each)
+  constexpr int kSeg4 = kT / 4;                                     // 24
+  constexpr int kPer4 = (kT * kSeg4 + kThreads - 1) / kThreads;     // 5
+  const bool vec4 = a.d % 4 == 0;
+  float4 cpre[kPer4], mpre[kPer4];
+  if (a.split == 1 && vec4) {
 #pragma unroll
-    for (int q = 0; q < kPer; ++q) {
+    for (int q = 0; q < kPer4; ++q) {
       const int e = threadIdx.x + kThreads * q;
-      const int row = e / kT, col = e % kT;
-      const bool in = I0 + row < a.d && J0 + col < a.d;
-      cpre[q] = in ? a.cov[(I0 + row) * a.d + J0 + col] : 0.f;
-      const bool min_ = !diag && J0 + row < a.d && I0 + col < a.d;
-      mpre[q] = min_ ? a.cov[(J0 + row) * a.d + I0 + col] : 0.f;
+      const int row = (e < kT * kSeg4 ? e : 0) / kSeg4, c4 = ((e < kT * kSeg4 ? e : 0) % kSeg4) * 4;
+      const bool in = e < kT * kSeg4 && I0 + row < a.d && J0 + c4 < a.d;
+      const bool min_ = e < kT * kSeg4 && !diag && J0 + row < a.d && I0 + c4 < a.d;
+      const float4 x = *reinterpret_cast<const float4*>(a.cov + (in ? (I0 + row) * a.d + J0 + c4 : 0));
+      const float4 y = *reinterpret_cast<const float4*>(a.cov + (min_ ? (J0 + row) * a.d + I0 + c4 : 0));
+      // per-component selects (a whole-float4 select is lowered through a stack slot)
+      cpre[q] = make_float4(in ? x.x : 0.f, in ? x.y : 0.f, in ? x.z : 0.f, in ? x.w : 0.f);
+      mpre[q] = make_float4(min_ ? y.x : 0.f, min_ ? y.y : 0.f, min_ ? y.z : 0.f, min_ ? y.w : 0.f);
     }
   }
 
@@ -312,17 +319,35 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
     return;
   }
 
-  // ---- epilogue: coalesced C[I, J] += tile and mirrored C[J, I] += tile^T (C read up front)
+  // ---- epilogue: C[I, J] += tile and mirrored C[J, I] += tile^T as float4 rows (C read up
+  // front); a scalar pass when d % 4 != 0
+  if (vec4) {
 #pragma unroll
-  for (int q = 0; q < kPer; ++q) {
-    const int e = threadIdx.x + kThreads * q;
-    const int row = e / kT, col = e % kT;
-    const int64_t gi = I0 + row, gj = J0 + col;
-    if (gi < a.d && gj < a.d) a.cov[gi * a.d + gj] = cpre[q] + sC[row * kCPad + col];
-    if (!diag) {
-      // mirrored tile: C[J0 + row][I0 + col] = tile[col][row]
-      const int64_t mi = J0 + row, mj = I0 + col;
-      if (mi < a.d && mj < a.d) a.cov[mi * a.d + mj] = mpre[q] + sC[col * kCPad + row];
+    for (int q = 0; q < kPer4; ++q) {
+      const int e = threadIdx.x + kThreads * q;
+      if (e >= kT * kSeg4) continue;
+      const int row = e / kSeg4, c4 = (e % kSeg4) * 4;
+      if (I0 + row < a.d && J0 + c4 < a.d) {
+        const float* t = sC + row * kCPad + c4;
+        *reinterpret_cast<float4*>(a.cov + (I0 + row) * a.d + J0 + c4) =
+            make_float4(cpre[q].x + t[0], cpre[q].y + t[1], cpre[q].z + t[2], cpre[q].w + t[3]);
+      }
+      if (!diag && J0 + row < a.d && I0 + c4 < a.d) {
+        // mirrored: C[J0 + row][I0 + c4 + k] = tile[c4 + k][row]
+        const float* t = sC + c4 * kCPad + row;
+        *reinterpret_cast<float4*>(a.cov + (J0 + row) * a.d + I0 + c4) =
+            make_float4(mpre[q].x + t[0], mpre[q].y + t[kCPad], mpre[q].z + t[2 * kCPad], mpre[q].w + t[3 * kCPad]);
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < kT * kT; e += kThreads) {
+      const int row = e / kT, col = e % kT;
+      const int64_t gi = I0 + row, gj = J0 + col;
+      if (gi < a.d && gj < a.d) a.cov[gi * a.d + gj] += sC[row * kCPad + col];
+      if (!diag) {
+        const int64_t mi = J0 + row, mj = I0 + col;
+        if (mi < a.d && mj < a.d) a.cov[mi * a.d + mj] += sC[col * kCPad + row];
+      }
     }
   }
   if (diag && a.colsum && threadIdx.x < kT && I0 + threadIdx.x < a.d) a.colsum[I0 + threadIdx.x] += colsum;
