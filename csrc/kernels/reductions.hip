@@ -89,6 +89,39 @@ __global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
   if (active) {
     for (int64_t i = r0 + rl; i < r1; i += static_cast<int64_t>(RPP) * U) {
       float xv[U][V], tv[U][V], wv[U];
+      if constexpr (V == 4) {
+        // f32 rows (launch_column_moments checked dtype, unit stride, alignment): every load
+        // from a clamped valid row, masked after - guarded loads through the dtype dispatch
+        // compiled to a branch + vmcnt(0) per load
+        // both operands always loaded (an absent one aliases the other; masked below)
+        const float* xp = static_cast<const float*>(want_x ? a.x : a.t);
+        const float* tp = static_cast<const float*>(want_t ? a.t : a.x);
+        const int64_t xrs = want_x ? a.x_row_stride : a.t_row_stride;
+        const int64_t trs = want_t ? a.t_row_stride : a.x_row_stride;
+        float4 xq[U], tq[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t row = i + static_cast<int64_t>(u) * RPP;
+          const int64_t rc = row < r1 ? row : i;
+          xq[u] = *reinterpret_cast<const float4*>(xp + rc * xrs + col);
+          tq[u] = *reinterpret_cast<const float4*>(tp + rc * trs + col);
+          wv[u] = a.w ? static_cast<float>(load_as_f64(a.w, a.w_dt, rc * a.w_stride)) : 1.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = i + static_cast<int64_t>(u) * RPP < r1;
+          const bool okx = ok && want_x, okt = ok && want_t;
+          wv[u] = ok ? wv[u] : 0.f;
+          xv[u][0] = okx ? xq[u].x : 0.f;
+          xv[u][1] = okx ? xq[u].y : 0.f;
+          xv[u][2] = okx ? xq[u].z : 0.f;
+          xv[u][3] = okx ? xq[u].w : 0.f;
+          tv[u][0] = okt ? tq[u].x : 0.f;
+          tv[u][1] = okt ? tq[u].y : 0.f;
+          tv[u][2] = okt ? tq[u].z : 0.f;
+          tv[u][3] = okt ? tq[u].w : 0.f;
+        }
+      } else {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int64_t row = i + static_cast<int64_t>(u) * RPP;
@@ -105,6 +138,7 @@ __global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
             if (want_t) tv[u][e] = static_cast<float>(load_as_f64(a.t, a.t_dt, row * a.t_row_stride + (col + e) * a.t_col_stride));
           }
         }
+      }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
