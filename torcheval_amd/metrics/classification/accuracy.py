@@ -92,6 +92,8 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         self._add_state("num_total", torch.zeros(shape, device=self.device), merge="sum")
         self._refresh_fast_path()
 
+    _err_words = 1  # K1's device flag: one int32 code
+
     def _refresh_fast_path(self) -> None:
         # north-star fast path (ROCm states, micro, k=1): ONE native call that tests every
         # precondition itself and returns False for anything it does not handle
@@ -174,8 +176,11 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
     @torch.inference_mode()
     def compute(self: TAccuracy) -> torch.Tensor:
         """Return the accuracy (NaN if ``update()`` was never called)."""
+        # the division is enqueued before the flag read, so that read (a host sync) does not
+        # hold the launch back
+        out = _accuracy_compute(self.num_correct, self.num_total, self.average)
         self._check_device_errors()
-        return _accuracy_compute(self.num_correct, self.num_total, self.average)
+        return out
 
     @torch.inference_mode()
     def merge_state(self: TAccuracy, metrics: Iterable[TAccuracy]) -> TAccuracy:
@@ -191,6 +196,8 @@ class BinaryAccuracy(MulticlassAccuracy):
     (``torch.where(input < threshold, 0, 1)``).
     Functional version: ``torcheval_amd.metrics.functional.binary_accuracy``.
     """
+
+    _err_words = 0  # no device flag
 
     def __init__(
         self: TBinaryAccuracy,
@@ -240,6 +247,8 @@ class MultilabelAccuracy(MulticlassAccuracy):
     Functional version: ``torcheval_amd.metrics.functional.multilabel_accuracy``.
     """
 
+    _err_words = 0  # no device flag
+
     def __init__(
         self: TMultilabelAccuracy,
         *,
@@ -280,6 +289,8 @@ class TopKMultilabelAccuracy(MulticlassAccuracy):
     default ``k=1`` always fails its own check, classification/accuracy.py:380).
     Functional version: ``torcheval_amd.metrics.functional.topk_multilabel_accuracy``.
     """
+
+    _err_words = 0  # no device flag
 
     def __init__(
         self: TTopKMultilabelAccuracy,

@@ -100,6 +100,9 @@ class Metric(Generic[TComputeReturn], ABC):
     # distributed sync: "max" (elementwise; codes and largest offending labels) or "first"
     # (the lowest flagged rank's whole record, for multi-word records).
     _err_merge: str = "max"
+    # Words of the device error flag, when every instance's flag has the same size: the sync
+    # then sizes a receiving rank's flag without reading the gathered record on the host.
+    _err_words: Optional[int] = None
 
     def _check_device_errors(self) -> None:
         """Raise input-validation errors that native kernels recorded on the device.

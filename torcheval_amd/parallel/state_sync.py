@@ -206,8 +206,11 @@ def _merge_err_flags(flags: torch.Tensor, mode: str, keys: List[str], metrics, r
         local = getattr(metrics[key], "_err", None)
         if isinstance(local, torch.Tensor):
             n, dev = local.numel(), local.device
-        else:  # this rank never ran a flagged update: size the flag from the record itself
-            n = int(chosen[i, _ERR_SLOT - 1].item())
+        else:  # this rank never ran a flagged update: size the flag from the metric type, or
+            # (types with variable-size flags) from the record itself - one host read
+            n = getattr(metrics[key], "_err_words", None)
+            if n is None:
+                n = int(chosen[i, _ERR_SLOT - 1].item())
             if n == 0:
                 continue
             dev = metrics[key].device
