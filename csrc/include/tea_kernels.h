@@ -400,6 +400,29 @@ int64_t radix_sort_tiles(int64_t rows, int64_t n);
 int64_t radix_sort_groups(int64_t tiles);
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream);
 int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream);
+// ------------------------------------------------------------------ K3s sample-sort AUROC
+struct SampleSortAucArgs {
+  const float* x = nullptr;  // [n] scores
+  const void* t = nullptr;   // [n] targets (f32 / i64 / i32 / u8 / bool)
+  DType t_dt = DType::f32;
+  int64_t n = 0;
+  int B = 0;      // samplesort_auc_buckets(n): splitters + 1 (power of two)
+  int S = 0;      // 8 * B sampled scores
+  int nbins = 0;  // 2 * B + 2 bins: NaN, +inf, 2B - 1 regular buckets (between / equal-to splitter), -inf
+  uint32_t* sp = nullptr;                          // [B] scratch
+  uint32_t* counts = nullptr;                      // [nbins] zeroed, left zeroed
+  uint32_t* cursor = nullptr;                      // [nbins] zeroed, left zeroed
+  uint32_t* keys_out = nullptr;                    // [n] scratch
+  float* t_out = nullptr;                          // [n] scratch
+  uint32_t* keys_tmp = nullptr;                    // [n] scratch (oversized buckets)
+  float* t_tmp = nullptr;                          // [n] scratch
+  double* rec = nullptr;                           // [nbins, 3] scratch
+  uint32_t* spc = nullptr;                         // [tiles, 3] scratch: special-bin counts per tile
+  double* out = nullptr;                           // [1] AUROC
+};
+int samplesort_auc_buckets(int64_t n);
+bool samplesort_auc_supported(int64_t n);
+int launch_samplesort_auc(const SampleSortAucArgs& a, hipStream_t stream);
 // ------------------------------------------------------------------ K10b retrieval top-k
 struct RetrievalArgs {
   const float* x = nullptr;        // [n] scores
