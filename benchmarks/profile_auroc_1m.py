@@ -2,6 +2,8 @@
 import os
 import sys
 
+os.environ.setdefault("TORCHEVAL_AMD_K3S", "1")
+
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))

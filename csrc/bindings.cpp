@@ -1070,12 +1070,12 @@ void binary_auroc_samplesort(const Tensor& x, const Tensor& t, const Tensor& out
   a.t_dt = dt_of(t);
   a.n = n;
   a.B = tea::samplesort_auc_buckets(n);
-  a.S = 8 * a.B;
+  a.S = 4 * a.B;
   a.nbins = 2 * a.B + 2;
   auto* z = static_cast<uint32_t*>(zeroed_workspace(x, st_, 2 * 4096 * 4, 8));
   a.counts = z;
   a.cursor = z + 4096;
-  const int64_t tiles = (n + 4095) / 4096;
+  const int64_t tiles = (n + 2047) / 2048;
   char* ws = static_cast<char*>(
       scratch_workspace(x, st_, 4 * n * 4 + a.B * 4 + a.nbins * 24 + tiles * 12 + 64, 2));
   a.rec = reinterpret_cast<double*>(ws);

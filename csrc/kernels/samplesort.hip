@@ -7,7 +7,7 @@
 // where TP_above_b is the positive mass of all higher-score buckets, N_b the negative mass of
 // bucket b, and W_b the Mann-Whitney term of b's own samples (tie groups never straddle a
 // bucket, since a sample's bucket is a function of its score).  Five launches:
-//   1. ss_sample : one block draws a stratified sample (8 per bucket), radix-sorts it in LDS
+//   1. ss_sample : one block draws a stratified sample (4 per bucket), radix-sorts it in LDS
 //                  and writes B-1 splitters.  Bucket ids: 2*lb for scores strictly between
 //                  splitters lb-1 and lb, 2*lb+1 for scores EQUAL to splitter lb - so a
 //                  heavily repeated score lands in an "equal" bucket that needs no sort;
@@ -23,6 +23,9 @@
 //                  and the per-bin counters zeroed for the next call (self-cleaning).
 // Within a bucket the scatter order is arbitrary; only tie-group tails contribute and their
 // prefix sums are order independent (exact for integer targets: FP64 accumulation).
+// Status (profiles/rocprof_k3s_samplesort_1m_r2.csv, 1M samples): correct (26 GPU parity tests)
+// but slower than K3a + K3 (~97 us): ss_local 154 us, ss_scatter 39, ss_sample 20, ss_hist 16,
+// ss_final 6.  Opt-in only (TORCHEVAL_AMD_K3S=1) until the local and scatter kernels are fixed.
 // Reference semantics: torcheval/metrics/functional/classification/auroc.py:115-152.
 #include "tea_common.h"
 #include "tea_kernels.h"
@@ -33,10 +36,10 @@ namespace {
 
 constexpr int kSsSampleT = 1024;
 constexpr int kSsT = 256;
-constexpr int kSsPer = 16;
+constexpr int kSsPer = 8;
 constexpr int kSsTile = kSsT * kSsPer;
-constexpr int kSsL = 512;
-constexpr int kSsCap = 4096;
+constexpr int kSsL = 256;
+constexpr int kSsCap = 8192;
 
 __device__ __forceinline__ uint32_t ss_key(float f) {  // ascending key = descending score
   uint32_t u = __float_as_uint(f);
@@ -306,13 +309,14 @@ __global__ __launch_bounds__(kSsT) void ss_scatter_kernel(SampleSortAucArgs a) {
   ss_excl_scan_lds<kSsT>(gbase, a.nbins, slds);  // global bucket starts
   ss_buckets(sp, a.B, a.nbins, k, bid);
   // special samples: ranks in source order (round, wave, lane); others: LDS-atomic ranks
+  const bool any_special = (a.spc[3 * blockIdx.x] | a.spc[3 * blockIdx.x + 1] | a.spc[3 * blockIdx.x + 2]) != 0u;
   const int lane = lane_id(), w = threadIdx.x >> 6;
   const uint64_t below = lane ? (~0ull >> (kWave - lane)) : 0ull;
   uint64_t spm[kSsPer];
 #pragma unroll
   for (int r = 0; r < kSsPer; ++r) {
     const bool valid = t0 + r * kSsT < a.n;
-    const int c = valid ? ss_special(k[r]) : -1;
+    const int c = valid && any_special ? ss_special(k[r]) : -1;
     const uint64_t m0 = __ballot(c == 0), m1 = __ballot(c == 1), m2 = __ballot(c == 2);
     if (lane == 0) {
       sord[(r * 4 + w) * 3] = static_cast<uint32_t>(__popcll(m0));
@@ -410,17 +414,103 @@ __device__ void ss_tie_scan(const uint32_t* sk, const float* sv, int m, bool sin
   P = run;
 }
 
+// W and P of a between bucket without sorting it: its samples are counted into 256 sub-bins by
+// the top 8 free key bits (LDS atomics), placed sub-bin-contiguous (any order inside), and every
+// negative-weight sample adds (1 - t) * (TP of lower sub-bins + TP of smaller keys in its own
+// sub-bin + half the TP of equal keys, itself included) - a pair loop over its sub-bin only
+// (~m / 256 samples for a quantile bucket).  The copy lives in LDS, or in global scratch for an
+// oversized bucket (same code, pointers of either address space).
+__device__ __forceinline__ void ss_subbin_area(const uint32_t* gk, const float* gt, int m, uint32_t* sk, float* st,
+                                               uint32_t* cnt, uint32_t* cur, uint32_t* off, double* tsum, double* dl,
+                                               uint32_t* slds, double& W, double& P) {
+  const int tid = threadIdx.x;
+  // the sub-bin width from the bucket's actual key range (a splitter-bounded range can be far
+  // wider than its samples - the end buckets are unbounded - and put every sample in one sub-bin)
+  uint32_t kmin = 0xffffffffu, kmax = 0u;
+  for (int i = tid; i < m; i += kSsL) {
+    const uint32_t k = gk[i];
+    kmin = k < kmin ? k : kmin;
+    kmax = k > kmax ? k : kmax;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t x = __shfl_xor(kmin, o, kWave), y = __shfl_xor(kmax, o, kWave);
+    kmin = x < kmin ? x : kmin;
+    kmax = y > kmax ? y : kmax;
+  }
+  if (lane_id() == 0) {
+    cnt[tid >> 6] = kmin;
+    cur[tid >> 6] = kmax;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kSsL / kWave; ++q) {
+    kmin = cnt[q] < kmin ? cnt[q] : kmin;
+    kmax = cur[q] > kmax ? cur[q] : kmax;
+  }
+  const uint32_t lo = kmin, span = kmax - kmin;
+  const int sbits = span ? 32 - __clz(static_cast<int>(span)) : 0;
+  const int shift = sbits > 8 ? sbits - 8 : 0;
+  __syncthreads();
+  cnt[tid] = 0u;
+  tsum[tid] = 0.0;
+  __syncthreads();
+  for (int i = tid; i < m; i += kSsL) {
+    const uint32_t sub = (gk[i] - lo) >> shift;
+    atomicAdd(&cnt[sub], 1u);
+    atomicAdd(&tsum[sub], static_cast<double>(gt[i]));
+  }
+  __syncthreads();
+  const uint32_t c = cnt[tid];
+  const double ts = tsum[tid];
+  uint32_t ctot;
+  const uint32_t cinc = ss_scan<kSsL>(c, slds, SsAdd{}, 0u, ctot);
+  double ttot;
+  const double tinc = ss_scan<kSsL>(ts, dl, SsAdd{}, 0.0, ttot);
+  off[tid] = cinc - c;
+  cur[tid] = cinc - c;
+  tsum[tid] = tinc - ts;  // TP of the lower sub-bins
+  __syncthreads();
+  for (int i = tid; i < m; i += kSsL) {
+    const uint32_t k = gk[i];
+    const uint32_t r = atomicAdd(&cur[(k - lo) >> shift], 1u);
+    sk[r] = k;
+    st[r] = gt[i];
+  }
+  __syncthreads();
+  double w = 0.0;
+  for (int i = tid; i < m; i += kSsL) {
+    const float t = st[i];
+    if (t != 1.f) {
+      const uint32_t k = sk[i];
+      const uint32_t sub = (k - lo) >> shift;
+      const int j0 = static_cast<int>(off[sub]), j1 = j0 + static_cast<int>(cnt[sub]);
+      float lt = 0.f, eq = 0.f;
+      for (int j = j0; j < j1; ++j) {
+        const uint32_t kj = sk[j];
+        const float tj = st[j];
+        lt += kj < k ? tj : 0.f;
+        eq += kj == k ? tj : 0.f;
+      }
+      w += (1.0 - static_cast<double>(t)) * (tsum[sub] + static_cast<double>(lt) + 0.5 * static_cast<double>(eq));
+    }
+  }
+  double wt;
+  ss_scan<kSsL>(w, dl, SsAdd{}, 0.0, wt);
+  W = wt;
+  P = ttot;
+}
+
 __global__ __launch_bounds__(kSsL) void ss_local_kernel(SampleSortAucArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
-  uint32_t* ka = sh;
-  uint32_t* kb = ka + kSsCap;
-  float* va = reinterpret_cast<float*>(kb + kSsCap);
-  float* vb = va + kSsCap;
-  uint32_t(*cnt)[256] = reinterpret_cast<uint32_t(*)[256]>(vb + kSsCap);
-  uint32_t* base = reinterpret_cast<uint32_t*>(cnt + kSsL / kWave);
-  uint32_t* tot = base + 256;
-  uint32_t* slds = tot + 256;
-  double* s_e = reinterpret_cast<double*>(slds + 16);
+  uint32_t* sk = sh;
+  float* st = reinterpret_cast<float*>(sk + kSsCap);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(st + kSsCap);
+  uint32_t* cur = cnt + 256;
+  uint32_t* off = cur + 256;
+  uint32_t* slds = off + 256;
+  double* tsum = reinterpret_cast<double*>(slds + 16);
+  double* s_e = tsum + 256;
   double* dl = s_e + kSsL;
   int* il = reinterpret_cast<int*>(dl + 16);
   double* s_cd = reinterpret_cast<double*>(il + 16);
@@ -450,23 +540,10 @@ __global__ __launch_bounds__(kSsL) void ss_local_kernel(SampleSortAucArgs a) {
         ss_scan<kSsL>(sum, dl, SsAdd{}, 0.0, P);
         W = 0.5 * (static_cast<double>(m) - P) * P;
       } else {
-        const int passes = (bits + 7) / 8;
-        if (m <= kSsCap) {
-          for (int i = tid; i < m; i += kSsL) {
-            ka[i] = gk[i];
-            va[i] = gt[i];
-          }
-          __syncthreads();
-          ss_block_lsd<kSsL, true>(ka, va, kb, vb, m, passes, cnt, base, tot, slds);
-          const bool odd = passes & 1;
-          ss_tie_scan(odd ? kb : ka, odd ? vb : va, m, false, s_e, dl, il, s_cd, s_ci, W, P);
-        } else {  // oversized bucket: the same sort over global scratch (L2-resident)
-          uint32_t* tk = a.keys_tmp + start;
-          float* tt = a.t_tmp + start;
-          ss_block_lsd<kSsL, true>(gk, gt, tk, tt, m, passes, cnt, base, tot, slds);
-          const bool odd = passes & 1;
-          ss_tie_scan(odd ? tk : gk, odd ? tt : gt, m, false, s_e, dl, il, s_cd, s_ci, W, P);
-        }
+        if (m <= kSsCap)
+          ss_subbin_area(gk, gt, m, sk, st, cnt, cur, off, tsum, dl, slds, W, P);
+        else  // oversized bucket: the sub-bin copy in global scratch (L2-resident)
+          ss_subbin_area(gk, gt, m, a.keys_tmp + start, a.t_tmp + start, cnt, cur, off, tsum, dl, slds, W, P);
       }
     }
   }
@@ -516,15 +593,14 @@ int samplesort_auc_buckets(int64_t n) {
 bool samplesort_auc_supported(int64_t n) { return n >= (int64_t{1} << 15) && n <= (int64_t{1} << 21); }
 
 int launch_samplesort_auc(const SampleSortAucArgs& a, hipStream_t stream) {
-  if (!samplesort_auc_supported(a.n) || a.B != samplesort_auc_buckets(a.n) || a.S != 8 * a.B ||
+  if (!samplesort_auc_supported(a.n) || a.B != samplesort_auc_buckets(a.n) || a.S != 4 * a.B ||
       a.nbins != 2 * a.B + 2 || a.spc == nullptr)
     return -2;
   const unsigned tiles = static_cast<unsigned>((a.n + kSsTile - 1) / kSsTile);
   const size_t lds_sample = (2 * static_cast<size_t>(a.S) + (kSsSampleT / kWave) * 256 + 512 + 16) * 4;
   const size_t lds_hist = (static_cast<size_t>(a.B) + a.nbins) * 4;
   const size_t lds_scatter = (static_cast<size_t>(a.B) + 2 * a.nbins + 3 * kSsTile + 16 + kSsPer * 12 + 4) * 4;
-  const size_t lds_local = (4 * static_cast<size_t>(kSsCap) + (kSsL / kWave) * 256 + 512 + 16) * 4 +
-                           (kSsL + 16) * 8 + 16 * 4 + 16;
+  const size_t lds_local = (2 * static_cast<size_t>(kSsCap) + 3 * 256 + 16) * 4 + (256 + kSsL + 16) * 8 + 16 * 4 + 16;
   // dynamic LDS beyond 64 KB needs the per-kernel opt-in
   static const bool lds_ok = [] {
     constexpr int kMax = 160 * 1024;

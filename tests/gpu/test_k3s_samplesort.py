@@ -144,7 +144,7 @@ def test_oversized_bucket():
     g = torch.Generator().manual_seed(9)
     x = 0.4 + 0.2 * torch.rand(n, generator=g, dtype=torch.float64)
     x = x.float()
-    pos = _sample_positions(n, 8 * B)
+    pos = _sample_positions(n, 4 * B)
     x[pos] = torch.where(torch.rand(len(pos), generator=g) < 0.5, torch.tensor(0.1), torch.tensor(0.9))
     t = torch.randint(0, 2, (n,), generator=g)
     _check(x, t)
