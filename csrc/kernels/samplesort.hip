@@ -24,8 +24,11 @@
 // Within a bucket the scatter order is arbitrary; only tie-group tails contribute and their
 // prefix sums are order independent (exact for integer targets: FP64 accumulation).
 // Status (profiles/rocprof_k3s_samplesort_1m_r2.csv, 1M samples): correct (26 GPU parity tests)
-// but slower than K3a + K3 (~97 us): ss_local 154 us, ss_scatter 39, ss_sample 20, ss_hist 16,
+// but slower than K3a + K3 (~97 us): ss_local 136 us, ss_scatter 30, ss_sample 20, ss_hist 17,
 // ss_final 6.  Opt-in only (TORCHEVAL_AMD_K3S=1) until the local and scatter kernels are fixed.
+// (Measured: buckets of a 1M uniform row are <= 6.2K samples with ~30-sample sub-bins, so the
+// local kernel is not an oversized-bucket or sub-bin-skew problem; batching its loads cut it
+// from 154 to 136 us only.)
 // Reference semantics: torcheval/metrics/functional/classification/auroc.py:115-152.
 #include "tea_common.h"
 #include "tea_kernels.h"
@@ -112,6 +115,41 @@ __device__ __forceinline__ void ss_excl_scan_lds(uint32_t* v, int len, uint32_t*
       run += x;
     }
   __syncthreads();
+}
+
+// Strided loops whose body waits on a global load (or a returning atomic) compile to one memory
+// round trip per iteration; these helpers issue U loads per thread before using any of them.
+template <int NT, int U = 8>
+__device__ __forceinline__ void ss_copy_lds(uint32_t* dst, const uint32_t* src, int len) {
+  for (int c0 = 0; c0 < len; c0 += NT * U) {
+    uint32_t v[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = c0 + q * NT + static_cast<int>(threadIdx.x);
+      v[q] = src[i < len ? i : len - 1];
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = c0 + q * NT + static_cast<int>(threadIdx.x);
+      if (i < len) dst[i] = v[q];
+    }
+  }
+}
+
+template <int NT, int U = 8>
+__device__ __forceinline__ uint32_t ss_sum_prefix(const uint32_t* src, int len) {  // this thread's share of sum src[0, len)
+  uint32_t s = 0;
+  for (int c0 = 0; c0 < len; c0 += NT * U) {
+    uint32_t v[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = c0 + q * NT + static_cast<int>(threadIdx.x);
+      v[q] = src[i < len ? i : 0];
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) s += c0 + q * NT + static_cast<int>(threadIdx.x) < len ? v[q] : 0u;
+  }
+  return s;
 }
 
 // Stable LSD radix sort of m keys (+ optional f32 values) by `passes` 8-bit digits from bit 0,
@@ -238,7 +276,7 @@ __global__ __launch_bounds__(kSsT) void ss_hist_kernel(SampleSortAucArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint32_t sh[];
   uint32_t* sp = sh;
   uint32_t* hist = sh + a.B;
-  for (int j = threadIdx.x; j < a.B; j += kSsT) sp[j] = a.sp[j];
+  ss_copy_lds<kSsT>(sp, a.sp, a.B);
   for (int j = threadIdx.x; j < a.nbins; j += kSsT) hist[j] = 0u;
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kSsTile + threadIdx.x;
   uint32_t k[kSsPer], bid[kSsPer];
@@ -276,11 +314,9 @@ __global__ __launch_bounds__(kSsT) void ss_scatter_kernel(SampleSortAucArgs a) {
   uint32_t* slds = sbid + kSsTile;
   uint32_t* sord = slds + 16;        // [kSsPer][4 waves][3 classes] ballot counts, then prefixes
   uint32_t* sprev = sord + kSsPer * 12;  // [3] special samples of the tiles before this one
-  for (int j = threadIdx.x; j < a.B; j += kSsT) sp[j] = a.sp[j];
-  for (int j = threadIdx.x; j < a.nbins; j += kSsT) {
-    lcnt[j] = 0u;
-    gbase[j] = a.counts[j];
-  }
+  ss_copy_lds<kSsT>(sp, a.sp, a.B);
+  ss_copy_lds<kSsT>(gbase, a.counts, a.nbins);
+  for (int j = threadIdx.x; j < a.nbins; j += kSsT) lcnt[j] = 0u;
   const int64_t t0 = static_cast<int64_t>(blockIdx.x) * kSsTile + threadIdx.x;
   uint32_t k[kSsPer], bid[kSsPer], rk[kSsPer];
   float tv[kSsPer];
@@ -293,10 +329,24 @@ __global__ __launch_bounds__(kSsT) void ss_scatter_kernel(SampleSortAucArgs a) {
   }
   {  // special samples of earlier tiles (per class)
     uint32_t c[3] = {0u, 0u, 0u};
-    for (int u = threadIdx.x; u < static_cast<int>(blockIdx.x); u += kSsT) {
-      c[0] += a.spc[3 * u];
-      c[1] += a.spc[3 * u + 1];
-      c[2] += a.spc[3 * u + 2];
+    const int nprev = static_cast<int>(blockIdx.x);
+    for (int u0 = 0; u0 < nprev; u0 += kSsT * 4) {
+      uint32_t v[4][3];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int u = u0 + q * kSsT + static_cast<int>(threadIdx.x);
+        const int uc = u < nprev ? u : 0;
+        v[q][0] = a.spc[3 * uc];
+        v[q][1] = a.spc[3 * uc + 1];
+        v[q][2] = a.spc[3 * uc + 2];
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const bool ok = u0 + q * kSsT + static_cast<int>(threadIdx.x) < nprev;
+        c[0] += ok ? v[q][0] : 0u;
+        c[1] += ok ? v[q][1] : 0u;
+        c[2] += ok ? v[q][2] : 0u;
+      }
     }
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -346,9 +396,19 @@ __global__ __launch_bounds__(kSsT) void ss_scatter_kernel(SampleSortAucArgs a) {
       rk[r] = sord[(r * 4 + w) * 3 + c] + static_cast<uint32_t>(__popcll(spm[r] & below));
     }
   }
-  for (int j = threadIdx.x + 2; j < a.nbins - 1; j += kSsT) {
-    const uint32_t c = lcnt[j];
-    if (c) gbase[j] += atomicAdd(&a.cursor[j], c);
+  for (int j0 = 2; j0 < a.nbins - 1; j0 += kSsT * 8) {  // all of this thread's cursor atomics in flight
+    uint32_t r[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = j0 + q * kSsT + static_cast<int>(threadIdx.x);
+      const uint32_t c = j < a.nbins - 1 ? lcnt[j] : 0u;
+      r[q] = c ? atomicAdd(&a.cursor[j], c) : 0u;
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int j = j0 + q * kSsT + static_cast<int>(threadIdx.x);
+      if (j < a.nbins - 1) gbase[j] += r[q];
+    }
   }
   ss_excl_scan_lds<kSsT>(lcnt, a.nbins, slds);  // tile starts (has a trailing barrier)
 #pragma unroll
@@ -426,11 +486,20 @@ __device__ __forceinline__ void ss_subbin_area(const uint32_t* gk, const float* 
   const int tid = threadIdx.x;
   // the sub-bin width from the bucket's actual key range (a splitter-bounded range can be far
   // wider than its samples - the end buckets are unbounded - and put every sample in one sub-bin)
+  constexpr int U = 8;  // loads in flight per thread in each sweep
   uint32_t kmin = 0xffffffffu, kmax = 0u;
-  for (int i = tid; i < m; i += kSsL) {
-    const uint32_t k = gk[i];
-    kmin = k < kmin ? k : kmin;
-    kmax = k > kmax ? k : kmax;
+  for (int c0 = 0; c0 < m; c0 += kSsL * U) {
+    uint32_t kk[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = c0 + q * kSsL + tid;
+      kk[q] = gk[i < m ? i : m - 1];  // the clamped duplicate leaves min / max unchanged
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      kmin = kk[q] < kmin ? kk[q] : kmin;
+      kmax = kk[q] > kmax ? kk[q] : kmax;
+    }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
@@ -455,10 +524,24 @@ __device__ __forceinline__ void ss_subbin_area(const uint32_t* gk, const float* 
   cnt[tid] = 0u;
   tsum[tid] = 0.0;
   __syncthreads();
-  for (int i = tid; i < m; i += kSsL) {
-    const uint32_t sub = (gk[i] - lo) >> shift;
-    atomicAdd(&cnt[sub], 1u);
-    atomicAdd(&tsum[sub], static_cast<double>(gt[i]));
+  for (int c0 = 0; c0 < m; c0 += kSsL * U) {
+    uint32_t kk[U];
+    float tt[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = c0 + q * kSsL + tid;
+      const int ic = i < m ? i : m - 1;
+      kk[q] = gk[ic];
+      tt[q] = gt[ic];
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      if (c0 + q * kSsL + tid < m) {
+        const uint32_t sub = (kk[q] - lo) >> shift;
+        atomicAdd(&cnt[sub], 1u);
+        atomicAdd(&tsum[sub], static_cast<double>(tt[q]));
+      }
+    }
   }
   __syncthreads();
   const uint32_t c = cnt[tid];
@@ -471,11 +554,24 @@ __device__ __forceinline__ void ss_subbin_area(const uint32_t* gk, const float* 
   cur[tid] = cinc - c;
   tsum[tid] = tinc - ts;  // TP of the lower sub-bins
   __syncthreads();
-  for (int i = tid; i < m; i += kSsL) {
-    const uint32_t k = gk[i];
-    const uint32_t r = atomicAdd(&cur[(k - lo) >> shift], 1u);
-    sk[r] = k;
-    st[r] = gt[i];
+  for (int c0 = 0; c0 < m; c0 += kSsL * U) {
+    uint32_t kk[U];
+    float tt[U];
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      const int i = c0 + q * kSsL + tid;
+      const int ic = i < m ? i : m - 1;
+      kk[q] = gk[ic];
+      tt[q] = gt[ic];
+    }
+#pragma unroll
+    for (int q = 0; q < U; ++q) {
+      if (c0 + q * kSsL + tid < m) {
+        const uint32_t r = atomicAdd(&cur[(kk[q] - lo) >> shift], 1u);
+        sk[r] = kk[q];
+        st[r] = tt[q];
+      }
+    }
   }
   __syncthreads();
   double w = 0.0;
@@ -517,8 +613,7 @@ __global__ __launch_bounds__(kSsL) void ss_local_kernel(SampleSortAucArgs a) {
   int* s_ci = reinterpret_cast<int*>(s_cd + 1);
   const int b = blockIdx.x;
   const int tid = threadIdx.x;
-  uint32_t part = 0;
-  for (int j = tid; j < b; j += kSsL) part += a.counts[j];
+  const uint32_t part = ss_sum_prefix<kSsL>(a.counts, b);
   uint32_t start;
   ss_scan<kSsL>(part, slds, SsAdd{}, 0u, start);
   const int m = static_cast<int>(a.counts[b]);
@@ -536,7 +631,16 @@ __global__ __launch_bounds__(kSsL) void ss_local_kernel(SampleSortAucArgs a) {
       const int bits = (rb & 1) || lo == hi ? 0 : 32 - __clz(static_cast<int>(lo ^ hi));
       if (bits == 0) {  // one score: a single tie group, W = N * P / 2
         double sum = 0.0;
-        for (int i = tid; i < m; i += kSsL) sum += gt[i];
+        for (int c0 = 0; c0 < m; c0 += kSsL * 8) {
+          float tt[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const int i = c0 + q * kSsL + tid;
+            tt[q] = gt[i < m ? i : m - 1];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) sum += c0 + q * kSsL + tid < m ? tt[q] : 0.f;
+        }
         ss_scan<kSsL>(sum, dl, SsAdd{}, 0.0, P);
         W = 0.5 * (static_cast<double>(m) - P) * P;
       } else {
