@@ -28,7 +28,10 @@
 // ss_final 6.  Opt-in only (TORCHEVAL_AMD_K3S=1) until the local and scatter kernels are fixed.
 // (Measured: buckets of a 1M uniform row are <= 6.2K samples with ~30-sample sub-bins, so the
 // local kernel is not an oversized-bucket or sub-bin-skew problem; batching its loads cut it
-// from 154 to 136 us only.)
+// from 154 to 136 us only.  SQ counters (profiles/pmc_k3s_samplesort_1m_r2.csv): its 4104 waves
+// live ~5.5K cycles each, 22.7M wave-cycles over a 136 us dispatch = ~70 waves resident on
+// average, so one long block (or a dispatch limit) sets the time, not the per-bucket work.  The
+// hist kernel's LDS binary search takes ~9 bank conflicts per LDS instruction.)
 // Reference semantics: torcheval/metrics/functional/classification/auroc.py:115-152.
 #include "tea_common.h"
 #include "tea_kernels.h"
