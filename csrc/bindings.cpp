@@ -923,6 +923,47 @@ void fid_cov_update(const Tensor& act_in, const Tensor& cov, const optional<Tens
 }
 
 
+// ---------------------------------------------------------------- K9b symmetric eigenvalues
+// Eigenvalues (ascending) of a symmetric FP64 [n, n] matrix by the LDS-resident one-launch
+// Householder reduction + multisection (csrc/kernels/symeig.hip).  Returns 0 when launched
+// (then status[0] != 0 after the stream reaches it means the grid aborted and lam is
+// invalid), non-zero when this device / size is not handled (nothing launched).
+int64_t sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) {
+  check_gpu(m, "matrix");
+  TORCH_CHECK(m.dim() == 2 && m.size(0) == m.size(1) && m.scalar_type() == at::kDouble && m.is_contiguous(),
+              "sym_eigvals: matrix must be a contiguous float64 [n, n]");
+  const int64_t n = m.size(0);
+  TORCH_CHECK(lam.scalar_type() == at::kDouble && lam.is_contiguous() && lam.numel() == n &&
+                  lam.device() == m.device(),
+              "sym_eigvals: lam must be a contiguous float64 [n] on the matrix's device");
+  TORCH_CHECK(status.scalar_type() == at::kInt && status.numel() >= 1 && status.device() == m.device(),
+              "sym_eigvals: status must be an int32 tensor on the matrix's device");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(m.device());
+  int grid = 0, rows = 0;
+  if (tea::symeig_plan(n, &grid, &rows) != 0) return 1;
+  const hipStream_t stream = stream_for(m);
+  tea::SymEigArgs a;
+  a.a = m.data_ptr<double>();
+  a.n = n;
+  a.ld = tea::symeig_slot_stride(n);
+  // layout: ctl (256 B), d [ld], e [ld], pslot [n-2, ld], rslot [n-2, ld]
+  const int64_t bytes = 256 + (2 * a.ld + 2 * (n - 2) * a.ld) * (int64_t)sizeof(double);
+  char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3));
+  a.ctl = reinterpret_cast<unsigned*>(ws);
+  a.d = reinterpret_cast<double*>(ws + 256);
+  a.e = a.d + a.ld;
+  a.pslot = a.e + a.ld;
+  a.rslot = a.pslot + (n - 2) * a.ld;
+  a.lam = lam.data_ptr<double>();
+  const int rc = tea::launch_symeig(a, stream);
+  if (rc == 1 || rc == 3) return rc;
+  check_launch(rc, "sym_eigvals");
+  TORCH_CHECK(hipMemcpyAsync(status.data_ptr<int>(), a.ctl + 1, sizeof(int), hipMemcpyDeviceToDevice, stream) ==
+                  hipSuccess,
+              "sym_eigvals: status copy failed");
+  return 0;
+}
+
 // K2: multilabel accuracy counts straight into float32 state scalars.
 void multilabel_counts(const Tensor& input, const Tensor& target, double threshold, int64_t k,
                        int64_t criteria, const Tensor& num_correct, const optional<Tensor>& num_total,
@@ -1210,6 +1251,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_rec") = py::none());
   m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
         py::arg("act"), py::arg("cov"), py::arg("colsum"));
+  m.def("sym_eigvals", &sym_eigvals, "K9b eigenvalues of a symmetric float64 matrix (LDS-resident Householder + multisection)",
+        py::arg("m"), py::arg("lam"), py::arg("status"));
   tea_register_runtime(m);
   tea_register_cpu_metrics(m);
 }

@@ -443,3 +443,25 @@ constexpr int kRetrievalMaxLds = 64 * 1024;  // 2 x Q int32 of LDS: Q <= 8192
 int launch_retrieval_topk(const RetrievalArgs& a, hipStream_t stream);
 
 }  // namespace tea
+
+namespace tea {
+
+// ------------------------------------------------------------------ K9b symmetric eigenvalues
+struct SymEigArgs {
+  const double* a = nullptr;  // [n, n] symmetric, contiguous
+  int64_t n = 0;
+  int64_t ld = 0;             // slot stride, symeig_slot_stride(n)
+  double* d = nullptr;        // [n] tridiagonal diagonal (workspace)
+  double* e = nullptr;        // [n] off-diagonal (workspace)
+  double* lam = nullptr;      // [n] eigenvalues, ascending
+  double* pslot = nullptr;    // [n - 2, ld] hand-off slots
+  double* rslot = nullptr;    // [n - 2, ld]
+  unsigned* ctl = nullptr;    // 16 B: arrivals, abort (zeroed by the launcher)
+};
+// 0 when the LDS-resident one-launch reduction fits this device (grid / rows per block out)
+int symeig_plan(int64_t n, int* grid, int* rows_per_block);
+int64_t symeig_slot_stride(int64_t n);
+// 0 launched, 1 unsupported size, 2 HIP error, 3 cooperative launch refused
+int launch_symeig(const SymEigArgs& a, hipStream_t stream);
+
+}  // namespace tea

@@ -1,0 +1,101 @@
+"""K9b symmetric eigenvalues (LDS-resident Householder reduction + multisection) vs CPU fp64
+``torch.linalg.eigvalsh``, and the FID compute built on it."""
+
+import pytest
+import torch
+
+from torcheval_amd.metrics.image.fid import _tr_sqrt_product, frechet_distance, sym_eigvalsh
+from torcheval_amd.ops import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _native_eig(m: torch.Tensor) -> torch.Tensor:
+    lam = torch.empty(m.shape[0], dtype=torch.float64, device=DEV)
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
+    rc = native().sym_eigvals(m.contiguous(), lam, status)
+    assert rc == 0, "K9b did not launch"
+    assert int(status.item()) == 0, "K9b grid aborted"
+    return lam.cpu()
+
+
+def _spd(n: int, seed: int, rank: int = None) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(n, rank or n + 7, generator=g, dtype=torch.float64)
+    return x @ x.T / x.shape[1]
+
+
+@pytest.mark.parametrize("n", [3, 4, 5, 17, 64, 255, 256, 257, 1000, 2048])
+def test_random_spd(n):
+    m = _spd(n, n)
+    ref = torch.linalg.eigvalsh(m)
+    got = _native_eig(m.to(DEV))
+    scale = ref.abs().max()
+    torch.testing.assert_close(got, ref, rtol=0, atol=float(1e-12 * n * scale))
+
+
+@pytest.mark.parametrize("n", [6, 300, 2048])
+def test_indefinite_and_clustered(n):
+    g = torch.Generator().manual_seed(7)
+    q, _ = torch.linalg.qr(torch.randn(n, n, generator=g, dtype=torch.float64))
+    lam = torch.cat([torch.full((n // 3,), 2.0), torch.linspace(-5, 5, n - n // 3, dtype=torch.float64)])
+    m = (q * lam) @ q.T
+    m = (m + m.T) / 2
+    ref = torch.linalg.eigvalsh(m)
+    got = _native_eig(m.to(DEV))
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-12 * n * 5)
+
+
+@pytest.mark.parametrize("kind", ["zeros", "identity", "diagonal", "rank3", "tridiagonal"])
+def test_structured(kind):
+    n = 129
+    if kind == "zeros":
+        m = torch.zeros(n, n, dtype=torch.float64)
+    elif kind == "identity":
+        m = torch.eye(n, dtype=torch.float64) * 3.0
+    elif kind == "diagonal":
+        m = torch.diag(torch.arange(n, dtype=torch.float64) - 40.0)
+    elif kind == "rank3":
+        m = _spd(n, 3, rank=3)
+    else:
+        m = torch.diag(torch.full((n,), 2.0, dtype=torch.float64))
+        m += torch.diag(torch.full((n - 1,), -1.0, dtype=torch.float64), 1)
+        m += torch.diag(torch.full((n - 1,), -1.0, dtype=torch.float64), -1)
+    ref = torch.linalg.eigvalsh(m)
+    got = _native_eig(m.to(DEV))
+    scale = max(float(ref.abs().max()), 1.0)
+    torch.testing.assert_close(got, ref, rtol=0, atol=1e-12 * n * scale)
+
+
+def test_repeated_calls_reuse_workspace():
+    a, b = _spd(512, 1), _spd(300, 2)
+    for _ in range(3):
+        torch.testing.assert_close(_native_eig(a.to(DEV)), torch.linalg.eigvalsh(a), rtol=0, atol=1e-9)
+        torch.testing.assert_close(_native_eig(b.to(DEV)), torch.linalg.eigvalsh(b), rtol=0, atol=1e-9)
+
+
+def test_fid_trace_sqrt_matches_cpu():
+    # FID-shaped covariances (D = 2048 from 3000 samples), tr sqrt(S1 S2) vs the CPU path
+    d = 2048
+    g = torch.Generator().manual_seed(0)
+    x1 = torch.randn(3000, d, generator=g, dtype=torch.float64)
+    x2 = torch.randn(3000, d, generator=g, dtype=torch.float64) * 1.3 + 0.1
+    s1, s2 = torch.cov(x1.T), torch.cov(x2.T)
+    ref = _tr_sqrt_product(s1, s2)
+    got = _tr_sqrt_product(s1.to(DEV), s2.to(DEV)).cpu()
+    torch.testing.assert_close(got, ref, rtol=1e-10, atol=0)
+    mu1, mu2 = x1.mean(0), x2.mean(0)
+    torch.testing.assert_close(
+        frechet_distance(mu1.to(DEV), s1.to(DEV), mu2.to(DEV), s2.to(DEV)).cpu(),
+        frechet_distance(mu1, s1, mu2, s2),
+        rtol=1e-9,
+        atol=1e-9,
+    )
+
+
+def test_fallback_sizes():
+    # sizes K9b does not take still go through sym_eigvalsh (rocSOLVER)
+    for n in (1, 2, 2600):
+        m = _spd(n, 5).to(DEV)
+        torch.testing.assert_close(sym_eigvalsh(m).cpu(), torch.linalg.eigvalsh(m.cpu()), rtol=0, atol=1e-9)
