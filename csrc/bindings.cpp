@@ -946,11 +946,11 @@ int64_t sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) {
   a.a = m.data_ptr<double>();
   a.n = n;
   a.ld = tea::symeig_slot_stride(n);
-  // layout: ctl (256 B), d [ld], e [ld], pslot [n-2, ld], rslot [n-2, ld]
-  const int64_t bytes = 256 + (2 * a.ld + 2 * (n - 2) * a.ld) * (int64_t)sizeof(double);
+  // layout: ctl (2 KB), d [ld], e [ld], pslot [n-2, ld], rslot [n-2, ld]
+  const int64_t bytes = 2048 + (2 * a.ld + 2 * (n - 2) * a.ld) * (int64_t)sizeof(double);
   char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3));
   a.ctl = reinterpret_cast<unsigned*>(ws);
-  a.d = reinterpret_cast<double*>(ws + 256);
+  a.d = reinterpret_cast<double*>(ws + 2048);
   a.e = a.d + a.ld;
   a.pslot = a.e + a.ld;
   a.rslot = a.pslot + (n - 2) * a.ld;

@@ -456,7 +456,7 @@ struct SymEigArgs {
   double* lam = nullptr;      // [n] eigenvalues, ascending
   double* pslot = nullptr;    // [n - 2, ld] hand-off slots
   double* rslot = nullptr;    // [n - 2, ld]
-  unsigned* ctl = nullptr;    // 16 B: arrivals, abort (zeroed by the launcher)
+  unsigned* ctl = nullptr;    // 2 KB: arrivals, abort, 8 per-XCD arrivals (zeroed by the launcher)
 };
 // 0 when the LDS-resident one-launch reduction fits this device (grid / rows per block out)
 int symeig_plan(int64_t n, int* grid, int* rows_per_block);

@@ -45,6 +45,7 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kMaxCols = 10;   // columns per thread: n <= 2560
 constexpr int kMaxRows = 10;   // rows per workgroup (LDS: R * n * 8 <= 160 KB)
 constexpr unsigned kSpinLimit = 1u << 18;
+constexpr size_t kCtlBytes = 128 * 9;  // top counter + abort, then one 128-B line per XCD
 
 // every handed-off word is a GLOBAL (address space 1) agent-scope access, never flat
 typedef __attribute__((address_space(1))) unsigned long long gu64;
@@ -61,10 +62,27 @@ __device__ __forceinline__ double ld_wt(double* p) {
       (gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
 }
 
+template <int Ctrl>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), Ctrl, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), Ctrl, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
+__device__ __forceinline__ double readlane_f64(double x, int lane) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), lane),
+                          __builtin_amdgcn_readlane(__double2loint(x), lane));
+}
+
+// Wave64 sum, uniform result: DPP within each 16-lane row (quad swaps, half-row and row
+// mirrors: a few cycles per step instead of an LDS-latency ds_bpermute), then the four row
+// totals by readlane.
 __device__ __forceinline__ double wave_sum(double x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
-  return x;
+  x += dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_f64<0x141>(x);  // row_half_mirror
+  x += dpp_f64<0x140>(x);  // row_mirror
+  return (readlane_f64(x, 15) + readlane_f64(x, 31)) + (readlane_f64(x, 47) + readlane_f64(x, 63));
 }
 
 // Block-wide sums of N values; every thread gets the totals.  `scratch` holds kWaves * N
@@ -89,12 +107,22 @@ __device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
 
 // Grid barrier over the write-through payload of this phase.  Returns false when the grid
 // aborted (a bounded spin ran out here or in another workgroup).
-__device__ __forceinline__ bool grid_arrive_wait(unsigned* ctl_flat, unsigned target, int* s_flag) {
+// XCD-hierarchical arrival: blocks b = x (mod 8) share counter ctl[32 (x + 1)] (one per XCD under
+// the round-robin dispatch), and the last arriver of each group adds to the top counter ctl[0]
+// - at most 32 same-address adds in a row instead of 256.  `phase` counts from 1; the top
+// counter reaches 8 * phase (fewer groups when the grid has < 8 blocks).
+__device__ __forceinline__ bool grid_arrive_wait(unsigned* ctl_flat, unsigned phase, int* s_flag) {
   gu32* ctl = (gu32*)ctl_flat;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are done
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned G = gridDim.x, x = blockIdx.x & 7u;
+    const unsigned groups = G < 8u ? G : 8u;
+    const unsigned members = (G - x + 7u) / 8u;
+    const unsigned target = groups * phase;
+    const unsigned old = __hip_atomic_fetch_add(&ctl[32u * (x + 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == members * phase - 1u)
+      __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     for (unsigned spins = 0;; ++spins) {
       if (__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
@@ -160,7 +188,7 @@ __device__ __forceinline__ void make_v(const double (&a)[kMaxCols], const Reflec
 
 // One workgroup per CU; dynamic LDS = R * n doubles (the owned rows).  Slots: pslot[q * ld + i]
 // = p_q[i], rslot[q * ld + k] = row q+1 as updated through step q-1.  ctl[0] arrivals,
-// ctl[1] abort, zeroed by the launcher.
+// ctl[1] abort, ctl[32 (x + 1)] per-XCD arrivals (own 128-B lines); zeroed by the launcher.
 __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restrict__ A, int n,
                                                            int R, int64_t ld, double* d_out,
                                                            double* e_out, double* pslot,
@@ -171,7 +199,6 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
   __shared__ int s_flag;
 
   const int t = threadIdx.x;
-  const unsigned G = gridDim.x;
   const int row0 = blockIdx.x * R;
   const int nrows = min(R, n - row0);
   for (int idx = t; idx < nrows * n; idx += kThreads) rows[idx] = A[(int64_t)row0 * n + idx];
@@ -214,7 +241,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       }
     }
   }
-  if (!grid_arrive_wait(ctl, G, &s_flag)) return;
+  if (!grid_arrive_wait(ctl, 1u, &s_flag)) return;
 
   for (int j = 0; j <= n - 3; ++j) {
     // ---- w_j from the gathered p_j; row j+1 updated through step j
@@ -294,10 +321,11 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
         }
       }
     }
-    block_sum<kMaxRows>(acc, red[2]);
+    // the owner of row j+2 (the grid's slowest arriver: 16 KB more to publish) issues the
+    // row's stores before the p reduction so they drain behind it; each thread re-reads only
+    // the LDS words it wrote itself
     double* pn = pslot + (int64_t)(j + 1) * ld;
     double* rn = rslot + (int64_t)(j + 1) * ld;
-    if (t < nrows && row0 + t >= j + 2) st_wt(&pn[row0 + t], hn.tau * acc[t]);
     const int ro = (j + 2) - row0;
     if (ro >= 0 && ro < nrows) {
 #pragma unroll
@@ -306,14 +334,18 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
         if (k >= j + 2 && k < n) st_wt(&rn[k], rows[ro * n + k]);
       }
     }
+    block_sum<kMaxRows>(acc, red[2]);
+    if (t < nrows && row0 + t >= j + 2) st_wt(&pn[row0 + t], hn.tau * acc[t]);
 #pragma unroll
     for (int s = 0; s < kMaxCols; ++s) v[s] = vn[s];
     h = hn;
-    if (!grid_arrive_wait(ctl, G * (unsigned)(j + 2), &s_flag)) return;
+    if (!grid_arrive_wait(ctl, (unsigned)(j + 2), &s_flag)) return;
   }
 }
 
 // # eigenvalues of the tridiagonal (d, e2 = e^2) below x (LAPACK dstebz's Sturm count).
+// (A v_rcp_f64 + Newton reciprocal with two interleaved chains per lane measured 13% slower
+// than this plain division at D = 2048: 2.15 vs 1.9 ms.)
 __device__ __forceinline__ int sturm_count(const double* d, const double* e2, int n, double x,
                                            double pivmin) {
   double q = d[0] - x;
@@ -415,7 +447,7 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   if (hipFuncSetAttribute(reinterpret_cast<const void*>(&tridiag_kernel),
                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return 2;
-  if (hipMemsetAsync(a.ctl, 0, 16, stream) != hipSuccess) return 2;
+  if (hipMemsetAsync(a.ctl, 0, kCtlBytes, stream) != hipSuccess) return 2;
   const double* A = a.a;
   int n = (int)a.n;
   int64_t ld = a.ld;
