@@ -57,7 +57,8 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
     The eigenvalues of S1 S2 equal those of the symmetric L^T S2 L when S1 = L L^T, so the
     fast path is one Cholesky, two triangular products and ONE eigenvalues-only ``eigvalsh``
     (no eigenvectors, no back-transformation).  A singular S1 (fewer samples than features)
-    has no Cholesky factor; then a full ``eigh`` gives S1 = W W^T with W = V_r sqrt(lam_r) over
+    has no Cholesky factor; the same holds with the roles swapped when S2 has one.  When both
+    are singular, a full ``eigh`` gives S1 = W W^T with W = V_r sqrt(lam_r) over
     the numerically non-zero eigenvalues (rank r, the ``matrix_rank`` tolerance of the FP64
     matrix), and the eigvalsh runs on the r x r matrix W^T S2 W: the same non-zero spectrum as
     S1 S2.  The tolerance is deliberately the FP64 one: covariances assembled from FP32 state
@@ -67,6 +68,10 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
     L, info = torch.linalg.cholesky_ex(s1)
     if int(info) == 0:
         m = L.T @ s2 @ L
+    elif int((L2 := torch.linalg.cholesky_ex(s2))[1]) == 0:
+        # S1 singular, S2 not: S1 S2 and S2 S1 share their spectrum, so factor S2 instead
+        # (one more Cholesky rather than a full eigh with eigenvectors)
+        m = L2[0].T @ s1 @ L2[0]
     else:
         lam, vec = torch.linalg.eigh(s1)
         keep = lam > lam.max().clamp(min=0) * lam.numel() * torch.finfo(lam.dtype).eps
