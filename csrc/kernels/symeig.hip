@@ -107,25 +107,26 @@ __device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
 
 // Grid barrier over the write-through payload of this phase.  Returns false when the grid
 // aborted (a bounded spin ran out here or in another workgroup).
-// XCD-hierarchical arrival: blocks b = x (mod 8) share counter ctl[32 (x + 1)] (one per XCD under
-// the round-robin dispatch), and the last arriver of each group adds to the top counter ctl[0]
-// - at most 32 same-address adds in a row instead of 256.  `phase` counts from 1; the top
-// counter reaches 8 * phase (fewer groups when the grid has < 8 blocks).
+// Arrivals are spread over 8 counters, one per XCD under the round-robin dispatch (block b
+// adds to ctl[32 (b % 8 + 1)], each on its own 128-B line) with a NON-returning add, and the
+// pollers sum the 8 counters (8 independent loads per poll): at most 32 same-address adds in a
+// row and no second hop through a top-level counter.  (The two-level form - last arriver of
+// each group adds to a top counter that everybody polls - took 17.9 ms at D = 2048.)
 __device__ __forceinline__ bool grid_arrive_wait(unsigned* ctl_flat, unsigned phase, int* s_flag) {
   gu32* ctl = (gu32*)ctl_flat;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are done
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned G = gridDim.x, x = blockIdx.x & 7u;
-    const unsigned groups = G < 8u ? G : 8u;
-    const unsigned members = (G - x + 7u) / 8u;
-    const unsigned target = groups * phase;
-    const unsigned old = __hip_atomic_fetch_add(&ctl[32u * (x + 1u)], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (old == members * phase - 1u)
-      __hip_atomic_fetch_add(&ctl[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned target = gridDim.x * phase;
+    __hip_atomic_fetch_add(&ctl[32u * ((blockIdx.x & 7u) + 1u)], 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     int ok = 1;
     for (unsigned spins = 0;; ++spins) {
-      if (__hip_atomic_load(&ctl[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) break;
+      unsigned sum = 0;
+#pragma unroll
+      for (unsigned x = 0; x < 8u; ++x)
+        sum += __hip_atomic_load(&ctl[32u * (x + 1u)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (sum >= target) break;
       if (__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
         ok = 0;
         break;
@@ -188,7 +189,7 @@ __device__ __forceinline__ void make_v(const double (&a)[kMaxCols], const Reflec
 
 // One workgroup per CU; dynamic LDS = R * n doubles (the owned rows).  Slots: pslot[q * ld + i]
 // = p_q[i], rslot[q * ld + k] = row q+1 as updated through step q-1.  ctl[0] arrivals,
-// ctl[1] abort, ctl[32 (x + 1)] per-XCD arrivals (own 128-B lines); zeroed by the launcher.
+// ctl[1] abort, ctl[32 (x + 1)] arrival counters (own 128-B lines); zeroed by the launcher.
 __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restrict__ A, int n,
                                                            int R, int64_t ld, double* d_out,
                                                            double* e_out, double* pslot,
