@@ -26,8 +26,8 @@
 // falls back to rocSOLVER when the status word is non-zero.
 //
 // The tridiagonal eigenvalues then come from ``tridiag_eigvals_kernel``: one wave per
-// eigenvalue index (16 lanes), 16-point multisection of the Gershgorin interval with Sturm
-// counts (LAPACK dstebz's count with pivmin), ~13 rounds to double precision.  Eigenvalues are written
+// eigenvalue index (16 or 64 lanes), multisection of the Gershgorin interval with Sturm counts
+// (LAPACK dstebz's count with pivmin), ~9-13 rounds to double precision.  Eigenvalues are written
 // in ascending order; the caller sums sqrt(max(lambda, 0)).
 
 #include <hip/hip_runtime.h>
@@ -363,10 +363,10 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e2, in
 }
 
 constexpr int kEigMaxN = 2560;
-constexpr int kEigPerWave = 4;
 
-// 16 lanes per eigenvalue index i (ascending): 16-point multisection of [lo, hi] keeping
+// L lanes per eigenvalue index i (ascending): L-point multisection of [lo, hi] keeping
 // count(a) <= i < count(b).
+template <int L>
 __global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double* __restrict__ d_in,
                                                                    const double* __restrict__ e_in,
                                                                    int n, double* lam) {
@@ -409,28 +409,29 @@ __global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double*
   // widen so count(lo) = 0 and count(hi) = n hold despite rounding
   double a = lo - 2.0 * DBL_EPSILON * span * n - 2.0 * pivmin;
   double b = hi + 2.0 * DBL_EPSILON * span * n + 2.0 * pivmin;
-  // 4 eigenvalues per wave, 16 lanes each: 16-point sections need ~13 rounds instead of ~9
-  // for 64 points, but the total Sturm work is 2.8x smaller (the kernel is throughput-bound on
-  // the FP64 division sequence)
-  const int grp = lane >> 4, sub = lane & 15;
-  const int idx = (blockIdx.x * kWaves + wave) * kEigPerWave + grp;
-  if ((blockIdx.x * kWaves + wave) * kEigPerWave >= n) return;  // whole wave idle; no barrier below
+  // L lanes per eigenvalue, 64 / L eigenvalues per wave.  L = 16 (D >= 1536): 16-point
+  // sections need ~13 rounds instead of ~9 for 64 points, but 2.8x less Sturm work in all
+  // (1.63 vs 1.86 ms at D = 2048); smaller D keeps L = 64 for occupancy (0.29 vs 0.39 ms at 512).
+  constexpr int kPer = 64 / L;
+  const int grp = lane / L, sub = lane % L;
+  const int idx = (blockIdx.x * kWaves + wave) * kPer + grp;
+  if ((blockIdx.x * kWaves + wave) * kPer >= n) return;  // whole wave idle; no barrier below
   bool done = idx >= n;
   for (int round = 0; round < 20; ++round) {
     const double width = b - a;
     // absolute tolerance eps * ||T|| (the accuracy any backward-stable solver delivers)
     done = done || width <= DBL_EPSILON * span + 2.0 * DBL_EPSILON * fmax(fabs(a), fabs(b)) + pivmin;
     if (__all(done)) break;
-    const double x = a + width * (double)(sub + 1) / 17.0;
+    const double x = a + width * (double)(sub + 1) / (double)(L + 1);
     const int c = sturm_count(d, e2, n, x, pivmin);
     const unsigned long long above = __ballot(c > idx);
-    const unsigned gm = (unsigned)(above >> (16 * grp)) & 0xffffu;
-    const int first = gm ? __ffs((int)gm) - 1 : 16;
-    const double xa = __shfl(x, 16 * grp + (first > 0 ? first - 1 : 0), 64);
-    const double xb = __shfl(x, 16 * grp + (first < 16 ? first : 15), 64);
+    const unsigned long long gm = L == 64 ? above : (above >> (L * grp)) & ((1ull << (L % 64)) - 1ull);
+    const int first = gm ? __ffsll((long long)gm) - 1 : L;
+    const double xa = __shfl(x, L * grp + (first > 0 ? first - 1 : 0), 64);
+    const double xb = __shfl(x, L * grp + (first < L ? first : L - 1), 64);
     if (!done) {
       if (first > 0) a = xa;
-      if (first < 16) b = xb;
+      if (first < L) b = xb;
     }
   }
   if (sub == 0 && idx < n) lam[idx] = 0.5 * (a + b);
@@ -470,7 +471,10 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tridiag_kernel), dim3(G),
                                  dim3(kThreads), args, lds, stream) != hipSuccess)
     return 3;
-  tridiag_eigvals_kernel<<<(n + kWaves * kEigPerWave - 1) / (kWaves * kEigPerWave), kThreads, 0, stream>>>(d, e, n, a.lam);
+  if (n >= 1536)
+    tridiag_eigvals_kernel<16><<<(n + kWaves * 4 - 1) / (kWaves * 4), kThreads, 0, stream>>>(d, e, n, a.lam);
+  else
+    tridiag_eigvals_kernel<64><<<(n + kWaves - 1) / kWaves, kThreads, 0, stream>>>(d, e, n, a.lam);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
