@@ -946,14 +946,28 @@ int64_t sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) {
   a.a = m.data_ptr<double>();
   a.n = n;
   a.ld = tea::symeig_slot_stride(n);
-  // layout: ctl (2 KB), d [ld], e [ld], pslot [n-2, ld], rslot [n-2, ld]
-  const int64_t bytes = 2048 + (2 * a.ld + 2 * (n - 2) * a.ld) * (int64_t)sizeof(double);
+  // layout: ctl (2 KB), d [ld], e [ld], then 4 granule planes [n-2, ld].  The granules must
+  // never match a phase tag by accident, so the block is zeroed whenever it is (re)allocated;
+  // afterwards only this op writes it, with tags that change every launch.
+  const int64_t bytes = 2048 + (2 * a.ld + 4 * (n - 2) * a.ld) * (int64_t)sizeof(double);
   char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3));
+  {
+    static std::mutex mu;
+    static std::unordered_map<void*, int64_t> zeroed;
+    static unsigned launches = 0;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = zeroed.find(ws);
+    if (it == zeroed.end() || it->second < bytes) {
+      TORCH_CHECK(hipMemsetAsync(ws, 0, bytes, stream) == hipSuccess, "sym_eigvals: workspace memset failed");
+      zeroed[ws] = bytes;
+    }
+    launches = launches % 0xFFFFFu + 1u;
+    a.tag_base = launches << 12;  // phase tags tag_base | (q + 1), q + 1 < 4096
+  }
   a.ctl = reinterpret_cast<unsigned*>(ws);
   a.d = reinterpret_cast<double*>(ws + 2048);
   a.e = a.d + a.ld;
-  a.pslot = a.e + a.ld;
-  a.rslot = a.pslot + (n - 2) * a.ld;
+  a.gran = reinterpret_cast<unsigned long long*>(a.e + a.ld);
   a.lam = lam.data_ptr<double>();
   const int rc = tea::launch_symeig(a, stream);
   if (rc == 1 || rc == 3) return rc;

@@ -454,9 +454,10 @@ struct SymEigArgs {
   double* d = nullptr;        // [n] tridiagonal diagonal (workspace)
   double* e = nullptr;        // [n] off-diagonal (workspace)
   double* lam = nullptr;      // [n] eigenvalues, ascending
-  double* pslot = nullptr;    // [n - 2, ld] hand-off slots
-  double* rslot = nullptr;    // [n - 2, ld]
-  unsigned* ctl = nullptr;    // 2 KB: arrivals, abort, 8 per-XCD arrivals (zeroed by the launcher)
+  unsigned long long* gran = nullptr;  // 4 planes of [n - 2, ld] tagged hand-off granules
+                                       // (zero when first allocated)
+  unsigned tag_base = 0;      // non-zero, multiple of 4096, different for every launch
+  unsigned* ctl = nullptr;    // 128 B: ctl[1] abort word (zeroed by the launcher)
 };
 // 0 when the LDS-resident one-launch reduction fits this device (grid / rows per block out)
 int symeig_plan(int64_t n, int* grid, int* rows_per_block);

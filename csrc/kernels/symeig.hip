@@ -45,21 +45,31 @@ constexpr int kWaves = kThreads / 64;
 constexpr int kMaxCols = 10;   // columns per thread: n <= 2560
 constexpr int kMaxRows = 10;   // rows per workgroup (LDS: R * n * 8 <= 160 KB)
 constexpr unsigned kSpinLimit = 1u << 18;
-constexpr size_t kCtlBytes = 128 * 9;  // top counter + abort, then one 128-B line per XCD
+constexpr size_t kCtlBytes = 128;  // ctl[1] = abort word
 
 // every handed-off word is a GLOBAL (address space 1) agent-scope access, never flat
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-__device__ __forceinline__ void st_wt(double* p, double x) {
-  __hip_atomic_store((gu64*)p,
-                     static_cast<unsigned long long>(__double_as_longlong(x)), __ATOMIC_RELAXED,
+// Hand-offs are 8-byte granules {tag, 32 bits of payload}: a double travels as a hi and a lo
+// granule in two planes.  One agent-scope (write-through) store each; the consumer polls the
+// granules themselves with agent-scope loads until every tag is the phase's, so the data IS
+// the flag: no drain, no counter, no fence.
+__device__ __forceinline__ void put(unsigned long long* g, int64_t plane, int64_t i, double x,
+                                    unsigned tag) {
+  const unsigned long long t = static_cast<unsigned long long>(tag) << 32;
+  __hip_atomic_store((gu64*)(g + i), t | static_cast<unsigned>(__double2hiint(x)), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((gu64*)(g + plane + i), t | static_cast<unsigned>(__double2loint(x)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ double ld_wt(double* p) {
-  return __longlong_as_double(static_cast<long long>(__hip_atomic_load(
-      (gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+__device__ __forceinline__ unsigned long long get(unsigned long long* g) {
+  return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ double join(unsigned long long hi, unsigned long long lo) {
+  return __hiloint2double(static_cast<int>(static_cast<unsigned>(hi)), static_cast<int>(static_cast<unsigned>(lo)));
 }
 
 template <int Ctrl>
@@ -105,45 +115,6 @@ __device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
   }
 }
 
-// Grid barrier over the write-through payload of this phase.  Returns false when the grid
-// aborted (a bounded spin ran out here or in another workgroup).
-// Arrivals are spread over 8 counters, one per XCD under the round-robin dispatch (block b
-// adds to ctl[32 (b % 8 + 1)], each on its own 128-B line) with a NON-returning add, and the
-// pollers sum the 8 counters (8 independent loads per poll): at most 32 same-address adds in a
-// row and no second hop through a top-level counter.  (The two-level form - last arriver of
-// each group adds to a top counter that everybody polls - took 17.9 ms at D = 2048.)
-__device__ __forceinline__ bool grid_arrive_wait(unsigned* ctl_flat, unsigned phase, int* s_flag) {
-  gu32* ctl = (gu32*)ctl_flat;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's payload stores are done
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const unsigned target = gridDim.x * phase;
-    __hip_atomic_fetch_add(&ctl[32u * ((blockIdx.x & 7u) + 1u)], 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    int ok = 1;
-    for (unsigned spins = 0;; ++spins) {
-      unsigned sum = 0;
-#pragma unroll
-      for (unsigned x = 0; x < 8u; ++x)
-        sum += __hip_atomic_load(&ctl[32u * (x + 1u)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (sum >= target) break;
-      if (__hip_atomic_load(&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        ok = 0;
-        break;
-      }
-      if (spins > kSpinLimit) {
-        __hip_atomic_store(&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    *s_flag = ok;
-  }
-  __syncthreads();
-  return *s_flag != 0;
-}
-
 struct Reflector {
   double tau, beta, scale, diag;
 };
@@ -187,17 +158,21 @@ __device__ __forceinline__ void make_v(const double (&a)[kMaxCols], const Reflec
   }
 }
 
-// One workgroup per CU; dynamic LDS = R * n doubles (the owned rows).  Slots: pslot[q * ld + i]
-// = p_q[i], rslot[q * ld + k] = row q+1 as updated through step q-1.  ctl[0] arrivals,
-// ctl[1] abort, ctl[32 (x + 1)] arrival counters (own 128-B lines); zeroed by the launcher.
+// One workgroup per CU; dynamic LDS = R * n doubles (the owned rows).  Granule planes of
+// [n - 2, ld] each at gran + {0, 1, 2, 3} * plane: p_q hi / lo, then row q+1 (as updated
+// through step q-1) hi / lo; phase q's tag is tag_base | (q + 1) (tag_base changes every launch,
+// the workspace is zeroed when allocated, so no stale granule matches).  ctl[1] = abort word,
+// zeroed by the launcher.
 __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restrict__ A, int n,
                                                            int R, int64_t ld, double* d_out,
-                                                           double* e_out, double* pslot,
-                                                           double* rslot, unsigned* ctl) {
+                                                           double* e_out, unsigned long long* gran,
+                                                           unsigned tag_base, unsigned* ctl) {
   extern __shared__ double rows[];
   __shared__ double red[3][kWaves * kMaxRows];
   __shared__ double vw[2][kMaxRows];
-  __shared__ int s_flag;
+  const int64_t plane = (int64_t)(n - 2) * ld;
+  unsigned long long* const gp0 = gran;              // p planes
+  unsigned long long* const gr0 = gran + 2 * plane;  // row planes
 
   const int t = threadIdx.x;
   const int row0 = blockIdx.x * R;
@@ -233,33 +208,62 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       }
     }
     block_sum<kMaxRows>(acc, red[2]);
-    if (t < nrows && row0 + t >= 1) st_wt(&pslot[row0 + t], h.tau * acc[t]);
+    if (t < nrows && row0 + t >= 1) put(gp0, plane, row0 + t, h.tau * acc[t], tag_base | 1u);
     if (1 >= row0 && 1 < row0 + nrows) {
 #pragma unroll
       for (int s = 0; s < kMaxCols; ++s) {
         const int k = t + s * kThreads;
-        if (k >= 1 && k < n) st_wt(&rslot[k], rows[(1 - row0) * n + k]);
+        if (k >= 1 && k < n) put(gr0, plane, k, rows[(1 - row0) * n + k], tag_base | 1u);
       }
     }
   }
-  if (!grid_arrive_wait(ctl, 1u, &s_flag)) return;
 
   // (Skipping whole dead column slots with wave-uniform branches in the loads and the LDS
   // pass measured slower - 19.4 vs 17.9 ms at D = 2048: the branches split the batched loads.)
   for (int j = 0; j <= n - 3; ++j) {
-    // ---- w_j from the gathered p_j; row j+1 updated through step j
-    double* ps = pslot + (int64_t)j * ld;
-    double* rs = rslot + (int64_t)j * ld;
+    // ---- w_j from the gathered p_j; row j+1 updated through step j.  Each thread polls the
+    // granules of ITS columns until all carry this phase's tag (bounded; any abort ends the
+    // block at the reduction barrier below)
+    unsigned long long* const gp = gp0 + (int64_t)j * ld;
+    unsigned long long* const gr = gr0 + (int64_t)j * ld;
+    const unsigned tag = tag_base | (unsigned)(j + 1);
+    bool aborted = false;
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int s = 0; s < kMaxCols; ++s) {
+        const int k = t + s * kThreads;
+        if (k >= j + 1 && k < n) {
+          const unsigned long long x0 = get(gp + k), x1 = get(gp + plane + k);
+          const unsigned long long y0 = get(gr + k), y1 = get(gr + plane + k);
+          ok = ok && (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag &&
+               (unsigned)(y0 >> 32) == tag && (unsigned)(y1 >> 32) == tag;
+          w[s] = join(x0, x1);
+          a[s] = join(y0, y1);
+        } else {
+          w[s] = 0.0;
+          a[s] = 0.0;
+        }
+      }
+      if (ok) break;
+      if (__hip_atomic_load((gu32*)&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        aborted = true;
+        break;
+      }
+      if (spins > kSpinLimit) {
+        __hip_atomic_store((gu32*)&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        aborted = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (__syncthreads_or(aborted)) return;
     double r1[2] = {0.0, 0.0};
 #pragma unroll
     for (int s = 0; s < kMaxCols; ++s) {
       const int k = t + s * kThreads;
-      const bool act = k >= j + 1 && k < n;
-      const double p = act ? ld_wt(ps + k) : 0.0;
-      a[s] = act ? ld_wt(rs + k) : 0.0;
-      w[s] = p;
-      r1[0] += p * v[s];
-      r1[1] += k == j + 1 ? p : 0.0;
+      r1[0] += w[s] * v[s];
+      r1[1] += k == j + 1 ? w[s] : 0.0;
     }
     block_sum<2>(r1, red[0]);
     const double c = 0.5 * h.tau * r1[0];
@@ -324,25 +328,22 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
         }
       }
     }
-    // the owner of row j+2 (the grid's slowest arriver: 16 KB more to publish) issues the
-    // row's stores before the p reduction so they drain behind it; each thread re-reads only
-    // the LDS words it wrote itself
-    double* pn = pslot + (int64_t)(j + 1) * ld;
-    double* rn = rslot + (int64_t)(j + 1) * ld;
+    // the owner of row j+2 publishes the row before the p reduction (each thread re-reads
+    // only the LDS words it wrote itself)
+    const unsigned tag1 = tag_base | (unsigned)(j + 2);
     const int ro = (j + 2) - row0;
     if (ro >= 0 && ro < nrows) {
 #pragma unroll
       for (int s = 0; s < kMaxCols; ++s) {
         const int k = t + s * kThreads;
-        if (k >= j + 2 && k < n) st_wt(&rn[k], rows[ro * n + k]);
+        if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, plane, k, rows[ro * n + k], tag1);
       }
     }
     block_sum<kMaxRows>(acc, red[2]);
-    if (t < nrows && row0 + t >= j + 2) st_wt(&pn[row0 + t], hn.tau * acc[t]);
+    if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, plane, row0 + t, hn.tau * acc[t], tag1);
 #pragma unroll
     for (int s = 0; s < kMaxCols; ++s) v[s] = vn[s];
     h = hn;
-    if (!grid_arrive_wait(ctl, (unsigned)(j + 2), &s_flag)) return;
   }
 }
 
@@ -465,9 +466,11 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   const double* A = a.a;
   int n = (int)a.n;
   int64_t ld = a.ld;
-  double *d = a.d, *e = a.e, *ps = a.pslot, *rs = a.rslot;
+  double *d = a.d, *e = a.e;
+  unsigned long long* gran = a.gran;
+  unsigned tag_base = a.tag_base;
   unsigned* ctl = a.ctl;
-  void* args[] = {&A, &n, &R, &ld, &d, &e, &ps, &rs, &ctl};
+  void* args[] = {&A, &n, &R, &ld, &d, &e, &gran, &tag_base, &ctl};
   if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tridiag_kernel), dim3(G),
                                  dim3(kThreads), args, lds, stream) != hipSuccess)
     return 3;
