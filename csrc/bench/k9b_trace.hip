@@ -1,0 +1,79 @@
+// K9b per-phase timeline: builds csrc/kernels/symeig.hip with TEA_SYMEIG_TRACE, runs the
+// D = 2048 tridiagonalisation on a dense symmetric matrix and prints, for workgroups 0 and 100
+// and 16 consecutive columns, the cycles spent waiting for the hand-off and in each step.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -Icsrc/include csrc/bench/k9b_trace.hip -o /tmp/k9b_trace
+#define TEA_SYMEIG_TRACE 1
+#include "../kernels/symeig.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                          \
+  do {                                                                 \
+    hipError_t e_ = (x);                                               \
+    if (e_ != hipSuccess) {                                            \
+      std::printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__); \
+      return 1;                                                        \
+    }                                                                  \
+  } while (0)
+
+int main() {
+  const int n = 2048;
+  std::vector<double> h((size_t)n * n);
+  unsigned long long st = 12345;
+  auto rnd = [&]() {
+    st = st * 6364136223846793005ull + 1442695040888963407ull;
+    return (double)((st >> 11) & ((1ull << 53) - 1)) / (double)(1ull << 53) * 2.0 - 1.0;
+  };
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j <= i; ++j) h[(size_t)i * n + j] = h[(size_t)j * n + i] = rnd() + (i == j ? 4.0 : 0.0);
+  tea::SymEigArgs a;
+  a.n = n;
+  a.ld = tea::symeig_slot_stride(n);
+  double *dA, *dd, *de, *dl;
+  unsigned long long *gran, *trace;
+  unsigned* ctl;
+  const size_t gbytes = (size_t)4 * (n - 2) * a.ld * 8;
+  CK(hipMalloc(&dA, (size_t)n * n * 8));
+  CK(hipMalloc(&dd, a.ld * 8));
+  CK(hipMalloc(&de, a.ld * 8));
+  CK(hipMalloc(&dl, n * 8));
+  CK(hipMalloc(&gran, gbytes));
+  CK(hipMalloc(&ctl, 2048));
+  CK(hipMalloc(&trace, 2 * 16 * 8 * 8));
+  CK(hipMemset(gran, 0, gbytes));
+  CK(hipMemset(trace, 0, 2 * 16 * 8 * 8));
+  CK(hipMemcpy(dA, h.data(), (size_t)n * n * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(tea::g_symeig_trace), &trace, sizeof(trace)));
+  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.gran = gran; a.ctl = ctl;
+  for (int it = 0; it < 3; ++it) {
+    a.tag_base = (unsigned)(it + 1) << 12;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, 0));
+    int rc = tea::launch_symeig(a, 0);
+    CK(hipEventRecord(e1, 0));
+    CK(hipDeviceSynchronize());
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    unsigned abort_word = 0;
+    CK(hipMemcpy(&abort_word, ctl + 1, 4, hipMemcpyDeviceToHost));
+    std::printf("run %d rc=%d abort=%u total %.3f ms\n", it, rc, abort_word, ms);
+  }
+  std::vector<unsigned long long> tr(2 * 16 * 8);
+  CK(hipMemcpy(tr.data(), trace, tr.size() * 8, hipMemcpyDeviceToHost));
+  const char* names[] = {"wait", "R1", "house", "pass", "R3", "publish"};
+  for (int b = 0; b < 2; ++b) {
+    std::printf("workgroup %d (cycles): wait R1 house pass R3 publish | phase total\n", b ? 100 : 0);
+    for (int j = 1; j < 16; ++j) {
+      const unsigned long long* t = &tr[b * 128 + j * 8];
+      const unsigned long long* p = &tr[b * 128 + (j - 1) * 8];
+      std::printf("  j=%d: %llu %llu %llu %llu %llu %llu | %llu\n", 1000 + j, t[0] - p[5], t[1] - t[0],
+                  t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[5] - p[5]);
+    }
+  }
+  (void)names;
+  return 0;
+}

@@ -47,6 +47,20 @@ constexpr int kMaxRows = 10;   // rows per workgroup (LDS: R * n * 8 <= 160 KB)
 constexpr unsigned kSpinLimit = 1u << 18;
 constexpr size_t kCtlBytes = 128;  // ctl[1] = abort word
 
+#ifdef TEA_SYMEIG_TRACE  // csrc/bench/k9b_trace.hip: per-phase timestamps of two workgroups
+__device__ unsigned long long* g_symeig_trace;
+#define SYM_TRACE(j, i)                                                                       \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 100) && (j) >= 1000 &&         \
+        (j) < 1016)                                                                          \
+      g_symeig_trace[(blockIdx.x ? 16 * 8 : 0) + ((j) - 1000) * 8 + (i)] = clock64();        \
+  } while (0)
+#else
+#define SYM_TRACE(j, i) \
+  do {                  \
+  } while (0)
+#endif
+
 // every handed-off word is a GLOBAL (address space 1) agent-scope access, never flat
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
@@ -121,11 +135,12 @@ struct Reflector {
 
 // LAPACK dlarfg on x = a[j+1 .. n): alpha = a[j+1], sigma = sum_{k >= j+2} a[k]^2; also
 // broadcasts the diagonal a[j].  v[k] = 1 at k = j+1, a[k] * scale beyond, 0 before.
-__device__ __forceinline__ Reflector householder(const double (&a)[kMaxCols], int j, int n,
+template <int C>
+__device__ __forceinline__ Reflector householder(const double (&a)[C], int j, int n,
                                                  double* scratch) {
   double r[3] = {0.0, 0.0, 0.0};
 #pragma unroll
-  for (int s = 0; s < kMaxCols; ++s) {
+  for (int s = 0; s < C; ++s) {
     const int k = threadIdx.x + s * kThreads;
     const double x = a[s];
     r[0] += (k >= j + 2 && k < n) ? x * x : 0.0;
@@ -149,10 +164,11 @@ __device__ __forceinline__ Reflector householder(const double (&a)[kMaxCols], in
   return h;
 }
 
-__device__ __forceinline__ void make_v(const double (&a)[kMaxCols], const Reflector& h, int j,
-                                       double (&v)[kMaxCols]) {
+template <int C>
+__device__ __forceinline__ void make_v(const double (&a)[C], const Reflector& h, int j,
+                                       double (&v)[C]) {
 #pragma unroll
-  for (int s = 0; s < kMaxCols; ++s) {
+  for (int s = 0; s < C; ++s) {
     const int k = threadIdx.x + s * kThreads;
     v[s] = k == j + 1 ? 1.0 : (k >= j + 2 ? a[s] * h.scale : 0.0);
   }
@@ -163,13 +179,14 @@ __device__ __forceinline__ void make_v(const double (&a)[kMaxCols], const Reflec
 // through step q-1) hi / lo; phase q's tag is tag_base | (q + 1) (tag_base changes every launch,
 // the workspace is zeroed when allocated, so no stale granule matches).  ctl[1] = abort word,
 // zeroed by the launcher.
+template <int C, int RM>
 __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restrict__ A, int n,
                                                            int R, int64_t ld, double* d_out,
                                                            double* e_out, unsigned long long* gran,
                                                            unsigned tag_base, unsigned* ctl) {
   extern __shared__ double rows[];
-  __shared__ double red[3][kWaves * kMaxRows];
-  __shared__ double vw[2][kMaxRows];
+  __shared__ double red[3][kWaves * RM];
+  __shared__ double vw[2][RM];
   const int64_t plane = (int64_t)(n - 2) * ld;
   unsigned long long* const gp0 = gran;              // p planes
   unsigned long long* const gr0 = gran + 2 * plane;  // row planes
@@ -179,9 +196,9 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
   const int nrows = min(R, n - row0);
   for (int idx = t; idx < nrows * n; idx += kThreads) rows[idx] = A[(int64_t)row0 * n + idx];
 
-  double a[kMaxCols], v[kMaxCols], w[kMaxCols], vn[kMaxCols];
+  double a[C], v[C], w[C], vn[C];
 #pragma unroll
-  for (int s = 0; s < kMaxCols; ++s) {
+  for (int s = 0; s < C; ++s) {
     const int k = t + s * kThreads;
     a[s] = k < n ? A[k] : 0.0;  // row 0
   }
@@ -195,23 +212,23 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     e_out[0] = h.beta;
   }
   {
-    double acc[kMaxRows];
+    double acc[RM];
 #pragma unroll
-    for (int r = 0; r < kMaxRows; ++r) {
+    for (int r = 0; r < RM; ++r) {
       acc[r] = 0.0;
       if (r < nrows) {
 #pragma unroll
-        for (int s = 0; s < kMaxCols; ++s) {
+        for (int s = 0; s < C; ++s) {
           const int k = t + s * kThreads;
           if (k < n) acc[r] += rows[r * n + k] * v[s];
         }
       }
     }
-    block_sum<kMaxRows>(acc, red[2]);
+    block_sum<RM>(acc, red[2]);
     if (t < nrows && row0 + t >= 1) put(gp0, plane, row0 + t, h.tau * acc[t], tag_base | 1u);
     if (1 >= row0 && 1 < row0 + nrows) {
 #pragma unroll
-      for (int s = 0; s < kMaxCols; ++s) {
+      for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
         if (k >= 1 && k < n) put(gr0, plane, k, rows[(1 - row0) * n + k], tag_base | 1u);
       }
@@ -231,7 +248,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
 #pragma unroll
-      for (int s = 0; s < kMaxCols; ++s) {
+      for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
         if (k >= j + 1 && k < n) {
           const unsigned long long x0 = get(gp + k), x1 = get(gp + plane + k);
@@ -258,18 +275,20 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       __builtin_amdgcn_s_sleep(1);
     }
     if (__syncthreads_or(aborted)) return;
+    SYM_TRACE(j, 0);
     double r1[2] = {0.0, 0.0};
 #pragma unroll
-    for (int s = 0; s < kMaxCols; ++s) {
+    for (int s = 0; s < C; ++s) {
       const int k = t + s * kThreads;
       r1[0] += w[s] * v[s];
       r1[1] += k == j + 1 ? w[s] : 0.0;
     }
     block_sum<2>(r1, red[0]);
+    SYM_TRACE(j, 1);
     const double c = 0.5 * h.tau * r1[0];
     const double wj1 = r1[1] - c;  // w_j[j+1] (v_j[j+1] = 1)
 #pragma unroll
-    for (int s = 0; s < kMaxCols; ++s) {
+    for (int s = 0; s < C; ++s) {
       w[s] -= c * v[s];
       a[s] -= w[s] + wj1 * v[s];  // row j+1 <- row j+1 - v_j[j+1] w_j - w_j[j+1] v_j
       const int k = t + s * kThreads;
@@ -284,7 +303,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       // last step: row n-2 is final; the owner of row n-1 finishes its diagonal
       if (blockIdx.x == 0) {
 #pragma unroll
-        for (int s = 0; s < kMaxCols; ++s) {
+        for (int s = 0; s < C; ++s) {
           const int k = t + s * kThreads;
           if (k == n - 2) d_out[n - 2] = a[s];
           if (k == n - 1) e_out[n - 2] = a[s];
@@ -294,7 +313,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       const int r = (n - 1) - row0;
       if (r >= 0 && r < nrows) {
 #pragma unroll
-        for (int s = 0; s < kMaxCols; ++s) {
+        for (int s = 0; s < C; ++s) {
           const int k = t + s * kThreads;
           if (k == n - 1) d_out[n - 1] = rows[r * n + k] - 2.0 * vw[0][r] * vw[1][r];
         }
@@ -305,20 +324,21 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     // ---- reflector j+1 (redundant in every workgroup)
     const Reflector hn = householder(a, j + 1, n, red[1]);  // its barrier publishes vw
     make_v(a, hn, j + 1, vn);
+    SYM_TRACE(j, 2);
     if (blockIdx.x == 0 && t == 0) {
       d_out[j + 1] = hn.diag;
       e_out[j + 1] = hn.beta;
     }
 
     // ---- one LDS pass: apply step j to the owned rows, accumulate p_{j+1}
-    double acc[kMaxRows];
+    double acc[RM];
 #pragma unroll
-    for (int r = 0; r < kMaxRows; ++r) {
+    for (int r = 0; r < RM; ++r) {
       acc[r] = 0.0;
       if (r < nrows && row0 + r >= j + 1) {
         const double vi = vw[0][r], wi = vw[1][r];
 #pragma unroll
-        for (int s = 0; s < kMaxCols; ++s) {
+        for (int s = 0; s < C; ++s) {
           const int k = t + s * kThreads;
           if (k >= j + 1 && k < n) {
             const double x = rows[r * n + k] - (vi * w[s] + wi * v[s]);
@@ -330,20 +350,23 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     }
     // the owner of row j+2 publishes the row before the p reduction (each thread re-reads
     // only the LDS words it wrote itself)
+    SYM_TRACE(j, 3);
     const unsigned tag1 = tag_base | (unsigned)(j + 2);
     const int ro = (j + 2) - row0;
     if (ro >= 0 && ro < nrows) {
 #pragma unroll
-      for (int s = 0; s < kMaxCols; ++s) {
+      for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
         if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, plane, k, rows[ro * n + k], tag1);
       }
     }
-    block_sum<kMaxRows>(acc, red[2]);
+    block_sum<RM>(acc, red[2]);
+    SYM_TRACE(j, 4);
     if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, plane, row0 + t, hn.tau * acc[t], tag1);
 #pragma unroll
-    for (int s = 0; s < kMaxCols; ++s) v[s] = vn[s];
+    for (int s = 0; s < C; ++s) v[s] = vn[s];
     h = hn;
+    SYM_TRACE(j, 5);
   }
 }
 
@@ -459,8 +482,12 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   int G = 0, R = 0;
   if (symeig_plan(a.n, &G, &R) != 0) return 1;
   const size_t lds = (size_t)R * a.n * sizeof(double);
-  if (hipFuncSetAttribute(reinterpret_cast<const void*>(&tridiag_kernel),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+  // n <= 2048 with <= 8 rows per block (the FID case) gets the 8 x 8 instance: no dead column
+  // slots or reduction lanes
+  const void* kern = (a.n <= 8 * kThreads && R <= 8)
+                         ? reinterpret_cast<const void*>(&tridiag_kernel<8, 8>)
+                         : reinterpret_cast<const void*>(&tridiag_kernel<kMaxCols, kMaxRows>);
+  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return 2;
   if (hipMemsetAsync(a.ctl, 0, kCtlBytes, stream) != hipSuccess) return 2;
   const double* A = a.a;
@@ -471,7 +498,7 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   unsigned tag_base = a.tag_base;
   unsigned* ctl = a.ctl;
   void* args[] = {&A, &n, &R, &ld, &d, &e, &gran, &tag_base, &ctl};
-  if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(&tridiag_kernel), dim3(G),
+  if (hipLaunchCooperativeKernel(kern, dim3(G),
                                  dim3(kThreads), args, lds, stream) != hipSuccess)
     return 3;
   if (n >= 1536)
