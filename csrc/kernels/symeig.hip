@@ -98,35 +98,55 @@ __device__ __forceinline__ double readlane_f64(double x, int lane) {
                           __builtin_amdgcn_readlane(__double2loint(x), lane));
 }
 
-// Wave64 sum, uniform result: DPP within each 16-lane row (quad swaps, half-row and row
-// mirrors: a few cycles per step instead of an LDS-latency ds_bpermute), then the four row
-// totals by readlane.
-__device__ __forceinline__ double wave_sum(double x) {
+// Sum of each 16-lane row of a wave, in every lane of the row: DPP quad swaps, half-row and
+// row mirrors (a few cycles per step instead of an LDS-latency ds_bpermute).
+__device__ __forceinline__ double row16_sum(double x) {
   x += dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]
   x += dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
   x += dpp_f64<0x141>(x);  // row_half_mirror
   x += dpp_f64<0x140>(x);  // row_mirror
-  return (readlane_f64(x, 15) + readlane_f64(x, 31)) + (readlane_f64(x, 47) + readlane_f64(x, 63));
+  return x;
 }
 
-// Block-wide sums of N values; every thread gets the totals.  `scratch` holds kWaves * N
-// doubles; callers rotate scratch slots so consecutive reductions need one barrier each.
+// Block-wide sums of N values: the 16 row sums of the block (4 waves x 4 rows) go to LDS
+// straight from lane 15 of each row, one barrier, then the 16 partials are added in a fixed
+// order.  `scratch` holds 16 * N doubles; callers rotate scratch slots so consecutive
+// reductions need one barrier each.  (Readlane-ing the 4 row sums of every wave first took
+// ~15% more of the column's cycles, profiles/k9b_phase_trace_r2.txt.)
 template <int N>
-__device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ void row_partials(const double (&v)[N], double* scratch) {
+  const bool tail = (threadIdx.x & 15) == 15;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    const double s = wave_sum(v[i]);
-    if (lane == 0) scratch[wave * N + i] = s;
+    const double x = row16_sum(v[i]);
+    if (tail) scratch[(threadIdx.x >> 4) * N + i] = x;
   }
   __syncthreads();
+}
+
+// every thread gets every total
+template <int N>
+__device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
+  row_partials<N>(v, scratch);
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double s = 0.0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) s += scratch[w * N + i];
+    for (int q = 0; q < 16; ++q) s += scratch[q * N + i];
     v[i] = s;
   }
+}
+
+// thread t < N gets total t (the per-row p values, published by thread t)
+template <int N>
+__device__ __forceinline__ double block_sum_own(const double (&v)[N], double* scratch) {
+  row_partials<N>(v, scratch);
+  double s = 0.0;
+  if (threadIdx.x < N) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += scratch[q * N + threadIdx.x];
+  }
+  return s;
 }
 
 struct Reflector {
@@ -137,20 +157,23 @@ struct Reflector {
 // broadcasts the diagonal a[j].  v[k] = 1 at k = j+1, a[k] * scale beyond, 0 before.
 template <int C>
 __device__ __forceinline__ Reflector householder(const double (&a)[C], int j, int n,
-                                                 double* scratch) {
-  double r[3] = {0.0, 0.0, 0.0};
+                                                 double* scratch, double* bcast) {
+  // sigma by the block reduction; alpha = a[j+1] and the diagonal a[j] are single elements,
+  // so their owner threads just store them next to the partials (the reduction's barrier
+  // publishes them)
+  double r[1] = {0.0};
 #pragma unroll
   for (int s = 0; s < C; ++s) {
     const int k = threadIdx.x + s * kThreads;
     const double x = a[s];
     r[0] += (k >= j + 2 && k < n) ? x * x : 0.0;
-    r[1] += (k == j + 1) ? x : 0.0;
-    r[2] += (k == j) ? x : 0.0;
+    if (k == j + 1) bcast[0] = x;
+    if (k == j) bcast[1] = x;
   }
-  block_sum<3>(r, scratch);
+  block_sum<1>(r, scratch);
   Reflector h;
-  const double sigma = r[0], alpha = r[1];
-  h.diag = r[2];
+  const double sigma = r[0], alpha = bcast[0];
+  h.diag = bcast[1];
   if (sigma == 0.0) {
     h.tau = 0.0;
     h.beta = alpha;
@@ -185,7 +208,8 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
                                                            double* e_out, unsigned long long* gran,
                                                            unsigned tag_base, unsigned* ctl) {
   extern __shared__ double rows[];
-  __shared__ double red[3][kWaves * RM];
+  __shared__ double red[3][16 * RM];
+  __shared__ double bc[2][4];  // single-element broadcasts riding on the reductions' barriers
   __shared__ double vw[2][RM];
   const int64_t plane = (int64_t)(n - 2) * ld;
   unsigned long long* const gp0 = gran;              // p planes
@@ -205,7 +229,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
   __syncthreads();
 
   // ---- phase 0: reflector 0 and p_0 from the original rows
-  Reflector h = householder(a, 0, n, red[0]);
+  Reflector h = householder(a, 0, n, red[0], bc[0]);
   make_v(a, h, 0, v);
   if (blockIdx.x == 0 && t == 0) {
     d_out[0] = h.diag;
@@ -224,8 +248,8 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
         }
       }
     }
-    block_sum<RM>(acc, red[2]);
-    if (t < nrows && row0 + t >= 1) put(gp0, plane, row0 + t, h.tau * acc[t], tag_base | 1u);
+    const double pt = block_sum_own<RM>(acc, red[2]);
+    if (t < nrows && row0 + t >= 1) put(gp0, plane, row0 + t, h.tau * pt, tag_base | 1u);
     if (1 >= row0 && 1 < row0 + nrows) {
 #pragma unroll
       for (int s = 0; s < C; ++s) {
@@ -276,17 +300,17 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     }
     if (__syncthreads_or(aborted)) return;
     SYM_TRACE(j, 0);
-    double r1[2] = {0.0, 0.0};
+    double r1[1] = {0.0};
 #pragma unroll
     for (int s = 0; s < C; ++s) {
       const int k = t + s * kThreads;
       r1[0] += w[s] * v[s];
-      r1[1] += k == j + 1 ? w[s] : 0.0;
+      if (k == j + 1) bc[0][2] = w[s];  // p_j[j+1], published by the reduction's barrier
     }
-    block_sum<2>(r1, red[0]);
+    block_sum<1>(r1, red[0]);
     SYM_TRACE(j, 1);
     const double c = 0.5 * h.tau * r1[0];
-    const double wj1 = r1[1] - c;  // w_j[j+1] (v_j[j+1] = 1)
+    const double wj1 = bc[0][2] - c;  // w_j[j+1] (v_j[j+1] = 1)
 #pragma unroll
     for (int s = 0; s < C; ++s) {
       w[s] -= c * v[s];
@@ -322,7 +346,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     }
 
     // ---- reflector j+1 (redundant in every workgroup)
-    const Reflector hn = householder(a, j + 1, n, red[1]);  // its barrier publishes vw
+    const Reflector hn = householder(a, j + 1, n, red[1], bc[1]);  // its barrier publishes vw
     make_v(a, hn, j + 1, vn);
     SYM_TRACE(j, 2);
     if (blockIdx.x == 0 && t == 0) {
@@ -360,9 +384,9 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
         if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, plane, k, rows[ro * n + k], tag1);
       }
     }
-    block_sum<RM>(acc, red[2]);
+    const double pt = block_sum_own<RM>(acc, red[2]);
     SYM_TRACE(j, 4);
-    if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, plane, row0 + t, hn.tau * acc[t], tag1);
+    if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, plane, row0 + t, hn.tau * pt, tag1);
 #pragma unroll
     for (int s = 0; s < C; ++s) v[s] = vn[s];
     h = hn;
