@@ -93,11 +93,6 @@ __device__ __forceinline__ double dpp_f64(double x) {
   return __hiloint2double(hi, lo);
 }
 
-__device__ __forceinline__ double readlane_f64(double x, int lane) {
-  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), lane),
-                          __builtin_amdgcn_readlane(__double2loint(x), lane));
-}
-
 // Sum of each 16-lane row of a wave, in every lane of the row: DPP quad swaps, half-row and
 // row mirrors (a few cycles per step instead of an LDS-latency ds_bpermute).
 __device__ __forceinline__ double row16_sum(double x) {
