@@ -978,6 +978,24 @@ int64_t sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) {
   return 0;
 }
 
+// K9c: one diagonal block of the blocked FP64 Cholesky (factor in place + inverse).
+void potrf_block(const Tensor& a, int64_t k0, int64_t b, const Tensor& linv, const Tensor& info) {
+  check_gpu(a, "matrix");
+  TORCH_CHECK(a.dim() == 2 && a.size(0) == a.size(1) && a.scalar_type() == at::kDouble && a.is_contiguous(),
+              "potrf_block: matrix must be a contiguous float64 [n, n]");
+  TORCH_CHECK(k0 >= 0 && b >= 1 && b <= tea::potrf_block_size() && k0 + b <= a.size(0),
+              "potrf_block: block out of range");
+  TORCH_CHECK(linv.scalar_type() == at::kDouble && linv.is_contiguous() && linv.numel() == b * b &&
+                  linv.device() == a.device(),
+              "potrf_block: linv must be a contiguous float64 [b, b]");
+  TORCH_CHECK(info.scalar_type() == at::kInt && info.numel() >= 1 && info.device() == a.device(),
+              "potrf_block: info must be int32 on the matrix's device");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(a.device());
+  check_launch(tea::launch_potrf_block(a.data_ptr<double>(), a.size(1), (int)k0, (int)b, linv.data_ptr<double>(),
+                                       info.data_ptr<int>(), stream_for(a)),
+               "potrf_block");
+}
+
 // K2: multilabel accuracy counts straight into float32 state scalars.
 void multilabel_counts(const Tensor& input, const Tensor& target, double threshold, int64_t k,
                        int64_t criteria, const Tensor& num_correct, const optional<Tensor>& num_total,
@@ -1265,6 +1283,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out_rec") = py::none());
   m.def("fid_cov_update", &fid_cov_update, "K8 FP32-MFMA symmetric rank-k covariance update",
         py::arg("act"), py::arg("cov"), py::arg("colsum"));
+  m.def("potrf_block", &potrf_block, "K9c diagonal-block FP64 Cholesky + inverse (blocked Cholesky step)",
+        py::arg("a"), py::arg("k0"), py::arg("b"), py::arg("linv"), py::arg("info"));
+  m.def("potrf_block_size", &tea::potrf_block_size, "K9c block size");
   m.def("sym_eigvals", &sym_eigvals, "K9b eigenvalues of a symmetric float64 matrix (LDS-resident Householder + multisection)",
         py::arg("m"), py::arg("lam"), py::arg("status"));
   tea_register_runtime(m);

@@ -466,3 +466,11 @@ int64_t symeig_slot_stride(int64_t n);
 int launch_symeig(const SymEigArgs& a, hipStream_t stream);
 
 }  // namespace tea
+
+namespace tea {
+// K9c: factor the b x b diagonal block A[k0:k0+b, k0:k0+b] (row-major, leading dimension lda)
+// in place into its lower Cholesky factor (upper part zeroed) and write its inverse to Linv
+// [b, b]; a non-positive pivot sets *info = k0 + column + 1 (if still 0).  b <= 64.
+int potrf_block_size();
+int launch_potrf_block(double* A, int64_t lda, int k0, int b, double* Linv, int* info, hipStream_t stream);
+}  // namespace tea

@@ -528,3 +528,110 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
 }
 
 }  // namespace tea
+
+// ------------------------------------------------------------------------------------------
+// K9c: diagonal-block Cholesky + triangular inverse for the blocked FP64 Cholesky of FID's
+// covariance (metrics/image/fid.py).  rocSOLVER's potrf at D = 2048 spent ~2.7 ms in 17
+// potf2 launches (~160 us each) and ~1.7 ms in its forward-substitution trsm
+// (profiles/rocprof_k9b_symeig_r2.csv); here one workgroup factors a b x b (b <= 64) diagonal
+// block in LDS (potf2, LAPACK semantics: a non-positive pivot records info = column + 1 and
+// stops) and inverts the factor in LDS, so the panel below becomes one GEMM with the inverse
+// and the trailing update one GEMM (rocBLAS/hipBLASLt FP64 MFMA) - no trsm, no small-kernel
+// chains.
+namespace tea {
+namespace {
+
+constexpr int kPotrfB = 64;
+
+__global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda, int k0, int b,
+                                                          double* Linv, int* info) {
+  __shared__ double L[kPotrfB][kPotrfB + 1];
+  __shared__ double X[kPotrfB][kPotrfB + 1];
+  __shared__ double part[4][kPotrfB];
+  __shared__ int s_bad;
+  const int t = threadIdx.x;
+  // 16 x 16 thread grid over the block: thread (ti, tj) owns rows ti + 16 x, columns tj + 16 y
+  const int ti = t >> 4, tj = t & 15;
+  double* blk = A + (int64_t)k0 * lda + k0;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int i = ti + 16 * x, j = tj + 16 * y;
+      if (i < b && j < b) L[i][j] = j <= i ? blk[(int64_t)i * lda + j] : 0.0;
+    }
+  if (t == 0) s_bad = 0;
+  __syncthreads();
+  // right-looking potf2 on the lower triangle: per column one sqrt, one scaled column, one
+  // rank-1 update of the trailing triangle (16 elements per thread, no index division)
+  for (int j = 0; j < b; ++j) {
+    const double d = L[j][j];
+    if (!(d > 0.0)) {  // not positive definite (or NaN): LAPACK info, then stop
+      if (t == 0) {
+        s_bad = 1;
+        if (*info == 0) *info = k0 + j + 1;
+      }
+      break;
+    }
+    const double rp = 1.0 / sqrt(d);
+    __syncthreads();  // everyone has read L[j][j]
+    if (t < b && t >= j) L[t][j] = t == j ? d * rp : L[t][j] * rp;
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < 4; ++x) {
+      const int i = ti + 16 * x;
+      if (i > j && i < b) {
+        const double lij = L[i][j];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) {
+          const int k = tj + 16 * y;
+          if (k > j && k <= i) L[i][k] -= lij * L[k][j];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  const bool bad = s_bad != 0;
+  // X = L^{-1} (lower), one row per step: thread (c = t & 63, q = t >> 6) adds the k = q mod 4
+  // part of sum_{c <= k < i} L[i][k] X[k][c]; the four parts are combined by thread q = 0
+  if (!bad) {
+    const int c = t & 63, q = t >> 6;
+    for (int i = 0; i < b; ++i) {
+      double sp = 0.0;
+      if (c < i) {
+        for (int k = c + ((q - c) & 3); k < i; k += 4) sp += L[i][k] * X[k][c];
+      }
+      part[q][c] = sp;
+      __syncthreads();
+      if (q == 0 && c < b) {
+        const double sum = (part[0][c] + part[1][c]) + (part[2][c] + part[3][c]);
+        X[i][c] = c > i ? 0.0 : ((c == i ? 1.0 : 0.0) - sum) / L[i][i];
+      }
+      __syncthreads();
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) {
+      const int i = ti + 16 * x, j = tj + 16 * y;
+      if (i < b && j < b) {
+        blk[(int64_t)i * lda + j] = j <= i ? L[i][j] : 0.0;
+        Linv[(int64_t)i * b + j] = bad ? 0.0 : X[i][j];
+      }
+    }
+}
+
+}  // namespace
+
+int potrf_block_size() { return kPotrfB; }
+
+int launch_potrf_block(double* A, int64_t lda, int k0, int b, double* Linv, int* info,
+                       hipStream_t stream) {
+  if (b < 1 || b > kPotrfB) return 1;
+  potrf_block_kernel<<<1, 256, 0, stream>>>(A, lda, k0, b, Linv, info);
+  return hipGetLastError() == hipSuccess ? 0 : 2;
+}
+
+}  // namespace tea

@@ -99,3 +99,28 @@ def test_fallback_sizes():
     for n in (1, 2, 2600):
         m = _spd(n, 5).to(DEV)
         torch.testing.assert_close(sym_eigvalsh(m).cpu(), torch.linalg.eigvalsh(m.cpu()), rtol=0, atol=1e-9)
+
+
+# ----------------------------------------------------------------------------- K9c
+@pytest.mark.parametrize("n", [2, 3, 63, 64, 65, 200, 1000, 2048])
+def test_blocked_cholesky_matches_cpu(n):
+    from torcheval_amd.metrics.image.fid import cholesky_ex
+
+    m = _spd(n, 100 + n)
+    L, info = cholesky_ex(m.to(DEV))
+    assert int(info) == 0
+    ref = torch.linalg.cholesky(m)
+    torch.testing.assert_close(L.cpu(), ref, rtol=1e-10, atol=1e-10 * float(ref.abs().max()))
+    assert torch.equal(L.cpu().triu(1), torch.zeros(n, n, dtype=torch.float64))
+
+
+@pytest.mark.parametrize("n,bad", [(50, 10), (300, 0), (300, 150), (2048, 2000)])
+def test_blocked_cholesky_reports_non_pd(n, bad):
+    from torcheval_amd.metrics.image.fid import cholesky_ex
+
+    m = _spd(n, 7)
+    m[bad, bad] = -1.0  # a leading minor of order bad + 1 is indefinite
+    _, info = cholesky_ex(m.to(DEV))
+    _, ref_info = torch.linalg.cholesky_ex(m)
+    assert int(info) != 0 and int(ref_info) != 0
+    assert int(info) <= bad + 1

@@ -65,10 +65,10 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
     sums carry rounding "noise" eigenvalues well above it, and the reference's
     ``eigvals(S1 S2)`` includes their square roots too, so they are kept (r is then the FP64
     numerical rank, usually above the sample rank - the r x r saving shrinks accordingly)."""
-    L, info = torch.linalg.cholesky_ex(s1)
+    L, info = cholesky_ex(s1)
     if int(info) == 0:
         m = L.T @ s2 @ L
-    elif int((L2 := torch.linalg.cholesky_ex(s2))[1]) == 0:
+    elif int((L2 := cholesky_ex(s2))[1]) == 0:
         # S1 singular, S2 not: S1 S2 and S2 S1 share their spectrum, so factor S2 instead
         # (one more Cholesky rather than a full eigh with eigenvectors)
         m = L2[0].T @ s1 @ L2[0]
@@ -81,6 +81,35 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
         m = w.T @ s2 @ w
     ev = sym_eigvalsh((m + m.T) / 2)
     return ev.clamp(min=0).sqrt().sum()
+
+
+def cholesky_ex(s: Tensor) -> "tuple[Tensor, Tensor]":
+    """Lower Cholesky factor of a symmetric FP64 matrix and an int ``info`` (0 = success, as
+    ``torch.linalg.cholesky_ex``).
+
+    On ROCm, blocked right-looking with K9c (``csrc/kernels/symeig.hip``): one workgroup
+    factors each 64 x 64 diagonal block in LDS and inverts it, the panel below is one GEMM with
+    that inverse and the trailing update one GEMM - instead of rocSOLVER's chain of ~160 us
+    potf2 launches and its forward-substitution trsm."""
+    n = s.shape[0]
+    if use_native(s) and s.dtype == torch.float64 and s.dim() == 2 and n >= 2:
+        from torcheval_amd.ops import native
+
+        b = native().potrf_block_size()
+        a = s.contiguous().clone()
+        info = torch.zeros(1, dtype=torch.int32, device=s.device)
+        for k0 in range(0, n, b):
+            bb = min(b, n - k0)
+            linv = torch.empty(bb, bb, dtype=torch.float64, device=s.device)
+            native().potrf_block(a, k0, bb, linv, info)
+            k1 = k0 + bb
+            if k1 < n:
+                l21 = a[k1:, k0:k1] @ linv.T
+                a[k1:, k0:k1] = l21
+                a[k0:k1, k1:] = 0.0
+                a[k1:, k1:].addmm_(l21, l21.T, alpha=-1.0)
+        return a, info[0]
+    return torch.linalg.cholesky_ex(s)
 
 
 def sym_eigvalsh(m: Tensor) -> Tensor:
