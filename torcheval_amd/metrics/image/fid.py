@@ -98,17 +98,17 @@ def cholesky_ex(s: Tensor) -> "tuple[Tensor, Tensor]":
         b = native().potrf_block_size()
         a = s.contiguous().clone()
         info = torch.zeros(1, dtype=torch.int32, device=s.device)
+        linv_full = torch.empty(b * b, dtype=torch.float64, device=s.device)  # reused (stream order)
         for k0 in range(0, n, b):
             bb = min(b, n - k0)
-            linv = torch.empty(bb, bb, dtype=torch.float64, device=s.device)
+            linv = linv_full[: bb * bb].view(bb, bb)
             native().potrf_block(a, k0, bb, linv, info)
             k1 = k0 + bb
             if k1 < n:
                 l21 = a[k1:, k0:k1] @ linv.T
                 a[k1:, k0:k1] = l21
-                a[k0:k1, k1:] = 0.0
                 a[k1:, k1:].addmm_(l21, l21.T, alpha=-1.0)
-        return a, info[0]
+        return a.tril_(), info[0]
     return torch.linalg.cholesky_ex(s)
 
 
