@@ -1208,6 +1208,40 @@ void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>&
   check_launch(tea::launch_binned_finalize(a, stream_for(tp)), "binned_finalize");
 }
 
+
+// ---------------------------------------------------------------- C3 gathered-state reduction
+void seg_reduce_rows(const Tensor& rows, const Tensor& out, int64_t ws, at::IntArrayRef offs,
+                     at::IntArrayRef counts, at::IntArrayRef dtypes, at::IntArrayRef ops) {
+  check_gpu(rows, "rows");
+  TORCH_CHECK(rows.scalar_type() == at::kByte && out.scalar_type() == at::kByte && rows.is_contiguous() &&
+                  out.is_contiguous() && out.device() == rows.device(),
+              "seg_reduce_rows: contiguous uint8 rows / out on one device expected");
+  const int64_t nseg = static_cast<int64_t>(offs.size());
+  TORCH_CHECK(nseg >= 1 && nseg <= tea::kSegMax && counts.size() == offs.size() && dtypes.size() == offs.size() &&
+                  ops.size() == offs.size(),
+              "seg_reduce_rows: 1..", tea::kSegMax, " segments with offs / counts / dtypes / ops each");
+  TORCH_CHECK(ws >= 1 && rows.numel() == ws * out.numel(), "seg_reduce_rows: rows must be [ws * row_bytes]");
+  static const int esize[] = {4, 2, 2, 8, 8, 4, 1, 1, 1, 2};  // by tea::DType
+  tea::SegReduceArgs a;
+  a.rows = rows.data_ptr<uint8_t>();
+  a.out = out.data_ptr<uint8_t>();
+  a.ws = static_cast<int>(ws);
+  a.row_bytes = out.numel();
+  a.nseg = static_cast<int>(nseg);
+  for (int64_t s = 0; s < nseg; ++s) {
+    TORCH_CHECK(dtypes[s] >= 0 && dtypes[s] <= 9 && ops[s] >= 0 && ops[s] <= 2 && counts[s] >= 0,
+                "seg_reduce_rows: bad segment ", s);
+    const int es = esize[dtypes[s]];
+    TORCH_CHECK(offs[s] >= 0 && offs[s] % es == 0 && offs[s] + counts[s] * es <= a.row_bytes,
+                "seg_reduce_rows: segment ", s, " outside the row or misaligned");
+    a.off[s] = offs[s];
+    a.first[s + 1] = a.first[s] + counts[s];
+    a.dtype[s] = static_cast<int>(dtypes[s]);
+    a.op[s] = static_cast<int>(ops[s]);
+  }
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(rows.device());
+  check_launch(tea::launch_seg_reduce(a, stream_for(rows)), "seg_reduce_rows");
+}
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -1215,6 +1249,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("ARCH") = "gfx950";
   m.def("rank_scores", &rank_scores, "K10 rank-of-target scores (hit rate / reciprocal rank)",
         py::arg("input"), py::arg("target"), py::arg("mode"), py::arg("k"), py::arg("err") = py::none());
+  m.def("seg_reduce_rows", &seg_reduce_rows,
+        "C3 reduce a gathered [ws][row] state buffer per (op, dtype) segment in one launch", py::arg("rows"),
+        py::arg("out"), py::arg("ws"), py::arg("offs"), py::arg("counts"), py::arg("dtypes"), py::arg("ops"));
   m.def("micro_accuracy_update", &micro_accuracy_update,
         "K1 micro accuracy (k=1) accumulated into float32 scalar states; false = not handled");
   m.def("cls_counts", &cls_counts, "K1 fused classification counts", py::arg("input"),

@@ -474,3 +474,21 @@ namespace tea {
 int potrf_block_size();
 int launch_potrf_block(double* A, int64_t lda, int k0, int b, double* Linv, int* info, hipStream_t stream);
 }  // namespace tea
+
+namespace tea {
+// C3: reduce a gathered [ws][row_bytes] metric-state buffer segment by segment across ranks
+// (rank 0 first) into ``out`` (same byte layout).  op: 0 sum, 1 max, 2 min; dtype: DType.
+constexpr int kSegMax = 32;
+struct SegReduceArgs {
+  const uint8_t* rows = nullptr;
+  uint8_t* out = nullptr;
+  int ws = 1;
+  int64_t row_bytes = 0;
+  int nseg = 0;
+  int64_t off[kSegMax] = {};        // byte offset of each segment in a row
+  int64_t first[kSegMax + 1] = {};  // prefix sum of segment element counts
+  int dtype[kSegMax] = {};
+  int op[kSegMax] = {};
+};
+int launch_seg_reduce(const SegReduceArgs& a, hipStream_t stream);
+}  // namespace tea

@@ -70,32 +70,40 @@ def test_error_flags_raise_on_every_rank(ws):
 
 
 def _fast_vs_general_job(rank, ws):
-    from torcheval_amd.metrics import Max, Mean, MulticlassAccuracy, MulticlassPrecision
-    from torcheval_amd.parallel import state_sync
+    from torcheval_amd.metrics import Max, Mean, MulticlassAccuracy, MulticlassConfusionMatrix, MulticlassPrecision
+    from torcheval_amd.parallel import state_buffer, state_sync
 
     g = torch.Generator().manual_seed(10 + rank)
     coll = {
         "acc": MulticlassAccuracy(num_classes=5, average="macro").update(torch.randn(40, 5, generator=g),
                                                                        torch.randint(0, 5, (40,), generator=g)),
+        "micro": MulticlassAccuracy().update(torch.randn(40, 5, generator=g), torch.randint(0, 5, (40,), generator=g)),
         "prec": MulticlassPrecision(num_classes=5, average=None).update(torch.randn(40, 5, generator=g),
                                                                       torch.randint(0, 5, (40,), generator=g)),
         "mean": Mean().update(torch.randn(17, generator=g)),
         "max": Max().update(torch.randn(9, generator=g)),
+        # 200 x 200 f32 = 160 KB: a "reduce group" (snapshot + all_reduce), integer counts
+        "cm": MulticlassConfusionMatrix(200).update(torch.randn(3000, 200, generator=g),
+                                                    torch.randint(0, 200, (3000,), generator=g)),
     }
-    fast = state_sync._fast_small_sync(coll, None, ws)
-    assert fast is not None
-    again = state_sync._fast_small_sync(coll, None, ws)  # cached plan
     general = state_sync.start_sync_collection(coll, None, ws, snapshot=False, blocking=True).finish()
+    fast = state_buffer.fast_sync(coll, None, ws)
+    assert fast is not None
+    assert state_buffer.plan_summary(coll["cm"])["reduce_groups"], "the 160 KB state must be all-reduced"
+    again = state_buffer.fast_sync(coll, None, ws)  # cached layout, live views
+    single = state_buffer.fast_sync({"m": coll["micro"]}, None, ws)["m"]
     out = []
     for key in coll:
         for name in coll[key]._state_merge_kinds():
             a, b, c = getattr(fast[key], name), getattr(again[key], name), getattr(general[key], name)
             assert torch.equal(a, b) and torch.equal(a, c), (key, name)
+            assert a.data_ptr() != getattr(coll[key], name).data_ptr()  # merged copies, inputs untouched
         out.append(float(fast[key].compute().float().sum()))
+    assert torch.equal(single.num_correct, fast["micro"].num_correct)
     return out
 
 
-@pytest.mark.parametrize("ws", [2, 3])
-def test_fast_small_sync_matches_general_path(ws):
+@pytest.mark.parametrize("ws", [2, 4])
+def test_state_buffer_sync_matches_general_path(ws):
     res = run_distributed(_fast_vs_general_job, ws)
     assert all(r == res[0] for r in res), res  # bit-identical on every rank

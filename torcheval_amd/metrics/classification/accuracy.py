@@ -92,7 +92,11 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         self._add_state("num_total", torch.zeros(shape, device=self.device), merge="sum")
         self._refresh_fast_path()
 
-    _err_words = 1  # K1's device flag: one int32 code
+    @property
+    def _err_words(self) -> int:
+        # K1's device flag (one int32 code) exists only where the update validates labels:
+        # micro k=1 never creates one, so its sync carries no flag slot and compute() no read
+        return 0 if self.average == "micro" and self.k == 1 else 1
 
     def _refresh_fast_path(self) -> None:
         # north-star fast path (ROCm states, micro, k=1): ONE native call that tests every

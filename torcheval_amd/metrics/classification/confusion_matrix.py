@@ -34,6 +34,8 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
     Functional version: ``multiclass_confusion_matrix``.
     """
 
+    _err_words = 3  # [flags, max bad target, max bad prediction]
+
     def __init__(
         self: TMulticlassConfusionMatrix,
         num_classes: int,
@@ -106,6 +108,8 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
 
 class BinaryConfusionMatrix(MulticlassConfusionMatrix):
     """2x2 confusion matrix of thresholded ``input``.  Functional: ``binary_confusion_matrix``."""
+
+    _err_words = 0  # ATen update: no device flag
 
     def __init__(
         self: TBinaryConfusionMatrix,

@@ -24,6 +24,8 @@ class MulticlassF1Score(Metric[torch.Tensor]):
     weighted | None.  Functional version: ``multiclass_f1_score``.
     """
 
+    _err_words = 1  # K1 device flag: one int32 code
+
     def __init__(
         self: TF1Score,
         *,
@@ -84,6 +86,8 @@ class MulticlassF1Score(Metric[torch.Tensor]):
 
 class BinaryF1Score(MulticlassF1Score):
     """F1 of thresholded ``input``.  Functional version: ``binary_f1_score``."""
+
+    _err_words = 0  # ATen update: no device flag
 
     def __init__(self: TBinaryF1Score, *, threshold: float = 0.5, device: Optional[torch.device] = None) -> None:
         super().__init__(average="micro", device=device)

@@ -31,6 +31,8 @@ class MulticlassPrecision(Metric[torch.Tensor]):
     Functional version: ``torcheval_amd.metrics.functional.multiclass_precision``.
     """
 
+    _err_words = 1  # K1 device flag: one int32 code
+
     def __init__(
         self: TPrecision,
         *,
@@ -90,6 +92,8 @@ class MulticlassPrecision(Metric[torch.Tensor]):
 class BinaryPrecision(MulticlassPrecision):
     """Precision of thresholded ``input`` (``input >= threshold`` is positive).
     Functional version: ``torcheval_amd.metrics.functional.binary_precision``."""
+
+    _err_words = 0  # ATen update: no device flag
 
     def __init__(
         self: TBinaryPrecision,

@@ -65,6 +65,8 @@ class MulticlassRecall(Metric[torch.Tensor]):
     None.  Functional version: ``multiclass_recall``.
     """
 
+    _err_words = 1  # K1 device flag: one int32 code
+
     def __init__(
         self: TRecall,
         *,

@@ -13,6 +13,9 @@ MI355X-first differences (documented decisions):
   reference's pickled ``all_gather_object`` of whole metric objects.  States that declare
   nothing are still synced correctly: their tensors travel through a device-resident
   all-gather-v and the metric's own ``merge_state`` is called, exactly as in the reference.
+* additive / extremal tensor states live as views into ONE contiguous device buffer per metric
+  (``torcheval_amd.parallel.state_buffer``), so ``sync_and_compute`` sends
+  one bucket and ``reset()`` is one copy.
 * ``reset()`` also restores ``int`` / ``float`` states (the reference leaves them stale,
   metric.py:126-146).
 * dict states use a picklable zero-tensor factory instead of a lambda, so every metric is
@@ -116,6 +119,9 @@ class Metric(Generic[TComputeReturn], ABC):
         self._state_name_to_default: Dict[str, TState] = {}
         self._state_merge_kind: Dict[str, Optional[str]] = {}
         self._device: torch.device = _as_device(device)
+        # contiguous device buffer of the sum / max / min states (built lazily by the sync
+        # engine, torcheval_amd.parallel.state_buffer); None until then
+        self._tea_sb = None
 
     # ------------------------------------------------------------------ state registry
     def _add_state(
@@ -171,6 +177,9 @@ class Metric(Generic[TComputeReturn], ABC):
         Reset the metric state variables to their default value.  Tensors in the default
         values are moved to the device of the last ``self.to(device)`` call.
         """
+        sb = getattr(self, "_tea_sb", None)
+        if sb is not None and sb.valid(self) and sb.device == self.device and sb.reset():
+            return self  # one copy of the default image into the state buffer (views kept)
         device = self.device
         for state_name, default in self._state_name_to_default.items():
             if isinstance(default, torch.Tensor):

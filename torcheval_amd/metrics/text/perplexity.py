@@ -14,6 +14,7 @@ class Perplexity(_SumStates):
     """Perplexity of token logits (fused K7 kernel on ROCm; label check deferred to compute)."""
 
     _names = ("sum_log_probs", "num_total")
+    _err_words = 1  # K7 device flag: one int32 code
 
     def __init__(self, ignore_index: Optional[int] = None, device: Optional[torch.device] = None) -> None:
         super().__init__(device=device)

@@ -1,0 +1,397 @@
+"""Contiguous per-metric state buffers and the one-collective state sync.
+
+A metric whose states are all ``sum`` / ``max`` / ``min`` tensors (counters, per-class
+vectors, confusion matrices, covariance sums) keeps them as views into ONE device buffer:
+
+    [ reduce groups | gather region: small groups ... | error-flag slot ]
+
+* every (op, dtype) group is contiguous, so a group is one RCCL operand;
+* groups larger than ``SMALL_STATE_BYTES`` ("reduce groups", e.g. a 4 MB confusion matrix)
+  are all-reduced from a snapshot copy (O(|state|) bytes per rank);
+* everything else - the small groups and the metric's device error flag - is the "gather
+  region": ONE ``all_gather_into_tensor`` of its raw bytes, then ONE fused kernel
+  (``_C.seg_reduce_rows``, csrc/kernels/sync_reduce.hip) reduces every segment over the
+  ranks in rank order, so every rank ends with bit-identical states.
+
+``sync_and_compute(MulticlassAccuracy)`` is therefore one collective on the live buffer (no
+packing ``cat``, no per-state loops: the plan is cached on the buffer) plus, at ws > 1, one
+reduction launch.  Update kernels keep writing the same views (the K1 fast path passes
+``num_correct`` / ``num_total`` pointers into the buffer).
+
+The buffer is built lazily (first sync or reset of an eligible metric).  Any rebinding of a
+state attribute (``load_state_dict``, ``to()``, a metric that assigns instead of updating in
+place) is detected by a data-pointer check before each use and the buffer is rebuilt, so the
+layout is an optimisation only, never a correctness assumption.
+
+Replaces reference torcheval/metrics/toolkit.py:371-391 (``all_gather_object`` of the whole
+pickled metric, then ``merge_state`` on every rank).
+"""
+
+import copy
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from torcheval_amd.parallel import collectives
+from torcheval_amd.parallel.distributed import backend_of
+
+# Groups up to this size (summed over the gather region) ride the single all-gather.
+SMALL_STATE_BYTES = 64 << 10
+_ALIGN = 16
+_FLAG_BYTES = 32  # [8] int32 slot for the metric's device error flag (<= 7 words)
+
+_DT_CODE = {
+    torch.float32: 0, torch.float16: 1, torch.bfloat16: 2, torch.float64: 3, torch.int64: 4,
+    torch.int32: 5, torch.uint8: 6, torch.bool: 7, torch.int8: 8, torch.int16: 9,
+}
+_OP_CODE = {"sum": 0, "max": 1, "min": 2}
+_RCCL_OP = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}
+
+
+def _pad(n: int) -> int:
+    return (n + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+def _esize(dtype: torch.dtype) -> int:
+    return torch.empty((), dtype=dtype).element_size()
+
+
+class _Group:
+    """One (op, dtype) run of states inside the buffer."""
+
+    __slots__ = ("op", "dtype", "off", "nbytes", "members")
+
+    def __init__(self, op: str, dtype: torch.dtype) -> None:
+        self.op = op
+        self.dtype = dtype
+        self.off = 0
+        self.nbytes = 0
+        self.members: List[Tuple[str, Tuple[int, ...], int, int]] = []  # name, shape, byte off, numel
+
+
+def _flag_words(metric) -> Optional[int]:
+    """Words of the metric's device error flag slot: 0 = no flag, None = not representable."""
+    if not hasattr(metric, "_err"):
+        return 0
+    words = getattr(metric, "_err_words", None)
+    if words == 0:
+        return 0
+    if not isinstance(words, int) or words < 0 or words >= _FLAG_BYTES // 4:
+        return None
+    if getattr(metric, "_err_merge", "max") != "max":
+        return None
+    return words
+
+
+def _eligible_states(metric) -> Optional[List[Tuple[str, str, torch.Tensor]]]:
+    kinds = metric._state_merge_kinds()
+    if not kinds:
+        return None
+    out = []
+    dev = None
+    for name, kind in kinds.items():
+        if kind not in _OP_CODE:
+            return None
+        v = getattr(metric, name, None)
+        if not isinstance(v, torch.Tensor) or v.dtype not in _DT_CODE or v.is_sparse:
+            return None
+        if dev is None:
+            dev = v.device
+        elif v.device != dev:
+            return None
+        out.append((name, kind, v))
+    return out
+
+
+class StateBuffer:
+    """The contiguous state buffer of one metric plus its cached sync plans."""
+
+    __slots__ = ("buf", "device", "groups", "reduce_end", "gather_off", "gather_bytes", "flag_off",
+                 "flag_words", "names", "ptrs", "err_obj", "default_img", "nbytes", "_seg_cache")
+
+    # ---------------------------------------------------------------- construction
+    @classmethod
+    def build(cls, metric) -> Optional["StateBuffer"]:
+        states = _eligible_states(metric)
+        words = _flag_words(metric)
+        if states is None or words is None:
+            return None
+        err = getattr(metric, "_err", None) if words else None
+        dev = states[0][2].device
+        if err is not None and (not isinstance(err, torch.Tensor) or err.dtype != torch.int32
+                                or err.numel() != words or err.device != dev):
+            return None
+        self = cls.__new__(cls)
+        self.device = dev
+        groups: Dict[Tuple[str, torch.dtype], _Group] = {}
+        for name, kind, v in states:
+            g = groups.get((kind, v.dtype))
+            if g is None:
+                g = groups[(kind, v.dtype)] = _Group(kind, v.dtype)
+            g.members.append((name, tuple(v.shape), g.nbytes, v.numel()))
+            g.nbytes += v.numel() * v.element_size()
+        # the smallest groups go to the gather region while they fit the budget
+        ordered = sorted(groups.values(), key=lambda g: (g.nbytes, g.op, str(g.dtype)))
+        budget, small, large = 0, [], []
+        for g in ordered:
+            if budget + g.nbytes <= SMALL_STATE_BYTES:
+                small.append(g)
+                budget += g.nbytes
+            else:
+                large.append(g)
+        off = 0
+        for g in large:
+            g.off = off
+            off += _pad(g.nbytes)
+        self.reduce_end = off
+        self.gather_off = off
+        for g in small:
+            g.off = off
+            off += _pad(g.nbytes)
+        self.flag_words = words
+        self.flag_off = off if words else -1
+        if words:
+            off += _FLAG_BYTES
+        self.gather_bytes = off - self.gather_off
+        self.nbytes = off
+        self.groups = large + small
+        with torch.inference_mode(False):
+            self.buf = torch.zeros(max(self.nbytes, _ALIGN), dtype=torch.uint8, device=dev)
+            views = self.views(self.buf)
+            for name, _, v in states:
+                views[name].copy_(v)
+            self.default_img = self._default_image(metric, states)
+        for name, _, _ in states:
+            setattr(metric, name, views[name])
+        self.names = tuple(n for n, _, _ in states)
+        if words and err is not None:
+            slot = self.flag_view(self.buf)
+            slot.copy_(err)
+            metric._err = slot
+        self.err_obj = getattr(metric, "_err", None) if words else None
+        self.ptrs = tuple(getattr(metric, n).data_ptr() for n in self.names)
+        self._seg_cache = None
+        metric._tea_sb = self
+        return self
+
+    def _default_image(self, metric, states) -> Optional[torch.Tensor]:
+        """The state region holding every state's default (one copy resets the metric)."""
+        defaults = metric._state_name_to_default
+        img = torch.zeros(max(self.flag_off if self.flag_words else self.nbytes, _ALIGN),
+                          dtype=torch.uint8, device=self.device)
+        views = self.views(img)
+        for name, _, v in states:
+            d = defaults.get(name)
+            if not isinstance(d, torch.Tensor) or d.dtype != v.dtype or tuple(d.shape) != tuple(v.shape):
+                return None  # lazily shaped states (MSE / R2): reset() takes the generic path
+            views[name].copy_(d)
+        return img
+
+    @staticmethod
+    def _dead() -> "StateBuffer":
+        self = StateBuffer.__new__(StateBuffer)
+        self.buf = None
+        return self
+
+    def __reduce__(self):
+        # pickled / deep-copied metrics rebuild their buffer on first use
+        return (StateBuffer._dead, ())
+
+    def __deepcopy__(self, memo):
+        return StateBuffer._dead()
+
+    # ---------------------------------------------------------------- layout views
+    def views(self, buf: torch.Tensor) -> Dict[str, torch.Tensor]:
+        out = {}
+        for g in self.groups:
+            for name, shape, boff, n in g.members:
+                o = g.off + boff
+                out[name] = buf[o : o + n * _esize(g.dtype)].view(g.dtype).view(shape)
+        return out
+
+    def flag_view(self, buf: torch.Tensor) -> torch.Tensor:
+        return buf[self.flag_off : self.flag_off + 4 * self.flag_words].view(torch.int32)
+
+    def valid(self, metric) -> bool:
+        if self.buf is None:
+            return False
+        if self.flag_words and getattr(metric, "_err", None) is not self.err_obj:
+            return False
+        try:
+            return tuple(getattr(metric, n).data_ptr() for n in self.names) == self.ptrs
+        except AttributeError:
+            return False
+
+    def segments(self, base: int = 0) -> Tuple[List[int], List[int], List[int], List[int]]:
+        """(byte offsets relative to the gather region + base, counts, dtype codes, op codes)."""
+        if self._seg_cache is None:
+            offs, counts, dts, ops = [], [], [], []
+            for g in self.groups:
+                if g.off < self.gather_off:
+                    continue
+                offs.append(g.off - self.gather_off)
+                counts.append(g.nbytes // _esize(g.dtype))
+                dts.append(_DT_CODE[g.dtype])
+                ops.append(_OP_CODE[g.op])
+            if self.flag_words:
+                offs.append(self.flag_off - self.gather_off)
+                counts.append(self.flag_words)
+                dts.append(_DT_CODE[torch.int32])
+                ops.append(_OP_CODE["max"])
+            self._seg_cache = (offs, counts, dts, ops)
+        offs, counts, dts, ops = self._seg_cache
+        return [o + base for o in offs], counts, dts, ops
+
+    # ---------------------------------------------------------------- reset
+    def reset(self) -> bool:
+        """Restore every state's default with ONE copy (views and kernel pointers kept)."""
+        if self.default_img is None:
+            return False
+        self.buf[: self.default_img.numel()].copy_(self.default_img)
+        return True
+
+
+def buffer_of(metric, build: bool = True) -> Optional[StateBuffer]:
+    """The metric's valid state buffer (rebuilt if a state was rebound), or None if the
+    metric's states cannot live in one (cat / untyped states, variable-size error flags)."""
+    sb = getattr(metric, "_tea_sb", None)
+    if sb is not None and sb.valid(metric):
+        return sb
+    if not build:
+        return None
+    metric._prepare_for_merge_state()
+    return StateBuffer.build(metric)
+
+
+# -------------------------------------------------------------------- reductions
+def _reduce_rows_torch(rows: torch.Tensor, out: torch.Tensor, segs, ws: int) -> None:
+    """ATen form of the fused kernel (CPU / gloo path): one reduction per segment."""
+    offs, counts, dts, ops = segs
+    inv = {v: k for k, v in _DT_CODE.items()}
+    for o, n, d, op in zip(offs, counts, dts, ops):
+        dtype = inv[d]
+        nb = n * _esize(dtype)
+        seg = rows[:, o : o + nb].view(dtype)
+        if dtype == torch.bool:
+            red = seg.amin(0) if op == 2 else seg.amax(0)
+        elif op == 0:
+            red = seg.sum(0, dtype=dtype)
+        else:
+            red = seg.amax(0) if op == 1 else seg.amin(0)
+        out[o : o + nb].view(dtype).copy_(red)
+
+
+def _reduce_gathered(rows: torch.Tensor, segs, ws: int, row_bytes: int) -> torch.Tensor:
+    out = torch.empty(row_bytes, dtype=torch.uint8, device=rows.device)
+    if rows.is_cuda and len(segs[0]) <= 32:
+        from torcheval_amd.ops import native
+
+        native().seg_reduce_rows(rows.reshape(-1), out, ws, *segs)
+    else:
+        _reduce_rows_torch(rows.view(ws, row_bytes), out, segs, ws)
+    return out
+
+
+def _all_reduce_group(t: torch.Tensor, op: str, group) -> None:
+    if t.dtype == torch.bool:  # logical or / and through uint8 max / min
+        t = t.view(torch.uint8)
+        op = "min" if op == "min" else "max"
+    work = dist.all_reduce(t, op=_RCCL_OP[op], group=group, async_op=collectives._issue_async(True))
+    if work is not None:
+        collectives._wait(work)
+
+
+# -------------------------------------------------------------------- the sync
+def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
+    """Blocking sync of a collection whose metrics all keep their states in a StateBuffer.
+
+    Returns ``{key: merged metric}`` (new shallow copies; the inputs are untouched) or None
+    when some metric is not eligible (the caller then runs the generic engine).  Every rank
+    must pass the same collection (same keys, types and state shapes)."""
+    sbs = []
+    for m in metrics.values():
+        sb = buffer_of(m)
+        if sb is None:
+            return None
+        sbs.append(sb)
+    dev = sbs[0].device
+    if any(sb.device != dev for sb in sbs):
+        return None
+    nccl = backend_of(group) == "nccl"
+    if nccl and dev.type != "cuda":
+        return None
+
+    # 1. large groups: snapshot + all_reduce (in place on the snapshot)
+    reduced: List[Optional[torch.Tensor]] = []
+    for sb in sbs:
+        if sb.reduce_end:
+            snap = sb.buf[: sb.reduce_end].clone()
+            for g in sb.groups:
+                if g.off < sb.reduce_end:
+                    _all_reduce_group(snap[g.off : g.off + g.nbytes].view(g.dtype), g.op, group)
+            reduced.append(snap)
+        else:
+            reduced.append(None)
+
+    # 2. the gather regions: ONE all-gather (zero-copy send for a single metric)
+    regions = [sb.buf[sb.gather_off : sb.gather_off + sb.gather_bytes] for sb in sbs if sb.gather_bytes]
+    merged_small: Optional[torch.Tensor] = None
+    if regions:
+        send = regions[0] if len(regions) == 1 else torch.cat(regions)
+        row_bytes = send.numel()
+        gathered = collectives.all_gather_fixed_async(send, group, ws, blocking=True).wait()
+        if ws == 1:
+            merged_small = gathered
+        else:
+            offs, counts, dts, ops = [], [], [], []
+            base = 0
+            for sb in sbs:
+                if not sb.gather_bytes:
+                    continue
+                o, c, d, p = sb.segments(base)
+                offs += o
+                counts += c
+                dts += d
+                ops += p
+                base += sb.gather_bytes
+            merged_small = _reduce_gathered(gathered, (offs, counts, dts, ops), ws, row_bytes)
+
+    # 3. the merged metrics: shallow copies whose states view the merged buffers
+    out = {}
+    base = 0
+    for (key, m), sb, snap in zip(metrics.items(), sbs, reduced):
+        r = copy.copy(m)
+        r._tea_sb = None
+        for g in sb.groups:
+            if g.off < sb.reduce_end:
+                src, goff = snap, g.off
+            else:
+                src, goff = merged_small, base + g.off - sb.gather_off
+            for name, shape, boff, n in g.members:
+                o = goff + boff
+                setattr(r, name, src[o : o + n * _esize(g.dtype)].view(g.dtype).view(shape))
+        if sb.flag_words:
+            o = base + sb.flag_off - sb.gather_off
+            r._err = merged_small[o : o + 4 * sb.flag_words].view(torch.int32)
+        if sb.gather_bytes:
+            base += sb.gather_bytes
+        out[key] = r
+    return out
+
+
+def plan_summary(metric) -> Optional[dict]:
+    """Layout of the metric's state buffer (for tests / docs): offsets, groups, collectives."""
+    sb = buffer_of(metric)
+    if sb is None:
+        return None
+    return {
+        "bytes": sb.nbytes,
+        "reduce_groups": [(g.op, str(g.dtype), g.off, g.nbytes) for g in sb.groups if g.off < sb.reduce_end],
+        "gather_groups": [(g.op, str(g.dtype), g.off, g.nbytes) for g in sb.groups if g.off >= sb.reduce_end],
+        "flag_words": sb.flag_words,
+        "collectives": sum(1 for g in sb.groups if g.off < sb.reduce_end) + (1 if sb.gather_bytes else 0),
+    }
+
+
+__all__: Sequence[str] = ["StateBuffer", "buffer_of", "fast_sync", "plan_summary", "SMALL_STATE_BYTES"]
