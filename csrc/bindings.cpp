@@ -96,8 +96,8 @@ void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, in
 }
 
 // Scratch that kernels overwrite before reading (no zeroing contract): per (device, stream,
-// slot), grown on demand.
-void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot) {
+// slot), grown on demand.  ``fresh`` (optional) reports whether this call (re)allocated it.
+void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot, bool* fresh = nullptr) {
   static std::mutex mu;
   static std::unordered_map<uint64_t, Tensor> cache;
   const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
@@ -109,6 +109,9 @@ void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, i
                           at::TensorOptions().dtype(at::kByte).device(like.device()));
     if (it == cache.end()) it = cache.emplace(key, ws).first;
     else it->second = ws;
+    if (fresh) *fresh = true;
+  } else if (fresh) {
+    *fresh = false;
   }
   return it->second.data_ptr();
 }
@@ -188,10 +191,13 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
 // the general Python path (which raises the reference's own errors).  One pybind call with
 // four positional tensors instead of the 15-argument cls_counts plus its Python-side checks.
 bool micro_accuracy_update(const Tensor& input, const Tensor& target, const Tensor& correct,
-                           const Tensor& total) {
+                           const Tensor& total, int64_t num_classes) {
   if (!input.is_cuda() || input.dim() != 2 || target.dim() != 1) return false;
   const int64_t n = input.size(0), c = input.size(1);
   if (target.size(0) != n || c <= 0 || c >= (int64_t(1) << 31) || input.stride(1) != 1) return false;
+  // a metric built with num_classes only accepts [N, num_classes] scores: anything else goes
+  // to the Python path, which raises the reference's ValueError (accuracy.py:340-346)
+  if (num_classes > 0 && c != num_classes) return false;
   const auto st = input.scalar_type();
   if (st != at::kFloat && st != at::kBFloat16 && st != at::kHalf) return false;
   switch (target.scalar_type()) {
@@ -947,24 +953,24 @@ int64_t sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) {
   a.n = n;
   a.ld = tea::symeig_slot_stride(n);
   // layout: ctl (2 KB), d [ld], e [ld], then 4 granule planes [n-2, ld].  The granules must
-  // never match a phase tag by accident, so the block is zeroed whenever it is (re)allocated;
-  // afterwards only this op writes it, with tags that change every launch.
+  // never match a phase tag by accident: the block is zeroed whenever the workspace call
+  // (re)allocates it (its own "fresh" flag, not a pointer map that a recycled address could
+  // fool) and again whenever the 20-bit launch counter in the tags wraps, so a stale granule
+  // can never carry a tag of the current launch.  Only this op writes the block.
   const int64_t bytes = 2048 + (2 * a.ld + 4 * (n - 2) * a.ld) * (int64_t)sizeof(double);
-  char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3));
   {
     static std::mutex mu;
-    static std::unordered_map<void*, int64_t> zeroed;
     static unsigned launches = 0;
     std::lock_guard<std::mutex> lock(mu);
-    auto it = zeroed.find(ws);
-    if (it == zeroed.end() || it->second < bytes) {
-      TORCH_CHECK(hipMemsetAsync(ws, 0, bytes, stream) == hipSuccess, "sym_eigvals: workspace memset failed");
-      zeroed[ws] = bytes;
-    }
+    bool fresh = false;
+    char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3, &fresh));
     launches = launches % 0xFFFFFu + 1u;
+    if (fresh || launches == 1u)
+      TORCH_CHECK(hipMemsetAsync(ws, 0, bytes, stream) == hipSuccess, "sym_eigvals: workspace memset failed");
     a.tag_base = launches << 12;  // phase tags tag_base | (q + 1), q + 1 < 4096
+    a.ctl = reinterpret_cast<unsigned*>(ws);
   }
-  a.ctl = reinterpret_cast<unsigned*>(ws);
+  char* ws = reinterpret_cast<char*>(a.ctl);
   a.d = reinterpret_cast<double*>(ws + 2048);
   a.e = a.d + a.ld;
   a.gran = reinterpret_cast<unsigned long long*>(a.e + a.ld);
@@ -1253,7 +1259,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "C3 reduce a gathered [ws][row] state buffer per (op, dtype) segment in one launch", py::arg("rows"),
         py::arg("out"), py::arg("ws"), py::arg("offs"), py::arg("counts"), py::arg("dtypes"), py::arg("ops"));
   m.def("micro_accuracy_update", &micro_accuracy_update,
-        "K1 micro accuracy (k=1) accumulated into float32 scalar states; false = not handled");
+        "K1 micro accuracy (k=1) accumulated into float32 scalar states; false = not handled", py::arg("input"),
+        py::arg("target"), py::arg("correct"), py::arg("total"), py::arg("num_classes") = 0);
   m.def("cls_counts", &cls_counts, "K1 fused classification counts", py::arg("input"),
         py::arg("target"), py::arg("k"), py::arg("num_classes"), py::arg("micro_correct"),
         py::arg("micro_total"), py::arg("cls_correct"), py::arg("cls_label"),

@@ -37,6 +37,56 @@ def test_out_of_range_target_raises_at_compute():
         m.compute()
 
 
+def test_fast_path_keeps_the_reference_shape_check():
+    """MulticlassAccuracy(num_classes=10) on [N, 1000] scores: the K1 fast path declines and
+    the reference's ValueError is raised (reference accuracy.py:340-346)."""
+    dev = torch.device("cuda")
+    m = MulticlassAccuracy(num_classes=10, device=dev)
+    assert m._fast
+    with pytest.raises(ValueError, match="input should have shape of"):
+        m.update(torch.randn(64, 1000, device=dev), torch.randint(0, 10, (64,), device=dev))
+    m.update(torch.randn(64, 10, device=dev), torch.randint(0, 10, (64,), device=dev))  # matching: fast path
+    assert float(m.num_total) == 64.0
+
+
+def test_state_buffer_sync_on_rccl_one_rank():
+    """The contiguous state buffer under a 1-rank RCCL group (collectives forced): same
+    results as local compute, inputs untouched, and a reset keeps the kernel's pointers."""
+    import socket
+
+    import torch.distributed as dist
+
+    from torcheval_amd.metrics import MulticlassConfusionMatrix
+    from torcheval_amd.metrics.toolkit import sync_and_compute
+    from torcheval_amd.parallel.collectives import collectives_at_world_size_1
+    from torcheval_amd.parallel.state_buffer import buffer_of
+
+    dev = torch.device("cuda", 0)
+    with socket.socket() as s_:
+        s_.bind(("127.0.0.1", 0))
+        port = s_.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1, device_id=dev)
+    try:
+        x = torch.randn(4096, 1000, device=dev)
+        y = torch.randint(0, 1000, (4096,), device=dev)
+        acc = MulticlassAccuracy(device=dev).update(x, y)
+        cm = MulticlassConfusionMatrix(1000, device=dev).update(x, y)
+        with collectives_at_world_size_1():
+            for m in (acc, cm):
+                local = m.compute().clone()
+                torch.testing.assert_close(sync_and_compute(m), local)
+                torch.testing.assert_close(m.compute(), local)  # inputs untouched
+        sb = buffer_of(acc, build=False)
+        assert sb is not None
+        ptr = acc.num_correct.data_ptr()
+        acc.reset()
+        assert acc.num_correct.data_ptr() == ptr and float(acc.num_total) == 0.0
+        acc.update(x, y)
+        torch.testing.assert_close(acc.compute(), (x.argmax(1) == y).float().mean())
+    finally:
+        dist.destroy_process_group()
+
+
 def test_binary_gpu():
     x = torch.rand(10000)
     y = torch.randint(0, 2, (10000,))

@@ -113,3 +113,21 @@ def test_ineligible_and_lazily_shaped_metrics():
     assert buffer_of(m, build=False) is None
     m.update(torch.ones(4, 2))
     assert m.compute().tolist() == [4.0, 4.0]
+
+
+def test_sorted_run_merge_without_native(monkeypatch):
+    """the synced-AUROC merge path must not need _C (or launch K3m) when the
+    native path is off; a stable sort of the concatenated runs is the same merge."""
+    from torcheval_amd.metrics.functional import binary_auprc, binary_auroc
+    from torcheval_amd.metrics.functional.classification import _curve
+
+    g = torch.Generator().manual_seed(4)
+    runs = [torch.sort(torch.randint(0, 30, (n,), generator=g).float() / 30, descending=True)[0]
+            for n in (50, 1, 77)]
+    ts = [torch.randint(0, 2, (r.numel(),), generator=g) for r in runs]
+    want = (binary_auroc(torch.cat(runs), torch.cat(ts)), binary_auprc(torch.cat(runs), torch.cat(ts)))
+    for loaded in (True, False):
+        monkeypatch.setattr(_curve, "native_loaded", lambda: loaded)
+        roc, pr = _curve.merged_areas(runs, ts, None, roc=True, pr=True)
+        torch.testing.assert_close(roc[0], want[0].double(), rtol=1e-12, atol=1e-12)
+        torch.testing.assert_close(pr[0], want[1].double(), rtol=1e-6, atol=1e-6)

@@ -109,6 +109,9 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
             and type(self) is MulticlassAccuracy
             and self._device.type == "cuda"
         )
+        # the native call declines inputs whose class count differs from num_classes, so the
+        # reference's shape ValueError is raised on the Python path (reference accuracy.py:340)
+        self._fast_nc = self.num_classes or 0
 
     def to(self: TAccuracy, device, *args, **kwargs) -> TAccuracy:
         super().to(device, *args, **kwargs)
@@ -120,7 +123,7 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         Update states with a batch of predictions (``[N]`` labels or ``[N, C]`` scores)
         and ``[N]`` ground-truth labels.
         """
-        if self._fast and _FAST_MICRO(input, target, self.num_correct, self.num_total):
+        if self._fast and _FAST_MICRO(input, target, self.num_correct, self.num_total, self._fast_nc):
             return self
         dev = self._device
         if input.device != dev:

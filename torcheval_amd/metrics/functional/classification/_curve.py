@@ -14,7 +14,7 @@ from typing import List, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from torcheval_amd.ops import use_native
+from torcheval_amd.ops import native_loaded, use_native
 
 
 def _group_ends(s: torch.Tensor) -> torch.Tensor:
@@ -226,8 +226,12 @@ def merged_areas(runs_x, runs_t, runs_w, *, roc: bool, pr: bool):
         return out_roc, out_pr
     t = torch.cat([r.reshape(-1) for r in runs_t])
     w = None if runs_w is None else torch.cat([r.reshape(-1) for r in runs_w])
-    s, order = native().merge_sorted_runs(xs)
-    if use_native(s) and t.is_cuda:
+    gpu = xs[0].is_cuda and use_native(xs[0])  # False under DISABLE_HIP: no GPU kernel then
+    if gpu or (not xs[0].is_cuda and native_loaded()):
+        s, order = native().merge_sorted_runs(xs)  # K3m on ROCm, the C++ host merge on CPU
+    else:  # ATen: a stable sort of the concatenation is the rank-ordered merge
+        s, order = torch.sort(torch.cat(xs), descending=True, stable=True)
+    if gpu and t.is_cuda:
         tt = t if t.dtype != torch.bool else t.to(torch.uint8)
         out_roc = torch.empty(1, dtype=torch.float64, device=s.device) if roc else None
         out_pr = torch.empty(1, dtype=torch.float64, device=s.device) if pr else None

@@ -198,9 +198,24 @@ def inception_v3(weights_path: Optional[str] = None, **kwargs) -> Inception3:
             state = load_file(weights_path)
         else:
             state = torch.load(weights_path, map_location="cpu", weights_only=True)
+        # the auxiliary classifier is not part of this feature model: drop it explicitly, then
+        # load strictly - a renamed or partial checkpoint must not leave random weights behind
         state = {k: v for k, v in state.items() if not k.startswith("AuxLogits.")}
-        model.load_state_dict(state, strict=False)
+        missing, unexpected = _key_mismatch(model, state)
+        if missing or unexpected:
+            raise RuntimeError(
+                f"Inception-v3 checkpoint {weights_path!r} does not match the model: "
+                f"missing keys {missing[:8]}{' ...' if len(missing) > 8 else ''}, "
+                f"unexpected keys {unexpected[:8]}{' ...' if len(unexpected) > 8 else ''}."
+            )
+        model.load_state_dict(state, strict=True)
     return model
+
+
+def _key_mismatch(model: nn.Module, state: dict):
+    want = set(model.state_dict().keys())
+    have = set(state.keys())
+    return sorted(want - have), sorted(have - want)
 
 
 class FIDInceptionV3(nn.Module):
