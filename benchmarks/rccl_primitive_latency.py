@@ -41,5 +41,18 @@ res = {
     "empty_kernel_add_us": t(lambda: a.add_(1)),
     "item_sync_us": t(lambda: a.sum().item()),
 }
+# lower-overhead entry points into the same RCCL calls (the sync engine's choice)
+from torch.distributed.distributed_c10d import _get_default_group
+
+pg = _get_default_group()
+res["pg_allgather_base_64B_us"] = t(lambda: pg._allgather_base(o, b).wait())
+res["empty_plus_all_gather_64B_us"] = t(lambda: dist.all_gather_into_tensor(torch.empty(64, dtype=torch.uint8, device=dev), b))
+res["pg_allreduce_8B_us"] = t(lambda: pg.allreduce([a]).wait())
+res["host_only_all_gather_64B_us"] = None
+t0 = time.perf_counter()
+for _ in range(200):
+    dist.all_gather_into_tensor(o, b)
+res["host_only_all_gather_64B_us"] = round((time.perf_counter() - t0) / 200 * 1e6, 2)
+torch.cuda.synchronize()
 print(json.dumps(res))
 dist.destroy_process_group()

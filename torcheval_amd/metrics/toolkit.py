@@ -15,6 +15,7 @@ from typing import Any, Dict, Iterable, List, MutableMapping, Optional, TypeVar,
 import torch
 import torch.distributed as dist
 
+from torcheval_amd.config import config as _cfg
 from torcheval_amd.config import trace_range
 from torcheval_amd.metrics.metric import Metric, TComputeReturn
 from datetime import timedelta
@@ -166,8 +167,11 @@ def get_synced_metric(
     _validate_rank_and_world_size(world_size)
     if skip_collectives(world_size):
         return metric
+    group = process_group if process_group else dist.group.WORLD
+    if timeout is None and not _cfg.trace:  # the common case: no context managers to enter
+        return sync_metric(metric, group, world_size)
     with trace_range("torcheval_amd.sync_metric"), sync_timeout(timeout):
-        return sync_metric(metric, process_group if process_group else dist.group.WORLD, world_size)
+        return sync_metric(metric, group, world_size)
 
 
 def get_synced_metric_collection(

@@ -108,7 +108,7 @@ class StateBuffer:
     """The contiguous state buffer of one metric plus its cached sync plans."""
 
     __slots__ = ("buf", "device", "groups", "reduce_end", "gather_off", "gather_bytes", "flag_off",
-                 "flag_words", "names", "ptrs", "err_obj", "default_img", "nbytes", "_seg_cache")
+                 "flag_words", "names", "ptrs", "err_obj", "default_img", "nbytes", "_seg_cache", "plans")
 
     # ---------------------------------------------------------------- construction
     @classmethod
@@ -172,6 +172,7 @@ class StateBuffer:
         self.err_obj = getattr(metric, "_err", None) if words else None
         self.ptrs = tuple(getattr(metric, n).data_ptr() for n in self.names)
         self._seg_cache = None
+        self.plans = {}
         metric._tea_sb = self
         return self
 
@@ -303,12 +304,110 @@ def _all_reduce_group(t: torch.Tensor, op: str, group) -> None:
 
 
 # -------------------------------------------------------------------- the sync
+class _Plan:
+    """Everything a single-metric sync needs, resolved once per (buffer, group, world size):
+    the send view, the receive size, the segment table and where each state lands."""
+
+    __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large")
+
+    def __init__(self, sb: StateBuffer, group, ws: int) -> None:
+        from torch.distributed.distributed_c10d import _get_default_group
+
+        self.group = group  # held: keeps id(group) from being reused while the plan lives
+        self.pg = group if group is not None else _get_default_group()
+        self.ws = ws
+        self.nccl = backend_of(group) == "nccl"
+        self.src = sb.buf[sb.gather_off : sb.gather_off + sb.gather_bytes] if sb.gather_bytes else None
+        self.row_bytes = sb.gather_bytes
+        self.segs = sb.segments(0)
+        self.large = [(g.off, g.nbytes, g.dtype, g.op) for g in sb.groups if g.off < sb.reduce_end]
+        # (name, from the reduce snapshot?, dtype, element offset, numel, shape or None for 0-dim):
+        # states are indexed out of ONE typed view per (source, dtype)
+        self.assign = []
+        for g in sb.groups:
+            big = g.off < sb.reduce_end
+            es = _esize(g.dtype)
+            for name, shape, boff, n in g.members:
+                o = (g.off if big else g.off - sb.gather_off) + boff
+                self.assign.append((name, big, g.dtype, o // es, n, shape if shape else None))
+        self.flag = (sb.flag_off - sb.gather_off, 4 * sb.flag_words) if sb.flag_words else None
+
+
+def _plan_for(sb: StateBuffer, group, ws: int) -> _Plan:
+    key = (id(group), ws)
+    plan = sb.plans.get(key)
+    if plan is None or plan.group is not group:
+        plan = sb.plans[key] = _Plan(sb, group, ws)
+    return plan
+
+
+def _gather(plan: _Plan, src: torch.Tensor) -> torch.Tensor:
+    """One all-gather of the raw gather region; RCCL: straight into one [ws * row] buffer."""
+    if plan.nccl and collectives.current_sync_timeout() is None:
+        out = torch.empty(plan.ws * plan.row_bytes, dtype=torch.uint8, device=src.device)
+        dist.all_gather_into_tensor(out, src, group=plan.group)
+        return out
+    return collectives.all_gather_fixed_async(src, plan.group, plan.ws, blocking=True).wait()
+
+
+def _sync_one(m, sb: StateBuffer, plan: _Plan):
+    ws = plan.ws
+    snap = None
+    if plan.large:
+        snap = sb.buf[: sb.reduce_end].clone()
+        for off, nb, dtype, op in plan.large:
+            _all_reduce_group(snap[off : off + nb].view(dtype), op, plan.group)
+    merged = None
+    if plan.src is not None:
+        merged = _gather(plan, plan.src)
+        if ws > 1:
+            merged = _reduce_gathered(merged, plan.segs, ws, plan.row_bytes)
+    r = object.__new__(type(m))  # a shallow copy (copy.copy costs ~4x this)
+    d = r.__dict__
+    d.update(m.__dict__)
+    d["_tea_sb"] = None
+    typed = {}
+    for name, big, dtype, eo, n, shape in plan.assign:
+        key = (big, dtype)
+        t = typed.get(key)
+        if t is None:
+            t = typed[key] = (snap if big else merged).view(dtype)
+        d[name] = t[eo] if shape is None else t[eo : eo + n].view(shape)
+    if plan.flag is not None:
+        o, nb = plan.flag
+        d["_err"] = merged[o : o + nb].view(torch.int32)
+    return r
+
+
+def sync_single(m, group, ws: int):
+    """``sync_metric`` of one metric through its cached plan, or None when not eligible."""
+    sb = m.__dict__.get("_tea_sb")
+    if sb is None or not sb.valid(m):
+        m._prepare_for_merge_state()
+        sb = StateBuffer.build(m)
+        if sb is None:
+            return None
+    plan = _plan_for(sb, group, ws)
+    if plan.nccl and sb.device.type != "cuda":
+        return None
+    return _sync_one(m, sb, plan)
+
+
 def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
     """Blocking sync of a collection whose metrics all keep their states in a StateBuffer.
 
     Returns ``{key: merged metric}`` (new shallow copies; the inputs are untouched) or None
     when some metric is not eligible (the caller then runs the generic engine).  Every rank
     must pass the same collection (same keys, types and state shapes)."""
+    if len(metrics) == 1:  # sync_and_compute / get_synced_metric: the cached plan
+        (key, m), = metrics.items()
+        sb = buffer_of(m)
+        if sb is None:
+            return None
+        plan = _plan_for(sb, group, ws)
+        if plan.nccl and sb.device.type != "cuda":
+            return None
+        return {key: _sync_one(m, sb, plan)}
     sbs = []
     for m in metrics.values():
         sb = buffer_of(m)

@@ -422,4 +422,8 @@ def sync_metric(
     process_group: Optional[dist.ProcessGroup] = None,
     world_size: Optional[int] = None,
 ) -> Metric:
-    return sync_metric_collection({"_": metric}, process_group, world_size)["_"]
+    ws = world_size if world_size is not None else dist.get_world_size(process_group)
+    fast = state_buffer.sync_single(metric, process_group, ws)  # the cached one-collective plan
+    if fast is not None:
+        return fast
+    return sync_metric_collection({"_": metric}, process_group, ws)["_"]
