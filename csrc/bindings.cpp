@@ -1377,9 +1377,100 @@ void op_cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t
              confusion, err, 0, c10::nullopt, c10::nullopt, c10::nullopt);
 }
 
+// ---- dispatcher wrappers of the remaining entry points (schemas below annotate mutation)
+void op_micro_accuracy(const Tensor& input, const Tensor& target, const Tensor& correct, const Tensor& total) {
+  TORCH_CHECK(micro_accuracy_update(input, target, correct, total, 0),
+              "micro_accuracy: unsupported input (needs [N, C] f32/bf16/f16 scores with unit column stride, "
+              "[N] integer targets and float32 scalar states on one ROCm device)");
+}
+Tensor op_rank_scores(const Tensor& input, const Tensor& target, int64_t mode, int64_t k, const optional<Tensor>& err) {
+  return rank_scores(input, target, mode, k, err);
+}
+void op_binary_counts(const Tensor& input, const Tensor& target, const optional<Tensor>& weight, double threshold,
+                      const optional<Tensor>& tp, const optional<Tensor>& fp, const optional<Tensor>& tn,
+                      const optional<Tensor>& fn, const optional<Tensor>& total, int64_t strict) {
+  binary_counts(input, target, weight, threshold, tp, fp, tn, fn, total, strict, 0, c10::nullopt, c10::nullopt,
+                c10::nullopt, c10::nullopt);
+}
+void op_curve_count(const Tensor& sorted, const Tensor& order, const Tensor& target, bool class_mode,
+                    int64_t payload_kind, const Tensor& workspace, const Tensor& sizes) {
+  curve_count(sorted, order, target, class_mode, payload_kind, workspace, sizes);
+}
+void op_curve_emit(const Tensor& sorted, const Tensor& order, const Tensor& target, bool class_mode,
+                   int64_t payload_kind, const Tensor& workspace, const Tensor& sizes, const Tensor& row_off,
+                   const Tensor& out_prec, const Tensor& out_rec, const Tensor& out_thr) {
+  curve_emit(sorted, order, target, class_mode, payload_kind, workspace, sizes, row_off, out_prec, out_rec, out_thr);
+}
+std::vector<Tensor> op_merge_sorted_runs(at::TensorList keys, at::TensorList payloads) {
+  optional<std::vector<Tensor>> pays;
+  if (!payloads.empty()) pays = payloads.vec();  // [] = no payloads (positions come back)
+  return merge_sorted_runs(keys.vec(), pays);
+}
+void op_retrieval_topk_update(const Tensor& x, const Tensor& t, const optional<Tensor>& q, const Tensor& topk,
+                              const Tensor& target, const Tensor& count) {
+  retrieval_topk_update(x, t, q, topk, target, count);
+}
+void op_binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr, int64_t mode, const Tensor& tp,
+                      const Tensor& fp, const Tensor& fn, int64_t uniform) {
+  binned_counts(input, target, thr, mode, tp, fp, fn, uniform);
+}
+void op_column_moments(const optional<Tensor>& x, const optional<Tensor>& t, const optional<Tensor>& w,
+                       const optional<Tensor>& sse, const optional<Tensor>& st, const optional<Tensor>& stt,
+                       const optional<Tensor>& sx, const optional<Tensor>& sw, int64_t overwrite, int64_t mse_mode,
+                       const optional<Tensor>& mse_out, int64_t num_regressors) {
+  column_moments(x, t, w, sse, st, stt, sx, sw, overwrite, mse_mode, mse_out, num_regressors);
+}
+void op_ne_sums(const Tensor& x, const Tensor& t, const optional<Tensor>& w, bool from_logits, const Tensor& out,
+                const optional<Tensor>& err, bool deterministic) {
+  ne_sums(x, t, w, from_logits, out, err, deterministic);
+}
+void op_multilabel_counts(const Tensor& input, const Tensor& target, double threshold, int64_t k, int64_t criteria,
+                          const Tensor& num_correct, const optional<Tensor>& num_total, double total) {
+  multilabel_counts(input, target, threshold, k, criteria, num_correct, num_total, total);
+}
+void op_binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>& fn,
+                        const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc,
+                        const optional<Tensor>& out_prec, const optional<Tensor>& out_rec) {
+  binned_finalize(tp, fp, fn, out_auroc, out_auprc, out_prec, out_rec);
+}
+int64_t op_sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) { return sym_eigvals(m, lam, status); }
+void op_potrf_block(const Tensor& a, int64_t k0, int64_t b, const Tensor& linv, const Tensor& info) {
+  potrf_block(a, k0, b, linv, info);
+}
+void op_seg_reduce_rows(const Tensor& rows, const Tensor& out, int64_t ws, at::IntArrayRef offs,
+                        at::IntArrayRef counts, at::IntArrayRef dtypes, at::IntArrayRef ops) {
+  seg_reduce_rows(rows, out, ws, offs, counts, dtypes, ops);
+}
+
 }  // namespace
 
 TORCH_LIBRARY(torcheval_amd, m) {
+  m.def("micro_accuracy(Tensor input, Tensor target, Tensor(a!) correct, Tensor(b!) total) -> ()");
+  m.def("rank_scores(Tensor input, Tensor target, int mode, int k, Tensor(a!)? err) -> Tensor");
+  m.def("binary_counts(Tensor input, Tensor target, Tensor? weight, float threshold, Tensor(a!)? tp, "
+        "Tensor(b!)? fp, Tensor(c!)? tn, Tensor(d!)? fn, Tensor(e!)? total, int strict) -> ()");
+  m.def("curve_count(Tensor sorted, Tensor order, Tensor target, bool class_mode, int payload_kind, "
+        "Tensor(a!) workspace, Tensor(b!) sizes) -> ()");
+  m.def("curve_emit(Tensor sorted, Tensor order, Tensor target, bool class_mode, int payload_kind, "
+        "Tensor(a!) workspace, Tensor sizes, Tensor row_off, Tensor(b!) out_prec, Tensor(c!) out_rec, "
+        "Tensor(d!) out_thr) -> ()");
+  m.def("merge_sorted_runs(Tensor[] keys, Tensor[] payloads) -> Tensor[]");
+  m.def("retrieval_topk_update(Tensor x, Tensor t, Tensor? q, Tensor(a!) topk, Tensor(b!) target, "
+        "Tensor(c!) count) -> ()");
+  m.def("binned_counts(Tensor input, Tensor target, Tensor thr, int mode, Tensor(a!) tp, Tensor(b!) fp, "
+        "Tensor(c!) fn, int uniform) -> ()");
+  m.def("column_moments(Tensor? x, Tensor? t, Tensor? w, Tensor(a!)? sse, Tensor(b!)? st, Tensor(c!)? stt, "
+        "Tensor(d!)? sx, Tensor(e!)? sw, int overwrite, int mse_mode, Tensor(f!)? mse_out, int num_regressors) -> ()");
+  m.def("ne_sums(Tensor x, Tensor t, Tensor? w, bool from_logits, Tensor(a!) out, Tensor(b!)? err, "
+        "bool deterministic) -> ()");
+  m.def("multilabel_counts(Tensor input, Tensor target, float threshold, int k, int criteria, "
+        "Tensor(a!) num_correct, Tensor(b!)? num_total, float total) -> ()");
+  m.def("binned_finalize(Tensor tp, Tensor fp, Tensor? fn, Tensor(a!)? out_auroc, Tensor(b!)? out_auprc, "
+        "Tensor(c!)? out_prec, Tensor(d!)? out_rec) -> ()");
+  m.def("sym_eigvals(Tensor m, Tensor(a!) lam, Tensor(b!) status) -> int");
+  m.def("potrf_block(Tensor(a!) a, int k0, int b, Tensor(b!) linv, Tensor(c!) info) -> ()");
+  m.def("seg_reduce_rows(Tensor rows, Tensor(a!) out, int ws, int[] offs, int[] counts, int[] dtypes, "
+        "int[] ops) -> ()");
   m.def("row_sums(Tensor x, Tensor? t, Tensor? w, float w_scalar, Tensor(a!)[] outs, int[] codes, int rows) -> ()");
   m.def("sort_desc(Tensor x, Tensor(a!) sorted, Tensor(b!) order, Tensor? payload, int payload_kind) -> ()");
   m.def("auc_scan(Tensor sorted, Tensor order, Tensor target, Tensor? weight, bool class_mode, "
@@ -1397,6 +1488,21 @@ TORCH_LIBRARY(torcheval_amd, m) {
 }
 
 TORCH_LIBRARY_IMPL(torcheval_amd, CUDA, m) {
+  m.impl("micro_accuracy", &op_micro_accuracy);
+  m.impl("rank_scores", &op_rank_scores);
+  m.impl("binary_counts", &op_binary_counts);
+  m.impl("curve_count", &op_curve_count);
+  m.impl("curve_emit", &op_curve_emit);
+  m.impl("merge_sorted_runs", &op_merge_sorted_runs);
+  m.impl("retrieval_topk_update", &op_retrieval_topk_update);
+  m.impl("binned_counts", &op_binned_counts);
+  m.impl("column_moments", &op_column_moments);
+  m.impl("ne_sums", &op_ne_sums);
+  m.impl("multilabel_counts", &op_multilabel_counts);
+  m.impl("binned_finalize", &op_binned_finalize);
+  m.impl("sym_eigvals", &op_sym_eigvals);
+  m.impl("potrf_block", &op_potrf_block);
+  m.impl("seg_reduce_rows", &op_seg_reduce_rows);
   m.impl("row_sums", &op_row_sums);
   m.impl("sort_desc", &op_sort_desc);
   m.impl("auc_scan", &op_auc_scan);
@@ -1413,6 +1519,40 @@ TORCH_LIBRARY_IMPL(torcheval_amd, CPU, m) {
 }
 
 TORCH_LIBRARY_IMPL(torcheval_amd, Meta, m) {
+  m.impl("micro_accuracy", [](const Tensor&, const Tensor&, const Tensor&, const Tensor&) {});
+  m.impl("rank_scores", [](const Tensor& input, const Tensor&, int64_t, int64_t, const optional<Tensor>&) {
+    return at::empty({input.size(0)}, input.options().dtype(at::kFloat));
+  });
+  m.impl("binary_counts", [](const Tensor&, const Tensor&, const optional<Tensor>&, double, const optional<Tensor>&,
+                             const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&,
+                             const optional<Tensor>&, int64_t) {});
+  m.impl("retrieval_topk_update", [](const Tensor&, const Tensor&, const optional<Tensor>&, const Tensor&,
+                                     const Tensor&, const Tensor&) {});
+  m.impl("binned_counts", [](const Tensor&, const Tensor&, const Tensor&, int64_t, const Tensor&, const Tensor&,
+                             const Tensor&, int64_t) {});
+  m.impl("column_moments", [](const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&,
+                              const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&,
+                              const optional<Tensor>&, const optional<Tensor>&, int64_t, int64_t,
+                              const optional<Tensor>&, int64_t) {});
+  m.impl("ne_sums", [](const Tensor&, const Tensor&, const optional<Tensor>&, bool, const Tensor&,
+                       const optional<Tensor>&, bool) {});
+  m.impl("multilabel_counts", [](const Tensor&, const Tensor&, double, int64_t, int64_t, const Tensor&,
+                                 const optional<Tensor>&, double) {});
+  m.impl("binned_finalize", [](const Tensor&, const Tensor&, const optional<Tensor>&, const optional<Tensor>&,
+                               const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&) {});
+  m.impl("potrf_block", [](const Tensor&, int64_t, int64_t, const Tensor&, const Tensor&) {});
+  m.impl("seg_reduce_rows", [](const Tensor&, const Tensor&, int64_t, at::IntArrayRef, at::IntArrayRef,
+                               at::IntArrayRef, at::IntArrayRef) {});
+  m.impl("cls_counts", [](const Tensor&, const Tensor&, int64_t, int64_t, const optional<Tensor>&,
+                          const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&,
+                          const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&) {});
+  m.impl("auc_scan", [](const Tensor&, const Tensor&, const Tensor&, const optional<Tensor>&, bool,
+                        const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&,
+                        const optional<Tensor>&, int64_t) {});
+  m.impl("rafp", [](const Tensor&, const Tensor&, const Tensor&, bool, int64_t, double, const Tensor&,
+                    const Tensor&) {});
+  m.impl("perplexity_sums", [](const Tensor&, const Tensor&, optional<int64_t>, const Tensor&,
+                               const optional<Tensor>&, bool) {});
   m.impl("row_sums", [](const Tensor&, const optional<Tensor>&, const optional<Tensor>&, double, at::TensorList,
                         at::IntArrayRef, int64_t) {});
   m.impl("sort_desc", [](const Tensor&, const Tensor&, const Tensor&, const optional<Tensor>&, int64_t) {});

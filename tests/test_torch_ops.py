@@ -31,3 +31,35 @@ def test_schemas_declare_mutation():
     schema = str(torch.ops.torcheval_amd.rafp.default._schema)
     assert "Tensor(a!) out_max_recall" in schema and "Tensor(b!) out_best_thr" in schema
     assert "Tensor(a!)[] outs" in str(torch.ops.torcheval_amd.row_sums.default._schema)
+
+
+HOT_OPS = ("micro_accuracy", "cls_counts", "binary_counts", "rank_scores", "multilabel_counts", "binned_counts",
+           "binned_finalize", "auc_scan", "sort_desc", "rafp", "curve_count", "curve_emit", "merge_sorted_runs",
+           "retrieval_topk_update", "row_sums", "column_moments", "ne_sums", "perplexity_sums", "fid_cov_update",
+           "sym_eigvals", "potrf_block", "transpose_f32", "seg_reduce_rows")
+
+
+@pytest.mark.parametrize("name", HOT_OPS)
+def test_every_native_entry_point_is_a_dispatcher_op(name):
+    op = getattr(torch.ops.torcheval_amd, name).default
+    schema = op._schema
+    # every kernel that writes into caller tensors says so in its schema
+    returns_only = name in ("merge_sorted_runs",)
+    assert returns_only or any(a.alias_info is not None and a.alias_info.is_write for a in schema.arguments) \
+        or len(schema.returns) > 0, str(schema)
+
+
+def test_meta_kernels_of_update_ops():
+    m = "meta"
+    x = torch.empty(64, 100, device=m)
+    y = torch.empty(64, dtype=torch.int64, device=m)
+    c, t = torch.empty((), device=m), torch.empty((), device=m)
+    torch.ops.torcheval_amd.micro_accuracy(x, y, c, t)
+    cm = torch.empty(100 * 100, device=m)
+    torch.ops.torcheval_amd.cls_counts(x, y, 1, 100, None, None, None, None, None, cm, None)
+    thr = torch.empty(50, device=m)
+    tp, fp, fn = (torch.empty(50, 100, device=m) for _ in range(3))
+    torch.ops.torcheval_amd.binned_counts(x, y, thr, 1, tp, fp, fn, 0)
+    assert torch.ops.torcheval_amd.rank_scores(x, y, 0, 5, None).shape == (64,)
+    rows, out = torch.empty(64, dtype=torch.uint8, device=m), torch.empty(32, dtype=torch.uint8, device=m)
+    torch.ops.torcheval_amd.seg_reduce_rows(rows, out, 2, [0], [8], [0], [0])

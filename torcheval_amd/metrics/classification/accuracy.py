@@ -32,7 +32,7 @@ from torcheval_amd.metrics.functional.classification.accuracy import (
 )
 from torcheval_amd.metrics.metric import Metric
 import torcheval_amd.ops as _ops
-from torcheval_amd.ops import native, native_loaded, use_native
+from torcheval_amd.ops import compiling, native, native_loaded, use_native
 
 # K1 micro-accuracy entry of the loaded extension (None when unbuilt); metrics built while
 # ``torcheval_amd.ops.DISABLE_HIP`` is set do not use it (checked per metric, at construction)
@@ -49,6 +49,25 @@ TAccuracy = TypeVar("TAccuracy")
 TBinaryAccuracy = TypeVar("TBinaryAccuracy")
 TMultilabelAccuracy = TypeVar("TMultilabelAccuracy")
 TTopKMultilabelAccuracy = TypeVar("TTopKMultilabelAccuracy")
+
+
+def _micro_op_ok(input: torch.Tensor, target: torch.Tensor, state: torch.Tensor, num_classes: int) -> bool:
+    """The preconditions ``_C.micro_accuracy_update`` tests itself, on metadata only (the
+    torch.compile route: static under tracing, so the op is traced unconditionally)."""
+    return (
+        input.is_cuda
+        and input.dim() == 2
+        and target.dim() == 1
+        and input.shape[0] == target.shape[0]
+        and input.shape[1] > 0
+        and (num_classes == 0 or input.shape[1] == num_classes)
+        and input.stride(1) == 1
+        and input.dtype in (torch.float32, torch.bfloat16, torch.float16)
+        and target.dtype in (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
+        and target.is_contiguous()
+        and target.device == input.device
+        and state.device == input.device
+    )
 
 
 def _raise_on_device_error(err: Optional[torch.Tensor]) -> None:
@@ -123,8 +142,13 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         Update states with a batch of predictions (``[N]`` labels or ``[N, C]`` scores)
         and ``[N]`` ground-truth labels.
         """
-        if self._fast and _FAST_MICRO(input, target, self.num_correct, self.num_total, self._fast_nc):
-            return self
+        if self._fast:
+            if not compiling():
+                if _FAST_MICRO(input, target, self.num_correct, self.num_total, self._fast_nc):
+                    return self
+            elif _micro_op_ok(input, target, self.num_correct, self._fast_nc):
+                torch.ops.torcheval_amd.micro_accuracy(input, target, self.num_correct, self.num_total)
+                return self
         dev = self._device
         if input.device != dev:
             input = input.to(dev)

@@ -14,7 +14,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops import native, native_loaded, use_native
+from torcheval_amd.ops import compiling, native, native_loaded, use_native
 from torcheval_amd.ops.classification import (
     binary_counts,
     cls_counts,
@@ -73,7 +73,7 @@ _CPU_FAST_MAX = 1 << 16
 
 
 def _cpu_fast_ok(input: torch.Tensor, target: torch.Tensor, k: int, num_classes: Optional[int]) -> bool:
-    if not native_loaded() or target.dim() != 1 or target.dtype != torch.int64 or target.numel() == 0:
+    if compiling() or not native_loaded() or target.dim() != 1 or target.dtype != torch.int64 or target.numel() == 0:
         return False
     if input.dim() == 2:
         ok = (

@@ -15,7 +15,12 @@ _UNIFORM: "weakref.WeakValueDictionary[int, torch.Tensor]" = weakref.WeakValueDi
 
 
 def _is_uniform_linspace(t: torch.Tensor) -> bool:
-    """True iff ``t`` is (the very tensor) ``linspace(0, 1, n)`` made from an int threshold."""
+    """True iff ``t`` is (the very tensor) ``linspace(0, 1, n)`` made from an int threshold.
+    (A speed hint only: under torch.compile the weak-reference lookup is skipped.)"""
+    from torch.compiler import is_compiling
+
+    if is_compiling():
+        return False
     return _UNIFORM.get(id(t)) is t
 
 

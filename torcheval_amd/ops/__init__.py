@@ -26,6 +26,13 @@ except ImportError as e:  # pragma: no cover - exercised only when unbuilt
     _LOAD_ERROR = e
 
 DISABLE_HIP = os.environ.get("TORCHEVAL_AMD_DISABLE_HIP", "0") == "1"
+
+# True while torch.compile (dynamo) traces a metric: hot paths then call the kernels through
+# the dispatcher (``torch.ops.torcheval_amd.*``, with Meta kernels and mutation-annotated
+# schemas, csrc/bindings.cpp) and CPU tensors take the ATen path instead of the pybind host
+# twins, so compiled update loops trace into one graph.  Eager calls keep the pybind entry
+# points, whose host cost per call is lower (benchmarks/host_overhead.py).
+from torch.compiler import is_compiling as compiling  # noqa: E402
 MAX_BLOCKS = int(os.environ.get("TORCHEVAL_AMD_MAX_BLOCKS", "0"))
 
 

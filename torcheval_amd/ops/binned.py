@@ -10,7 +10,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops import native, use_native
+from torcheval_amd.ops import compiling, native, use_native
 
 
 def binned_counts(
@@ -33,7 +33,11 @@ def binned_counts(
         t = target
         if t.dtype == torch.bool:
             t = t.to(torch.uint8)
-        native().binned_counts(scores, t, thr.to(torch.float32).contiguous(), int(mode), *out, uniform=int(uniform))
+        thr32 = thr.to(torch.float32).contiguous()
+        if compiling():
+            torch.ops.torcheval_amd.binned_counts(scores, t, thr32, int(mode), *out, int(uniform))
+        else:
+            native().binned_counts(scores, t, thr32, int(mode), *out, uniform=int(uniform))
         return out
     if _cpu_binned(scores, target, thr, mode):
         # small CPU batches: one C++ call (the ATen chain below is ~10 dispatches)
@@ -49,7 +53,7 @@ def binned_counts(
 def _cpu_binned(scores: torch.Tensor, target: torch.Tensor, thr: torch.Tensor, mode: int) -> bool:
     import torcheval_amd.ops as ops
 
-    if scores.is_cuda or target.is_cuda or thr.is_cuda or ops.DISABLE_HIP or not ops.native_loaded():
+    if ops.compiling() or scores.is_cuda or target.is_cuda or thr.is_cuda or ops.DISABLE_HIP or not ops.native_loaded():
         return False
     if scores.numel() > (1 << 16) or scores.dtype not in (torch.float32, torch.float64):
         return False

@@ -9,7 +9,7 @@ from typing import Optional
 import torch
 
 import torcheval_amd.ops as _ops
-from torcheval_amd.ops import MAX_BLOCKS, native, native_loaded, use_native
+from torcheval_amd.ops import MAX_BLOCKS, compiling, native, native_loaded, use_native
 
 _SCORE_DTYPES = (torch.float32, torch.bfloat16, torch.float16)
 _LABEL_DTYPES = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
@@ -33,7 +33,7 @@ _CPU_MAX = 1 << 16
 
 
 def _cpu_cls(input: torch.Tensor, target: torch.Tensor, num_classes: Optional[int]) -> bool:
-    if input.is_cuda or target.is_cuda or _ops.DISABLE_HIP or not native_loaded():
+    if compiling() or input.is_cuda or target.is_cuda or _ops.DISABLE_HIP or not native_loaded():
         return False
     if input.numel() > _CPU_MAX or target.dim() != 1 or target.dtype not in (torch.int64, torch.int32):
         return False
@@ -100,6 +100,13 @@ def cls_counts(
         target = target.contiguous()
     if input.dim() == 2 and num_classes <= 0:
         num_classes = input.shape[1]
+    if compiling() and input.is_cuda:  # dispatcher op: visible to torch.compile
+        if micro_incorrect is not None or micro_total2 is not None or cls_fp is not None:
+            raise NotImplementedError("cls_counts under torch.compile: micro_incorrect / micro_total2 / "
+                                      "cls_fp destinations are eager-only")
+        torch.ops.torcheval_amd.cls_counts(input, target, int(k), int(num_classes), micro_correct, micro_total,
+                                           cls_correct, cls_label, cls_pred, confusion, err)
+        return
     op = native().cls_counts if input.is_cuda else native().cpu_cls_counts
     op(
         input,
