@@ -15,6 +15,16 @@ Usage::
     torchrun --nproc-per-node N bench.py --gpus N ...     (driver launches N > 1 this way)
 
 Rank 0 prints ONE JSON line.
+
+Timing: barrier + device synchronize, then ``t0``; K updates and the ``sync_and_compute``
+(at N > 1 an RCCL all-gather of the metric's state buffer: no rank can leave it before every
+rank has entered it, so it closes the region like a barrier would); device synchronize, then
+the elapsed time, max-reduced over ranks.
+
+Rehearsal switches (not used by the driver): ``BENCH_BACKEND=gloo`` runs the multi-rank path
+over gloo, ``BENCH_DEVICE=cpu`` on CPU tensors (so the exact ``torchrun --nproc-per-node 8``
+launch can be exercised without GPUs, tests/test_bench_rehearsal.py), ``BENCH_EXTRAS=0`` skips
+the secondary sync timings.
 """
 
 import argparse
@@ -137,10 +147,19 @@ def main() -> None:
 
     # BENCH_BACKEND=gloo lets the multi-rank path be rehearsed with several ranks per GPU
     backend = os.environ.get("BENCH_BACKEND", "nccl")
-    dev = torch.device("cuda", local_rank % torch.cuda.device_count())
-    torch.cuda.set_device(dev)
+    on_cpu = os.environ.get("BENCH_DEVICE", "cuda") == "cpu"
+    if on_cpu:
+        backend = "gloo"
+        dev = torch.device("cpu")
+    else:
+        dev = torch.device("cuda", local_rank % torch.cuda.device_count())
+        torch.cuda.set_device(dev)
     if world > 1:
         init_from_env(device_type="cuda" if backend == "nccl" else "cpu", pg_backend=backend)
+
+    def device_sync():
+        if not on_cpu:
+            torch.cuda.synchronize()
 
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -166,7 +185,7 @@ def main() -> None:
     # this GPU.  Running it before the warmup also brings the GPU out of its idle clock state,
     # so the K timed steps see the same clocks as a long run does.
     ref_rate = None
-    if not args.no_reference:
+    if not args.no_reference and not on_cpu:
         rate = _reference_eager_rate(x_pool, y_pool, 2000)
         ref_rate = rate if rank == 0 else None
 
@@ -175,21 +194,20 @@ def main() -> None:
     # communicator setup - is paid here and not inside the timed region.
     for _ in range(2):
         run(max(args.warmup, 1))
-        torch.cuda.synchronize()
+        device_sync()
         metric.reset()
 
     barrier()
-    torch.cuda.synchronize()
+    device_sync()
     t0 = time.perf_counter()
-    acc = run(args.steps)
-    torch.cuda.synchronize()
-    barrier()
+    acc = run(args.steps)  # ends in sync_and_compute at N > 1: the closing rendezvous
+    device_sync()
     elapsed = time.perf_counter() - t0
 
     # correctness guard: the synced count must equal world * steps * batch
     total = float(metric.num_total) if world == 1 else None
     if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev if backend == "nccl" else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     else:
@@ -211,7 +229,8 @@ def main() -> None:
             "scaling": "weak",
             "vs_baseline": round(updates_per_s / BASELINE_UPDATES_PER_S, 2),
             "dtype": "fp32",
-            "data": "synthetic (8-batch pool of randn logits / randint targets per GPU)",
+            "data": "synthetic (8-batch pool of randn logits / randint targets per GPU)"
+            + (" [CPU rehearsal: not a GPU measurement]" if on_cpu else ""),
             "config": {
                 "model": "MulticlassAccuracy",
                 "global_batch": BATCH * world,
@@ -231,7 +250,7 @@ def main() -> None:
     # rank abandons (an exception inside an extra) would leave the others blocked forever, so a
     # watchdog bounds the whole section: on expiry rank 0 prints the headline line without the
     # extras and every rank exits 0 - the driver always gets its one JSON line.
-    if world > 1:
+    if world > 1 and os.environ.get("BENCH_EXTRAS", "1") != "0":
         import threading
 
         def _bail():

@@ -38,11 +38,13 @@ def test_timed_region_only_runs_the_warmed_sequence():
                 and ast.unparse(s.targets[0]) == "elapsed")
     timed = _calls(body[start + 1:stop])
     assert "run" in timed
-    allowed = {"run", "torch.cuda.synchronize", "barrier"}
+    allowed = {"run", "device_sync"}  # the closing rendezvous is run()'s sync_and_compute
     assert set(timed) <= allowed, set(timed) - allowed
     # the warmup (before t0) calls the same run() and synchronises
     warm = _calls(body[:start])
     assert "run" in warm and "metric.reset" in warm
+    # barrier + device synchronize right before t0
+    assert _calls(body[start - 2:start]) == ["barrier", "device_sync"]
 
 
 def test_run_includes_compute():
