@@ -8,7 +8,7 @@ from torcheval_amd.metrics.functional.aggregation import (
     _auc_compute,
     _auc_update_input_check,
 )
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 
 __all__ = ["AUC"]
 
@@ -23,7 +23,7 @@ class AUC(Metric[torch.Tensor]):
         self.n_tasks = n_tasks
         self.reorder = reorder
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, x: torch.Tensor, y: torch.Tensor) -> "AUC":
         _auc_update_input_check(x, y, n_tasks=self.n_tasks)
         self.x.append(x.unsqueeze(0) if x.ndim == 1 else x)

@@ -4,7 +4,7 @@ from typing import Iterable, Optional
 
 import torch
 
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 
 __all__ = ["Cat"]
 
@@ -17,7 +17,7 @@ class Cat(Metric[torch.Tensor]):
         self._add_state("dim", dim)
         self._add_state("inputs", [])
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor) -> "Cat":
         self.inputs.append(input)
         return self

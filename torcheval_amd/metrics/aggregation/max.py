@@ -4,7 +4,7 @@ from typing import Iterable, Optional
 
 import torch
 
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 
 __all__ = ["Max"]
 
@@ -16,7 +16,7 @@ class Max(Metric[torch.Tensor]):
         super().__init__(device=device)
         self._add_state("max", torch.tensor(float("-inf"), device=self.device), merge="max")
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor) -> "Max":
         self.max = torch.max(self.max, torch.max(input))
         return self

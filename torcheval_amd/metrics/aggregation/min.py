@@ -4,7 +4,7 @@ from typing import Iterable, Optional
 
 import torch
 
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 
 __all__ = ["Min"]
 
@@ -16,7 +16,7 @@ class Min(Metric[torch.Tensor]):
         super().__init__(device=device)
         self._add_state("min", torch.tensor(float("inf"), device=self.device), merge="min")
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor) -> "Min":
         self.min = torch.min(self.min, torch.min(input))
         return self

@@ -5,7 +5,7 @@ from typing import Iterable, Optional
 
 import torch
 
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 
 _logger = logging.getLogger(__name__)
 
@@ -20,7 +20,7 @@ class Throughput(Metric[float]):
         self._add_state("num_total", 0.0)
         self._add_state("elapsed_time_sec", 0.0)
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, num_processed: int, elapsed_time_sec: float) -> "Throughput":
         if num_processed < 0:
             raise ValueError(

@@ -30,7 +30,7 @@ from torcheval_amd.metrics.functional.classification.accuracy import (
     _topk_multilabel_accuracy_update_input_check,
     _cpu_fast_ok,
 )
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 import torcheval_amd.ops as _ops
 from torcheval_amd.ops import compiling, native, native_loaded, use_native
 
@@ -297,7 +297,7 @@ class MultilabelAccuracy(MulticlassAccuracy):
         self.threshold = threshold
         self.criteria = criteria
 
-    @torch.inference_mode()
+    @inference_update
     def update(
         self: TMultilabelAccuracy, input: torch.Tensor, target: torch.Tensor
     ) -> TMultilabelAccuracy:
@@ -340,7 +340,7 @@ class TopKMultilabelAccuracy(MulticlassAccuracy):
         self.criteria = criteria
         self.k = k
 
-    @torch.inference_mode()
+    @inference_update
     def update(
         self: TTopKMultilabelAccuracy, input: torch.Tensor, target: torch.Tensor
     ) -> TTopKMultilabelAccuracy:

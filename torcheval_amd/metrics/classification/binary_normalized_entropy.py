@@ -13,7 +13,7 @@ from torcheval_amd.metrics.functional.classification.binary_normalized_entropy i
     _binary_normalized_entropy_update,
     _ne_device_error,
 )
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 
 TNormalizedEntropy = TypeVar("TNormalizedEntropy")
 
@@ -50,7 +50,7 @@ class BinaryNormalizedEntropy(Metric[torch.Tensor]):
                 name, torch.zeros(num_tasks, dtype=torch.float64, device=self.device), merge="sum"
             )
 
-    @torch.inference_mode()
+    @inference_update
     def update(
         self: TNormalizedEntropy,
         input: torch.Tensor,

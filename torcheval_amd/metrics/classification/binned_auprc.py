@@ -4,6 +4,8 @@ from typing import List, Optional, Union
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.classification.binned_auprc import (
     _binary_binned_auprc_param_check,
     _binary_binned_auprc_update_input_check,
@@ -43,7 +45,7 @@ class BinaryBinnedAUPRC(_BinnedCountsMetric):
     def _views(self):
         return self.num_tp.t(), self.num_fp.t(), self.num_fn.t()
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "BinaryBinnedAUPRC":
         input = input.to(self.device)
         target = target.to(self.device)
@@ -81,7 +83,7 @@ class MulticlassBinnedAUPRC(_BinnedCountsMetric):
         self.optimization = optimization
         self._init_counts((len(threshold), num_classes))
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "MulticlassBinnedAUPRC":
         input = input.to(self.device)
         target = target.to(self.device)
@@ -117,7 +119,7 @@ class MultilabelBinnedAUPRC(_BinnedCountsMetric):
         self.optimization = optimization
         self._init_counts((len(threshold), num_labels))
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "MultilabelBinnedAUPRC":
         input = input.to(self.device)
         target = target.to(self.device)

@@ -17,7 +17,7 @@ from torcheval_amd.metrics.functional.classification.confusion_matrix import (
     _confusion_matrix_update,
     _raise_confusion_err,
 )
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 from torcheval_amd.ops.classification import cls_counts, native_cls
 
 TMulticlassConfusionMatrix = TypeVar("TMulticlassConfusionMatrix")
@@ -121,7 +121,7 @@ class BinaryConfusionMatrix(MulticlassConfusionMatrix):
         super().__init__(num_classes=2, device=device, normalize=normalize)
         self.threshold = threshold
 
-    @torch.inference_mode()
+    @inference_update
     def update(
         self: TBinaryConfusionMatrix, input: torch.Tensor, target: torch.Tensor
     ) -> TBinaryConfusionMatrix:

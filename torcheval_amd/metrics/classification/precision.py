@@ -14,7 +14,7 @@ from torcheval_amd.metrics.functional.classification.precision import (
     _precision_update,
     _precision_update_input_check,
 )
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 from torcheval_amd.ops.classification import cls_counts, native_cls
 
 TPrecision = TypeVar("TPrecision")
@@ -104,7 +104,7 @@ class BinaryPrecision(MulticlassPrecision):
         super().__init__(num_classes=2, device=device)
         self.threshold = threshold
 
-    @torch.inference_mode()
+    @inference_update
     def update(self: TBinaryPrecision, input: torch.Tensor, target: torch.Tensor) -> TBinaryPrecision:
         """Update states with ``[N]`` scores and ``[N]`` binary targets."""
         input = input.to(self.device)

@@ -18,7 +18,7 @@ from typing import Any, Iterable, Optional, Union
 import torch
 from torch import nn, Tensor
 
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 from torcheval_amd.models.inception import FIDInceptionV3
 from torcheval_amd.ops import use_native
 
@@ -173,7 +173,7 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
         self._add_state("num_real_images", torch.tensor(0, device=self.device).int(), merge="sum")
         self._add_state("num_fake_images", torch.tensor(0, device=self.device).int(), merge="sum")
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, images: Tensor, is_real: bool) -> "FrechetInceptionDistance":
         """Add a batch of [B, 3, H, W] images (float32 in [0, 1] for the default model)."""
         self._FID_update_input_check(images=images, is_real=is_real)

@@ -84,6 +84,21 @@ def _instrument(fn: Callable, label: str, check_after: bool) -> Callable:
     return wrapper
 
 
+def inference_update(fn: Callable) -> Callable:
+    """``torch.inference_mode()`` for eager ``update()`` calls; a plain call while torch.compile
+    traces (states never require grad, and inference-mode views inside a compiled region break
+    inductor's storage bookkeeping)."""
+
+    @functools.wraps(fn)
+    def wrapper(*args, **kwargs):
+        if torch.compiler.is_compiling():
+            return fn(*args, **kwargs)
+        with torch.inference_mode():
+            return fn(*args, **kwargs)
+
+    return wrapper
+
+
 class Metric(Generic[TComputeReturn], ABC):
     """
     Base class for all metrics present in the Metrics API.

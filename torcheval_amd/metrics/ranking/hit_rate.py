@@ -2,6 +2,8 @@
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.ranking import hit_rate
 from torcheval_amd.metrics.ranking._score_list import _RankScoreList
 
@@ -11,7 +13,7 @@ __all__ = ["HitRate"]
 class HitRate(_RankScoreList):
     """Per-sample hit (target within top-k) scores, concatenated over updates."""
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "HitRate":
         self.scores.append(hit_rate(input, target, k=self.k, _err=self._err_for(input)))
         return self

@@ -2,6 +2,8 @@
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.ranking import reciprocal_rank
 from torcheval_amd.metrics.ranking._score_list import _RankScoreList
 
@@ -11,7 +13,7 @@ __all__ = ["ReciprocalRank"]
 class ReciprocalRank(_RankScoreList):
     """Per-sample reciprocal rank scores, concatenated over updates."""
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "ReciprocalRank":
         self.scores.append(reciprocal_rank(input, target, k=self.k, _err=self._err_for(input)))
         return self

@@ -31,7 +31,7 @@ from torcheval_amd.metrics.functional.ranking import (
     _retrieval_precision_param_check,
     _retrieval_precision_update_input_check,
 )
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 
 __all__ = ["RetrievalPrecision"]
 
@@ -84,7 +84,7 @@ class RetrievalPrecision(Metric[torch.Tensor]):
                 self._add_state(name, torch.zeros(Q, dtype=torch.float64, device=self.device), merge="sum")
 
     # ------------------------------------------------------------------ update
-    @torch.inference_mode()
+    @inference_update
     def update(
         self, input: torch.Tensor, target: torch.Tensor, indexes: Optional[torch.Tensor] = None
     ) -> "RetrievalPrecision":

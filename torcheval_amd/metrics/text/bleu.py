@@ -4,6 +4,8 @@ from typing import Optional, Sequence, Union
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.text import _bleu_score_compute, _bleu_score_update
 from torcheval_amd.metrics.text._sum_states import _SumStates
 
@@ -31,7 +33,7 @@ class BLEUScore(_SumStates):
         self._add_state("matches_by_order", torch.zeros(n_gram, dtype=f64, device=self.device), merge="sum")
         self._add_state("possible_matches_by_order", torch.zeros(n_gram, dtype=f64, device=self.device), merge="sum")
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: Union[str, Sequence[str]], target: Sequence[Union[str, Sequence[str]]]) -> "BLEUScore":
         il, tl, m, p = _bleu_score_update(input, target, self.n_gram, self.device)
         self.input_len += il

@@ -4,6 +4,8 @@ from typing import List, Optional, Union
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.text import (
     _word_error_rate_compute,
     _word_error_rate_update,
@@ -23,7 +25,7 @@ class WordErrorRate(_SumStates):
         self._add_state("errors", torch.tensor(0, dtype=torch.float, device=self.device), merge="sum")
         self._add_state("total", torch.tensor(0, dtype=torch.float, device=self.device), merge="sum")
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: Union[str, List[str]], target: Union[str, List[str]]) -> "WordErrorRate":
         errors, total = _word_error_rate_update(input, target)
         self.errors += errors.to(self.device)

@@ -4,6 +4,8 @@ from typing import List, Optional, Union
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.text import _wil_compute, _wil_update
 from torcheval_amd.metrics.text._sum_states import _SumStates
 
@@ -20,7 +22,7 @@ class WordInformationLost(_SumStates):
         for n in self._names:
             self._add_state(n, torch.tensor(0.0, dtype=torch.float64, device=self.device), merge="sum")
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: Union[str, List[str]], target: Union[str, List[str]]) -> "WordInformationLost":
         c, t, p = _wil_update(input, target)
         self.correct_total += c.to(self.device)

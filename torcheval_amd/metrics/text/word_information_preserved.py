@@ -4,6 +4,8 @@ from typing import List, Optional, Union
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.text import (
     _word_information_preserved_compute,
     _word_information_preserved_update,
@@ -23,7 +25,7 @@ class WordInformationPreserved(_SumStates):
         for n in self._names:
             self._add_state(n, torch.tensor(0, dtype=torch.float64, device=self.device), merge="sum")
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: Union[str, List[str]], target: Union[str, List[str]]) -> "WordInformationPreserved":
         c, t, i = _word_information_preserved_update(input, target)
         self.correct_total += c.to(self.device)

@@ -16,7 +16,7 @@ from torcheval_amd.metrics.functional.classification.auroc import (
     _binary_auroc_compute,
     _binary_auroc_update_input_check,
 )
-from torcheval_amd.metrics.metric import Metric
+from torcheval_amd.metrics.metric import Metric, inference_update
 from torcheval_amd.metrics.window._ring import _check_window_args
 
 
@@ -40,7 +40,7 @@ class WindowedBinaryAUROC(Metric[torch.Tensor]):
         for name in ("inputs", "targets", "weights"):
             self._add_state(name, torch.zeros(num_tasks, max_num_samples, device=self.device))
 
-    @torch.inference_mode()
+    @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor, weight: Optional[torch.Tensor] = None):
         if weight is None:
             weight = torch.ones_like(input, dtype=torch.double)

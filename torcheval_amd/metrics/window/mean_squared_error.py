@@ -6,6 +6,8 @@ from typing import Optional, Tuple, Union
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.regression import (
     _mean_squared_error_compute,
     _mean_squared_error_param_check,
@@ -36,7 +38,7 @@ class WindowedMeanSquaredError(_WindowedSums):
         )
         self.multioutput = multioutput
 
-    @torch.inference_mode()
+    @inference_update
     def update(
         self, input: torch.Tensor, target: torch.Tensor, *, sample_weight: Optional[torch.Tensor] = None
     ):

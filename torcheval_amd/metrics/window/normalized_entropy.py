@@ -7,6 +7,8 @@ from typing import Optional, Tuple, Union
 
 import torch
 
+from torcheval_amd.metrics.metric import inference_update
+
 from torcheval_amd.metrics.functional.classification.binary_normalized_entropy import (
     _baseline_update,
     _binary_normalized_entropy_update,
@@ -47,7 +49,7 @@ class WindowedBinaryNormalizedEntropy(_WindowedSums):
         self.from_logits = from_logits
         self._err: Optional[torch.Tensor] = None
 
-    @torch.inference_mode()
+    @inference_update
     def update(
         self, input: torch.Tensor, target: torch.Tensor, *, weight: Optional[torch.Tensor] = None
     ):
