@@ -191,7 +191,7 @@ void cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t nu
 // the general Python path (which raises the reference's own errors).  One pybind call with
 // four positional tensors instead of the 15-argument cls_counts plus its Python-side checks.
 bool micro_accuracy_update(const Tensor& input, const Tensor& target, const Tensor& correct,
-                           const Tensor& total, int64_t num_classes) {
+                           const Tensor& total, int64_t num_classes, const optional<Tensor>& pend) {
   if (!input.is_cuda() || input.dim() != 2 || target.dim() != 1) return false;
   const int64_t n = input.size(0), c = input.size(1);
   if (target.size(0) != n || c <= 0 || c >= (int64_t(1) << 31) || input.stride(1) != 1) return false;
@@ -225,9 +225,39 @@ bool micro_accuracy_update(const Tensor& input, const Tensor& target, const Tens
   a.micro_correct = correct.data_ptr<float>();
   a.micro_total = total.data_ptr<float>();
   const hipStream_t stream = stream_for(input);
-  a.fold_ws = fold_workspace(input, stream);
+  if (pend.has_value()) {
+    if (pend->scalar_type() != at::kLong || pend->numel() < tea::kPendCells * tea::kPendStride ||
+        pend->device() != dev || !pend->is_contiguous())
+      return false;
+    a.pend = reinterpret_cast<unsigned long long*>(pend->data_ptr<int64_t>());
+  } else {
+    a.fold_ws = fold_workspace(input, stream);
+  }
   check_launch(tea::launch_cls_counts(a, stream), "micro_accuracy_update");
   return true;
+}
+
+// Fold the K1 micro kernel's pending cells into ``correct`` (cells zeroed); with ``out``, also
+// write correct / total there: the deferred fold and the accuracy division in one launch.
+void micro_accuracy_finish(const Tensor& pend, const Tensor& correct, const Tensor& total,
+                           const optional<Tensor>& out) {
+  check_gpu(pend, "pend");
+  TORCH_CHECK(pend.scalar_type() == at::kLong && pend.is_contiguous() &&
+                  pend.numel() >= tea::kPendCells * tea::kPendStride,
+              "micro_accuracy_finish: pend must be int64 [>= 512]");
+  TORCH_CHECK(correct.scalar_type() == at::kFloat && total.scalar_type() == at::kFloat && correct.numel() == 1 &&
+                  total.numel() == 1 && correct.device() == pend.device() && total.device() == pend.device(),
+              "micro_accuracy_finish: float32 scalar states on the pending cells' device");
+  float* o = nullptr;
+  if (out.has_value()) {
+    TORCH_CHECK(out->scalar_type() == at::kFloat && out->numel() == 1 && out->device() == pend.device(),
+                "micro_accuracy_finish: out must be a float32 scalar");
+    o = out->data_ptr<float>();
+  }
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(pend.device());
+  check_launch(tea::launch_micro_finish(reinterpret_cast<unsigned long long*>(pend.data_ptr<int64_t>()),
+                                        correct.data_ptr<float>(), total.data_ptr<float>(), o, stream_for(pend)),
+               "micro_accuracy_finish");
 }
 
 // ---------------------------------------------------------------- K10 rank-of-target scores
@@ -1260,7 +1290,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"), py::arg("ws"), py::arg("offs"), py::arg("counts"), py::arg("dtypes"), py::arg("ops"));
   m.def("micro_accuracy_update", &micro_accuracy_update,
         "K1 micro accuracy (k=1) accumulated into float32 scalar states; false = not handled", py::arg("input"),
-        py::arg("target"), py::arg("correct"), py::arg("total"), py::arg("num_classes") = 0);
+        py::arg("target"), py::arg("correct"), py::arg("total"), py::arg("num_classes") = 0,
+        py::arg("pend") = py::none());
+  m.def("micro_accuracy_finish", &micro_accuracy_finish,
+        "fold the micro kernel's pending cells into correct (and write correct / total to out)", py::arg("pend"),
+        py::arg("correct"), py::arg("total"), py::arg("out") = py::none());
   m.def("cls_counts", &cls_counts, "K1 fused classification counts", py::arg("input"),
         py::arg("target"), py::arg("k"), py::arg("num_classes"), py::arg("micro_correct"),
         py::arg("micro_total"), py::arg("cls_correct"), py::arg("cls_label"),
@@ -1379,7 +1413,7 @@ void op_cls_counts(const Tensor& input, const Tensor& target, int64_t k, int64_t
 
 // ---- dispatcher wrappers of the remaining entry points (schemas below annotate mutation)
 void op_micro_accuracy(const Tensor& input, const Tensor& target, const Tensor& correct, const Tensor& total) {
-  TORCH_CHECK(micro_accuracy_update(input, target, correct, total, 0),
+  TORCH_CHECK(micro_accuracy_update(input, target, correct, total, 0, c10::nullopt),
               "micro_accuracy: unsupported input (needs [N, C] f32/bf16/f16 scores with unit column stride, "
               "[N] integer targets and float32 scalar states on one ROCm device)");
 }
@@ -1446,7 +1480,7 @@ void op_seg_reduce_rows(const Tensor& rows, const Tensor& out, int64_t ws, at::I
 
 TORCH_LIBRARY(torcheval_amd, m) {
   m.def("micro_accuracy(Tensor input, Tensor target, Tensor(a!) correct, Tensor(b!) total) -> ()");
-  m.def("rank_scores(Tensor input, Tensor target, int mode, int k, Tensor(a!)? err) -> Tensor");
+  m.def("rank_scores(Tensor input, Tensor target, int score_mode, int k, Tensor(a!)? err) -> Tensor");
   m.def("binary_counts(Tensor input, Tensor target, Tensor? weight, float threshold, Tensor(a!)? tp, "
         "Tensor(b!)? fp, Tensor(c!)? tn, Tensor(d!)? fn, Tensor(e!)? total, int strict) -> ()");
   m.def("curve_count(Tensor sorted, Tensor order, Tensor target, bool class_mode, int payload_kind, "
@@ -1457,7 +1491,7 @@ TORCH_LIBRARY(torcheval_amd, m) {
   m.def("merge_sorted_runs(Tensor[] keys, Tensor[] payloads) -> Tensor[]");
   m.def("retrieval_topk_update(Tensor x, Tensor t, Tensor? q, Tensor(a!) topk, Tensor(b!) target, "
         "Tensor(c!) count) -> ()");
-  m.def("binned_counts(Tensor input, Tensor target, Tensor thr, int mode, Tensor(a!) tp, Tensor(b!) fp, "
+  m.def("binned_counts(Tensor input, Tensor target, Tensor thr, int target_mode, Tensor(a!) tp, Tensor(b!) fp, "
         "Tensor(c!) fn, int uniform) -> ()");
   m.def("column_moments(Tensor? x, Tensor? t, Tensor? w, Tensor(a!)? sse, Tensor(b!)? st, Tensor(c!)? stt, "
         "Tensor(d!)? sx, Tensor(e!)? sw, int overwrite, int mse_mode, Tensor(f!)? mse_out, int num_regressors) -> ()");

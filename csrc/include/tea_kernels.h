@@ -34,9 +34,16 @@ struct ClsCountsArgs {
   int* err_max = nullptr;        // optional [2]: largest target / prediction >= num_classes
   int check_target = 0;          // flag bad targets even without histograms
   unsigned long long* fold_ws = nullptr;  // tea_fold.h cells (per-stream, self-cleaning)
+  // micro kernel only: per-wave correct counts go to these 64 pending cells (u64, 64-B stride)
+  // instead of the fold into micro_correct; launch_micro_finish folds them later
+  unsigned long long* pend = nullptr;
   int max_blocks = 0;
 };
 int launch_cls_counts(const ClsCountsArgs& a, hipStream_t stream);
+// pending cells -> correct (+= their sum, cells zeroed); out = correct / total when given
+constexpr int kPendCells = 64;
+constexpr int kPendStride = 8;
+int launch_micro_finish(unsigned long long* pend, float* correct, const float* total, float* out, hipStream_t stream);
 
 struct BinaryCountsArgs {
   const void* input = nullptr;

@@ -23,6 +23,8 @@
 //  * "narrow" kernel (C <= 32): one thread per row, LDS-privatised class histograms.
 //  * invalid targets / predictions never fault: they are skipped and flagged in ``err``
 //    (bit 0: target out of range, bit 1: predicted label out of range).
+#include <cstdlib>
+
 #include "tea_common.h"
 #include "tea_fold.h"
 #include "tea_kernels.h"
@@ -319,6 +321,128 @@ __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
   block_micro(a, correct_acc, rows_acc);
 }
 
+
+// ---------------------------------------------------------------- micro accuracy (k = 1)
+// The north-star update (MulticlassAccuracy micro, bs 8192 x C 1000): one wave per row, the
+// row's 4 x 16-B loads per lane and the target's scalar load all in flight together.  What the
+// A/B harness showed (csrc/bench/k1_v3.hip, profiles/k1_v3_ab_r3.md): the per-row work runs
+// after the row's LAST load lands, and the loads of all 8192 waves land near the end of the
+// stream, so every VALU instruction per row sits on the kernel's tail.  This body keeps it to
+// ~40: a v_maximum3 tree over the lane's values, a DPP wave max (quad perms + half/full row
+// mirrors, 4 readlanes) in place of six ds_bpermute round trips, and the target's own score
+// by ONE uniform register-indexed move (s_set_gpr_idx_on + v_mov from the owner lane's
+// register, then a readlane) in place of a select per element.  Only rows whose target holds
+// the max count the other columns equal to it (ballots + scalar popcounts); a second holder
+// or a NaN row takes the exact torch.argmax path.  Lanes past C re-read the row's first
+// columns (clamped addresses), which cannot change the max and are masked out of the count.
+// Replaces reference accuracy.py:260-278 (argmax -> eq -> long -> sum, plus a host tensor).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+
+__device__ __forceinline__ float wave_max_dpp(float x) {  // NaN-propagating, wave-uniform
+  x = fmaximum(x, dpp_f32<0xB1>(x));   // quad_perm [1,0,3,2]
+  x = fmaximum(x, dpp_f32<0x4E>(x));   // quad_perm [2,3,0,1]
+  x = fmaximum(x, dpp_f32<0x141>(x));  // row_half_mirror
+  x = fmaximum(x, dpp_f32<0x140>(x));  // row_mirror: every lane holds its 16-lane row max
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), 48));
+  return fmaximum(fmaximum(r0, r1), fmaximum(r2, r3));
+}
+
+template <int NV>
+struct RowVals;
+template <>
+struct RowVals<16> {
+  typedef float type __attribute__((ext_vector_type(16)));
+};
+template <>
+struct RowVals<32> {
+  typedef float type __attribute__((ext_vector_type(32)));
+};
+
+// KIND 0: f32 (4 floats per 16-B load), 1: bf16, 2: f16 (8 per load); TGT: int64_t / int32_t
+template <int KIND, typename TGT>
+__global__ __launch_bounds__(kBlock) void cls_micro_kernel(ClsCountsArgs a) {
+  constexpr int VEC = KIND == 0 ? 4 : 8;
+  constexpr int NV = kChunkLoads * VEC;  // values per lane
+  constexpr int STEP = kWave * VEC;      // columns per wave-load
+  constexpr int ELSIZE = KIND == 0 ? 4 : 2;
+  typedef typename RowVals<NV>::type vec_t;
+  const int lane = lane_id();
+  const int C = static_cast<int>(a.c);
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  uint32_t correct_acc = 0, rows_acc = 0;
+  for (int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id(); row < a.n; row += nwaves) {
+    const char* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELSIZE;
+    float f[kChunkLoads][VEC];
+#pragma unroll
+    for (int u = 0; u < kChunkLoads; ++u) {
+      const int col = u * STEP + lane * VEC;
+      load_vec<KIND, VEC>(rp, col < C ? col : 0, f[u]);
+    }
+    const int64_t t = static_cast<const TGT*>(a.target)[row];
+    vec_t v;
+#pragma unroll
+    for (int u = 0; u < kChunkLoads; ++u)
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) v[u * VEC + e] = f[u][e];
+    float m = fmaximum(v[0], v[1]);
+#pragma unroll
+    for (int e = 2; e < NV; ++e) m = fmaximum(m, v[e]);
+    const float wm = wave_max_dpp(m);
+    bool correct = false;
+    if (__builtin_expect(wm != wm, 0)) {  // NaN in the row: exact torch.argmax semantics
+      correct = row_argmax_exact<KIND>(rp, C, lane) == t;
+    } else if (t >= 0 && t < C) {
+      const int tu = static_cast<int>(t);
+      const float sel = v[(tu / STEP) * VEC + (tu % VEC)];  // uniform index: one indexed move
+      const float xt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sel), (tu % STEP) / VEC));
+      if (xt == wm) {  // the target holds the max: correct iff it is the only column that does
+        int cnt = 0;
+#pragma unroll
+        for (int u = 0; u < kChunkLoads; ++u) {
+          const int valid = min(max((C - u * STEP + VEC - 1) / VEC, 0), kWave);
+          const uint64_t lanes = valid >= kWave ? ~0ull : ((1ull << valid) - 1);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) cnt += __builtin_popcountll(__ballot(v[u * VEC + e] == wm) & lanes);
+        }
+        correct = cnt == 1 || row_argmax_exact<KIND>(rp, C, lane) == t;
+      }
+    }
+    if (lane == 0) {
+      correct_acc += correct;
+      rows_acc += 1;
+    }
+  }
+  if (a.pend) {
+    // deferred fold: one no-return atomic per wave into one of 64 pending cells, no LDS, no
+    // block barrier, no returning atomic on the kernel's tail (the fold's ~0.6 us + the block
+    // reduction's ~0.45 us in the A/B harness); the metric folds the cells at compute / sync
+    if (lane == 0 && correct_acc)
+      atomicAdd(a.pend + ((blockIdx.x * kWavesPerBlock + wave_id()) % kPendCells) * kPendStride,
+                static_cast<unsigned long long>(correct_acc));
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.micro_total) atomicAdd(a.micro_total, static_cast<float>(a.n));
+    return;
+  }
+  block_micro(a, correct_acc, rows_acc);
+}
+
+__global__ __launch_bounds__(kWave) void micro_finish_kernel(unsigned long long* pend, float* correct,
+                                                             const float* total, float* out) {
+  unsigned long long* cell = pend + threadIdx.x * kPendStride;
+  const unsigned long long s = wave_sum(*cell);
+  *cell = 0ull;
+  if (threadIdx.x == 0) {
+    const float c = correct[0] + static_cast<float>(s);
+    correct[0] = c;
+    if (out) out[0] = c / total[0];
+  }
+}
+
 template <int KIND, int VEC, bool TOPK, bool PRED = true>
 __global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
   // (amdgpu_waves_per_eu(8, 8) on the f32 kernels - 64 VGPRs, every row of an 8192-row batch
@@ -448,6 +572,22 @@ void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
   constexpr int kChunkCols = kWave * VEC * kChunkLoads;
   const bool pred_free = a.cls_pred == nullptr && a.cls_fp == nullptr && a.confusion == nullptr &&
                          a.c <= kChunkCols;
+  // pure micro counts (no class histograms, no label validation) with 64/32-bit targets
+  // (TORCHEVAL_AMD_K1_MICRO=0 keeps the general kernel: A/B switch for profiling)
+  static const bool micro_on = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K1_MICRO");
+    return e == nullptr || std::atoi(e) != 0;
+  }();
+  const bool micro_only = micro_on && pred_free && VEC > 1 && a.k == 1 && a.cls_correct == nullptr &&
+                          a.cls_label == nullptr && a.err == nullptr && a.err_max == nullptr && !a.check_target;
+  if (micro_only && a.tg_dt == DType::i64) {
+    hipLaunchKernelGGL((cls_micro_kernel<KIND, int64_t>), dim3(grid), dim3(kBlock), 0, s, a);
+    return;
+  }
+  if (micro_only && a.tg_dt == DType::i32) {
+    hipLaunchKernelGGL((cls_micro_kernel<KIND, int32_t>), dim3(grid), dim3(kBlock), 0, s, a);
+    return;
+  }
   if (a.k > 1)
     hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, true>), dim3(grid), dim3(kBlock), 0, s, a);
   else if (pred_free)
@@ -493,6 +633,12 @@ int launch_cls_counts(const ClsCountsArgs& a, hipStream_t stream) {
     const int grid = stream_grid(a.n, kBlock, cap);
     hipLaunchKernelGGL(cls_labels_kernel, dim3(grid), dim3(kBlock), 0, stream, a);
   }
+  return static_cast<int>(hipGetLastError());
+}
+
+int launch_micro_finish(unsigned long long* pend, float* correct, const float* total, float* out,
+                        hipStream_t stream) {
+  hipLaunchKernelGGL(micro_finish_kernel, dim3(1), dim3(kPendCells), 0, stream, pend, correct, total, out);
   return static_cast<int>(hipGetLastError());
 }
 

@@ -106,6 +106,12 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         self.num_classes = num_classes
         self.k = k
         self._err: Optional[torch.Tensor] = None
+        # K1 micro kernel: correct counts of the launches since the last fold, in 64 int64
+        # cells (one no-return atomic per wave, no grid-wide fold on the update's tail);
+        # ``num_correct`` folds them in on its next read (compute, sync, state_dict, merge)
+        self._pend: Optional[torch.Tensor] = None
+        self._pend_id = 0
+        self._pend_dirty = False
         shape = () if average == "micro" else (num_classes or 0,)
         self._add_state("num_correct", torch.zeros(shape, device=self.device), merge="sum")
         self._add_state("num_total", torch.zeros(shape, device=self.device), merge="sum")
@@ -133,9 +139,56 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         self._fast_nc = self.num_classes or 0
 
     def to(self: TAccuracy, device, *args, **kwargs) -> TAccuracy:
-        super().to(device, *args, **kwargs)
+        super().to(device, *args, **kwargs)  # reads (so folds) num_correct first
+        self._pend = None
         self._refresh_fast_path()
         return self
+
+    # -- num_correct with the deferred fold of the K1 micro kernel's pending cells
+    def _get_num_correct(self) -> torch.Tensor:
+        d = self.__dict__
+        if d.get("_pend_dirty"):
+            self._fold_pending()
+        return d["num_correct"]
+
+    def _set_num_correct(self, value: torch.Tensor) -> None:
+        d = self.__dict__
+        if d.get("_pend_dirty"):  # the pending counts belong to the value being replaced
+            d["_pend"].zero_()
+            d["_pend_dirty"] = False
+        d["num_correct"] = value
+
+    num_correct = property(_get_num_correct, _set_num_correct)
+
+    def _fold_pending(self, out: Optional[torch.Tensor] = None) -> None:
+        d = self.__dict__
+        native().micro_accuracy_finish(d["_pend"], d["num_correct"], d["num_total"], out)
+        d["_pend_dirty"] = False
+
+    def _mark_updated(self) -> None:
+        """Called after a HIP-graph replay of ``update`` (torcheval_amd.utils.graphs)."""
+        if self.__dict__.get("_pend") is not None:
+            self.__dict__["_pend_dirty"] = True
+
+    def __getstate__(self):
+        # copies (copy / deepcopy / pickle) carry folded states and no pending cells
+        d = self.__dict__
+        if d.get("_pend_dirty"):
+            self._fold_pending()
+        state = dict(d)
+        state["_pend"] = None
+        state["_pend_dirty"] = False
+        return state
+
+    def __setstate__(self, state) -> None:
+        self.__dict__.update(state)
+
+    def reset(self: TAccuracy) -> TAccuracy:
+        d = self.__dict__
+        if d.get("_pend_dirty"):
+            d["_pend"].zero_()
+            d["_pend_dirty"] = False
+        return super().reset()
 
     def update(self: TAccuracy, input: torch.Tensor, target: torch.Tensor) -> TAccuracy:
         """
@@ -144,7 +197,13 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         """
         if self._fast:
             if not compiling():
-                if _FAST_MICRO(input, target, self.num_correct, self.num_total, self._fast_nc):
+                d = self.__dict__
+                pend = d["_pend"]
+                if pend is None or d["_pend_id"] != id(self):
+                    pend = d["_pend"] = torch.zeros(512, dtype=torch.int64, device=self._device)
+                    d["_pend_id"] = id(self)
+                if _FAST_MICRO(input, target, d["num_correct"], d["num_total"], self._fast_nc, pend):
+                    d["_pend_dirty"] = True
                     return self
             elif _micro_op_ok(input, target, self.num_correct, self._fast_nc):
                 torch.ops.torcheval_amd.micro_accuracy(input, target, self.num_correct, self.num_total)
@@ -210,7 +269,11 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         # hold the launch back.  The states never require grad, so no autograd graph is
         # recorded; the inference_mode context (~4 us of host time) is only entered for the
         # macro path's masked indexing.
-        if self.average == "micro" or self.average is None or self.average == "none":
+        d = self.__dict__
+        if d.get("_pend_dirty"):  # fold the pending cells and divide: one launch
+            out = torch.empty((), dtype=torch.float32, device=d["num_total"].device)
+            self._fold_pending(out)
+        elif self.average == "micro" or self.average is None or self.average == "none":
             out = self.num_correct / self.num_total
         else:
             with torch.inference_mode():

@@ -364,7 +364,8 @@ def _sync_one(m, sb: StateBuffer, plan: _Plan):
             merged = _reduce_gathered(merged, plan.segs, ws, plan.row_bytes)
     r = object.__new__(type(m))  # a shallow copy (copy.copy costs ~4x this)
     d = r.__dict__
-    d.update(m.__dict__)
+    getstate = getattr(type(m), "__getstate__", None)
+    d.update(m.__dict__ if getstate is None else getstate(m))
     d["_tea_sb"] = None
     typed = {}
     for name, big, dtype, eo, n, shape in plan.assign:

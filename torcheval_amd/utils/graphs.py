@@ -97,4 +97,7 @@ class GraphedUpdate:
             if src.data_ptr() != dst.data_ptr():
                 dst.copy_(src, non_blocking=True)
         self.graph.replay()
+        mark = getattr(self.metric, "_mark_updated", None)
+        if mark is not None:  # metrics with deferred folds (K1 micro's pending cells)
+            mark()
         return self.metric
