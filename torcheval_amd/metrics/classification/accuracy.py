@@ -145,24 +145,26 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         return self
 
     # -- num_correct with the deferred fold of the K1 micro kernel's pending cells
+    # (the tensor lives under "_nc": an instance-dict key named like the property confuses
+    # torch.compile's tracing of the property)
     def _get_num_correct(self) -> torch.Tensor:
         d = self.__dict__
         if d.get("_pend_dirty"):
             self._fold_pending()
-        return d["num_correct"]
+        return d["_nc"]
 
     def _set_num_correct(self, value: torch.Tensor) -> None:
         d = self.__dict__
         if d.get("_pend_dirty"):  # the pending counts belong to the value being replaced
             d["_pend"].zero_()
             d["_pend_dirty"] = False
-        d["num_correct"] = value
+        d["_nc"] = value
 
     num_correct = property(_get_num_correct, _set_num_correct)
 
     def _fold_pending(self, out: Optional[torch.Tensor] = None) -> None:
         d = self.__dict__
-        native().micro_accuracy_finish(d["_pend"], d["num_correct"], d["num_total"], out)
+        native().micro_accuracy_finish(d["_pend"], d["_nc"], d["num_total"], out)
         d["_pend_dirty"] = False
 
     def _mark_updated(self) -> None:
@@ -202,7 +204,7 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
                 if pend is None or d["_pend_id"] != id(self):
                     pend = d["_pend"] = torch.zeros(512, dtype=torch.int64, device=self._device)
                     d["_pend_id"] = id(self)
-                if _FAST_MICRO(input, target, d["num_correct"], d["num_total"], self._fast_nc, pend):
+                if _FAST_MICRO(input, target, d["_nc"], d["num_total"], self._fast_nc, pend):
                     d["_pend_dirty"] = True
                     return self
             elif _micro_op_ok(input, target, self.num_correct, self._fast_nc):

@@ -310,7 +310,7 @@ class _Plan:
 
     __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large")
 
-    def __init__(self, sb: StateBuffer, group, ws: int) -> None:
+    def __init__(self, sb: StateBuffer, group, ws: int, metric) -> None:
         from torch.distributed.distributed_c10d import _get_default_group
 
         self.group = group  # held: keeps id(group) from being reused while the plan lives
@@ -321,23 +321,26 @@ class _Plan:
         self.row_bytes = sb.gather_bytes
         self.segs = sb.segments(0)
         self.large = [(g.off, g.nbytes, g.dtype, g.op) for g in sb.groups if g.off < sb.reduce_end]
-        # (name, from the reduce snapshot?, dtype, element offset, numel, shape or None for 0-dim):
-        # states are indexed out of ONE typed view per (source, dtype)
+        # (name, from the reduce snapshot?, dtype, element offset, numel, shape or None for 0-dim,
+        # set through the class's property?): states are indexed out of ONE typed view per
+        # (source, dtype)
         self.assign = []
+        cls = type(metric)
         for g in sb.groups:
             big = g.off < sb.reduce_end
             es = _esize(g.dtype)
             for name, shape, boff, n in g.members:
                 o = (g.off if big else g.off - sb.gather_off) + boff
-                self.assign.append((name, big, g.dtype, o // es, n, shape if shape else None))
+                prop = isinstance(getattr(cls, name, None), property)
+                self.assign.append((name, big, g.dtype, o // es, n, shape if shape else None, prop))
         self.flag = (sb.flag_off - sb.gather_off, 4 * sb.flag_words) if sb.flag_words else None
 
 
-def _plan_for(sb: StateBuffer, group, ws: int) -> _Plan:
+def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
     key = (id(group), ws)
     plan = sb.plans.get(key)
     if plan is None or plan.group is not group:
-        plan = sb.plans[key] = _Plan(sb, group, ws)
+        plan = sb.plans[key] = _Plan(sb, group, ws, metric)
     return plan
 
 
@@ -368,12 +371,16 @@ def _sync_one(m, sb: StateBuffer, plan: _Plan):
     d.update(m.__dict__ if getstate is None else getstate(m))
     d["_tea_sb"] = None
     typed = {}
-    for name, big, dtype, eo, n, shape in plan.assign:
+    for name, big, dtype, eo, n, shape, prop in plan.assign:
         key = (big, dtype)
         t = typed.get(key)
         if t is None:
             t = typed[key] = (snap if big else merged).view(dtype)
-        d[name] = t[eo] if shape is None else t[eo : eo + n].view(shape)
+        v = t[eo] if shape is None else t[eo : eo + n].view(shape)
+        if prop:
+            setattr(r, name, v)
+        else:
+            d[name] = v
     if plan.flag is not None:
         o, nb = plan.flag
         d["_err"] = merged[o : o + nb].view(torch.int32)
@@ -388,7 +395,7 @@ def sync_single(m, group, ws: int):
         sb = StateBuffer.build(m)
         if sb is None:
             return None
-    plan = _plan_for(sb, group, ws)
+    plan = _plan_for(sb, group, ws, m)
     if plan.nccl and sb.device.type != "cuda":
         return None
     return _sync_one(m, sb, plan)
@@ -405,7 +412,7 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
         sb = buffer_of(m)
         if sb is None:
             return None
-        plan = _plan_for(sb, group, ws)
+        plan = _plan_for(sb, group, ws, m)
         if plan.nccl and sb.device.type != "cuda":
             return None
         return {key: _sync_one(m, sb, plan)}
