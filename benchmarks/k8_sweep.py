@@ -45,6 +45,13 @@ def main():
             act = torch.randn(K, D, device="cuda")
             out = torch.empty(D, D, device="cuda")
             t_mm = timeit(lambda: torch.mm(act.T, act, out=out))
+            cacc, sacc = torch.zeros(D, D, device="cuda"), torch.zeros(D, device="cuda")
+
+            def lib_update():  # what the metric update would run on the library path
+                cacc.addmm_(act.T, act)
+                sacc.add_(act.sum(0))
+
+            t_lib = timeit(lib_update)
             ref = act.double().T @ act.double()
             for sp in args.splits:
                 if sp > 0:
@@ -58,7 +65,8 @@ def main():
                 t_k8 = timeit(lambda: native().fid_cov_update(act, cov, cs))
                 flops_tri = 2.0 * K * 96 * 96 * T * (T + 1) / 2
                 row = {"D": D, "K": K, "split": sp, "k8_us": round(t_k8, 2), "gemm_us": round(t_mm, 2),
-                       "speedup_vs_gemm": round(t_mm / t_k8, 2), "k8_tflops_tri": round(flops_tri / t_k8 / 1e6, 1),
+                       "speedup_vs_gemm": round(t_mm / t_k8, 2), "lib_update_us": round(t_lib, 2),
+                       "speedup_vs_lib_update": round(t_lib / t_k8, 2), "k8_tflops_tri": round(flops_tri / t_k8 / 1e6, 1),
                        "gemm_tflops": round(2.0 * K * D * D / t_mm / 1e6, 1), "max_rel_err": err}
                 rows.append(row)
                 print(json.dumps(row), flush=True)

@@ -1245,6 +1245,37 @@ void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>&
 }
 
 
+// ---------------------------------------------------------------- C3 flags inside the all-reduce
+void snapshot_flags(const Tensor& src, const Tensor& dst, const optional<Tensor>& err, int64_t words, int64_t rank,
+                    int64_t ws) {
+  check_gpu(src, "src");
+  TORCH_CHECK(src.scalar_type() == at::kByte && dst.scalar_type() == at::kByte && src.is_contiguous() &&
+                  dst.is_contiguous() && dst.device() == src.device() && src.numel() % 16 == 0 &&
+                  dst.numel() == src.numel() + ws * words * 8,
+              "snapshot_flags: uint8 src [16k] and dst [src + ws * words * 8] on one device");
+  const int* e = nullptr;
+  if (err.has_value()) {
+    TORCH_CHECK(err->scalar_type() == at::kInt && err->numel() >= words && err->device() == src.device(),
+                "snapshot_flags: err must be int32 [>= words]");
+    e = err->data_ptr<int>();
+  }
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
+  check_launch(tea::launch_snapshot_flags(src.data_ptr(), dst.data_ptr(), src.numel(), e, (int)words, (int)rank, (int)ws,
+                                          stream_for(src)),
+               "snapshot_flags");
+}
+
+void merge_flag_slots(const Tensor& slots, const Tensor& out, int64_t words, int64_t ws) {
+  check_gpu(slots, "slots");
+  TORCH_CHECK(slots.scalar_type() == at::kFloat && slots.is_contiguous() && slots.numel() == ws * words * 2 &&
+                  out.scalar_type() == at::kInt && out.numel() == words && out.device() == slots.device(),
+              "merge_flag_slots: float32 [ws * words * 2] slots and int32 [words] out");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(slots.device());
+  check_launch(tea::launch_merge_flag_slots(slots.data_ptr<float>(), out.data_ptr<int>(), (int)words, (int)ws,
+                                            stream_for(slots)),
+               "merge_flag_slots");
+}
+
 // ---------------------------------------------------------------- C3 gathered-state reduction
 void seg_reduce_rows(const Tensor& rows, const Tensor& out, int64_t ws, at::IntArrayRef offs,
                      at::IntArrayRef counts, at::IntArrayRef dtypes, at::IntArrayRef ops) {
@@ -1285,6 +1316,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("ARCH") = "gfx950";
   m.def("rank_scores", &rank_scores, "K10 rank-of-target scores (hit rate / reciprocal rank)",
         py::arg("input"), py::arg("target"), py::arg("mode"), py::arg("k"), py::arg("err") = py::none());
+  m.def("snapshot_flags", &snapshot_flags, "C3 snapshot of a state region + this rank's flag slot (f32 hi/lo)",
+        py::arg("src"), py::arg("dst"), py::arg("err"), py::arg("words"), py::arg("rank"), py::arg("ws"));
+  m.def("merge_flag_slots", &merge_flag_slots, "C3 summed flag slots -> int32 words (max over ranks)",
+        py::arg("slots"), py::arg("out"), py::arg("words"), py::arg("ws"));
   m.def("seg_reduce_rows", &seg_reduce_rows,
         "C3 reduce a gathered [ws][row] state buffer per (op, dtype) segment in one launch", py::arg("rows"),
         py::arg("out"), py::arg("ws"), py::arg("offs"), py::arg("counts"), py::arg("dtypes"), py::arg("ops"));

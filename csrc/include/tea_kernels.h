@@ -498,4 +498,10 @@ struct SegReduceArgs {
   int op[kSegMax] = {};
 };
 int launch_seg_reduce(const SegReduceArgs& a, hipStream_t stream);
+// copy ``bytes`` (multiple of 16) of src to dst and append this rank's flag words as f32 (hi16,
+// lo16) pairs in slot ``rank`` of a zeroed [ws][words][2] block (err null: zeros)
+int launch_snapshot_flags(const void* src, void* dst, int64_t bytes, const int* err, int words, int rank, int ws,
+                          hipStream_t stream);
+// summed [ws][words][2] slots -> int32 [words], max over ranks
+int launch_merge_flag_slots(const float* slots, int* out, int words, int ws, hipStream_t stream);
 }  // namespace tea

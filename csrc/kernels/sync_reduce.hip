@@ -105,7 +105,61 @@ __global__ __launch_bounds__(kBlock) void seg_reduce_kernel(SegReduceArgs a) {
   }
 }
 
+// Snapshot of a large-state region plus this rank's device error flag in the same f32 SUM
+// all-reduce: the flag words (uint32) go as exact (hi16, lo16) float pairs into this rank's slot
+// of a [ws][words][2] block whose other slots are zero, so the SUM delivers every rank's flag
+// and the collective that gathered flags separately is gone.
+__global__ __launch_bounds__(kBlock) void snapshot_flags_kernel(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                                int64_t n4, const int* __restrict__ err, int words,
+                                                                int rank, int ws) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * kBlock;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x; i < n4; i += stride) dst[i] = src[i];
+  if (blockIdx.x == 0) {
+    float* slots = reinterpret_cast<float*>(dst + n4);
+    for (int j = threadIdx.x; j < ws * words * 2; j += kBlock) {
+      const int r = j / (2 * words), w = (j / 2) % words, half = j % 2;
+      float v = 0.f;
+      if (r == rank && err) {
+        const uint32_t u = static_cast<uint32_t>(err[w]);
+        v = static_cast<float>(half == 0 ? (u >> 16) : (u & 0xffffu));
+      }
+      slots[j] = v;
+    }
+  }
+}
+
+// [ws][words][2] summed slots -> int32 [words]: elementwise max over ranks (the engine's "max"
+// flag merge), rank order irrelevant
+__global__ void merge_flag_slots_kernel(const float* __restrict__ slots, int* __restrict__ out, int words, int ws) {
+  const int w = threadIdx.x;
+  if (w >= words) return;
+  uint32_t m = 0;
+  for (int r = 0; r < ws; ++r) {
+    const uint32_t hi = static_cast<uint32_t>(slots[(r * words + w) * 2]);
+    const uint32_t lo = static_cast<uint32_t>(slots[(r * words + w) * 2 + 1]);
+    const uint32_t u = (hi << 16) | lo;
+    m = u > m ? u : m;
+  }
+  out[w] = static_cast<int>(m);
+}
+
 }  // namespace
+
+int launch_snapshot_flags(const void* src, void* dst, int64_t bytes, const int* err, int words, int rank, int ws,
+                          hipStream_t stream) {
+  if (bytes % 16 != 0 || words < 1 || words > 7 || ws < 1 || rank < 0 || rank >= ws) return -1;
+  const int64_t n4 = bytes / 16;
+  const int grid = stream_grid(n4 > 0 ? n4 : 1, kBlock, 1024);
+  hipLaunchKernelGGL(snapshot_flags_kernel, dim3(grid), dim3(kBlock), 0, stream, static_cast<const float4*>(src),
+                     static_cast<float4*>(dst), n4, err, words, rank, ws);
+  return static_cast<int>(hipGetLastError());
+}
+
+int launch_merge_flag_slots(const float* slots, int* out, int words, int ws, hipStream_t stream) {
+  if (words < 1 || words > 7 || ws < 1) return -1;
+  hipLaunchKernelGGL(merge_flag_slots_kernel, dim3(1), dim3(kWave), 0, stream, slots, out, words, ws);
+  return static_cast<int>(hipGetLastError());
+}
 
 int launch_seg_reduce(const SegReduceArgs& a, hipStream_t stream) {
   if (a.nseg <= 0 || a.nseg > kSegMax || a.ws <= 0) return -1;

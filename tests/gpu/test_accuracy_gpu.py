@@ -57,7 +57,7 @@ def test_state_buffer_sync_on_rccl_one_rank():
     import torch.distributed as dist
 
     from torcheval_amd.metrics import MulticlassConfusionMatrix
-    from torcheval_amd.metrics.toolkit import sync_and_compute
+    from torcheval_amd.metrics.toolkit import get_synced_metric, sync_and_compute
     from torcheval_amd.parallel.collectives import collectives_at_world_size_1
     from torcheval_amd.parallel.state_buffer import buffer_of
 
@@ -76,6 +76,20 @@ def test_state_buffer_sync_on_rccl_one_rank():
                 local = m.compute().clone()
                 torch.testing.assert_close(sync_and_compute(m), local)
                 torch.testing.assert_close(m.compute(), local)  # inputs untouched
+        # the confusion matrix's flag rides its all-reduce (one collective): a bad label on
+        # this rank still raises from the synced copy, whose states match local compute
+        from torcheval_amd.parallel.state_buffer import _plan_for
+
+        cm_sb = buffer_of(cm, build=False)
+        assert _plan_for(cm_sb, dist.group.WORLD, 1, cm).fused
+        bad = y.clone()
+        bad[7] = 1000 + 3
+        cm2 = MulticlassConfusionMatrix(1000, device=dev).update(x, bad)
+        with collectives_at_world_size_1():
+            synced = get_synced_metric(cm2)
+        assert synced._err.tolist()[0] != 0 and synced._err.tolist()[1] == 1003
+        with pytest.raises(ValueError):
+            synced.compute()
         sb = buffer_of(acc, build=False)
         assert sb is not None
         ptr = acc.num_correct.data_ptr()

@@ -308,7 +308,8 @@ class _Plan:
     """Everything a single-metric sync needs, resolved once per (buffer, group, world size):
     the send view, the receive size, the segment table and where each state lands."""
 
-    __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large")
+    __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large", "fused",
+                 "rank", "flag_src")
 
     def __init__(self, sb: StateBuffer, group, ws: int, metric) -> None:
         from torch.distributed.distributed_c10d import _get_default_group
@@ -334,6 +335,17 @@ class _Plan:
                 prop = isinstance(getattr(cls, name, None), property)
                 self.assign.append((name, big, g.dtype, o // es, n, shape if shape else None, prop))
         self.flag = (sb.flag_off - sb.gather_off, 4 * sb.flag_words) if sb.flag_words else None
+        # ONE collective for "one large f32 sum group + a device error flag" (confusion matrices,
+        # binned counts): the flag rides the all-reduce as exact f32 (hi16, lo16) pairs in this
+        # rank's slot of a [ws][words][2] block (csrc/kernels/sync_reduce.hip), so the separate
+        # flag all-gather disappears; one tiny kernel merges the slots afterwards.
+        small = [g for g in sb.groups if g.off >= sb.reduce_end]
+        self.fused = (
+            self.nccl and sb.device.type == "cuda" and sb.flag_words > 0 and not small and len(self.large) == 1
+            and self.large[0][0] == 0 and self.large[0][2] == torch.float32 and self.large[0][3] == "sum"
+        )
+        self.rank = dist.get_rank(group) if self.fused else 0
+        self.flag_src = sb.flag_view(sb.buf) if self.fused else None
 
 
 def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
@@ -356,12 +368,22 @@ def _gather(plan: _Plan, src: torch.Tensor) -> torch.Tensor:
 def _sync_one(m, sb: StateBuffer, plan: _Plan):
     ws = plan.ws
     snap = None
-    if plan.large:
+    merged_err = None
+    if plan.fused:
+        from torcheval_amd.ops import native
+
+        words = sb.flag_words
+        snap = torch.empty(sb.reduce_end + ws * words * 8, dtype=torch.uint8, device=sb.device)
+        native().snapshot_flags(sb.buf[: sb.reduce_end], snap, plan.flag_src, words, plan.rank, ws)
+        _all_reduce_group(snap.view(torch.float32), "sum", plan.group)
+        merged_err = torch.empty(words, dtype=torch.int32, device=sb.device)
+        native().merge_flag_slots(snap[sb.reduce_end :].view(torch.float32), merged_err, words, ws)
+    elif plan.large:
         snap = sb.buf[: sb.reduce_end].clone()
         for off, nb, dtype, op in plan.large:
             _all_reduce_group(snap[off : off + nb].view(dtype), op, plan.group)
     merged = None
-    if plan.src is not None:
+    if plan.src is not None and not plan.fused:
         merged = _gather(plan, plan.src)
         if ws > 1:
             merged = _reduce_gathered(merged, plan.segs, ws, plan.row_bytes)
@@ -381,7 +403,9 @@ def _sync_one(m, sb: StateBuffer, plan: _Plan):
             setattr(r, name, v)
         else:
             d[name] = v
-    if plan.flag is not None:
+    if merged_err is not None:
+        d["_err"] = merged_err
+    elif plan.flag is not None:
         o, nb = plan.flag
         d["_err"] = merged[o : o + nb].view(torch.int32)
     return r
