@@ -1,5 +1,5 @@
-"""binary_auroc + binary_auprc N=1M kernel breakdown: run under rocprofv3 --kernel-trace --stats.
-``TORCHEVAL_AMD_K3B=0`` profiles the K3a sort + K3 scan path instead of K3b."""
+"""binary_auroc + binary_auprc kernel breakdown (N=1M, or AUROC_N): run under
+rocprofv3 --kernel-trace --stats."""
 import os
 import sys
 

@@ -1155,62 +1155,6 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
 }
 
 
-// K3b: one-row unweighted binary AUROC / AUPRC by buckets, no global sort (32K..4M samples)
-bool bucket_auc_ok(int64_t n) { return tea::bucket_auc_supported(n); }
-
-void binary_auc_bucket(const Tensor& x, const Tensor& t, const optional<Tensor>& out_roc,
-                       const optional<Tensor>& out_pr) {
-  check_gpu(x, "x");
-  TORCH_CHECK(x.dim() == 1 && x.scalar_type() == at::kFloat && x.is_contiguous(),
-              "binary_auc_bucket: x must be contiguous float32 [n]");
-  TORCH_CHECK(t.dim() == 1 && t.size(0) == x.size(0) && t.is_contiguous() && t.device() == x.device(),
-              "binary_auc_bucket: t must be contiguous [n] on x's device");
-  const auto st = t.scalar_type();
-  TORCH_CHECK(st == at::kFloat || st == at::kLong || st == at::kInt || st == at::kByte || st == at::kBool,
-              "binary_auc_bucket: unsupported target dtype ", st);
-  for (const auto* o : {&out_roc, &out_pr})
-    if (o->has_value())
-      TORCH_CHECK((*o)->scalar_type() == at::kDouble && (*o)->numel() == 1 && (*o)->device() == x.device(),
-                  "binary_auc_bucket: outputs must be float64 [1]");
-  TORCH_CHECK(out_roc.has_value() || out_pr.has_value(), "binary_auc_bucket: no output requested");
-  const int64_t n = x.size(0);
-  TORCH_CHECK(tea::bucket_auc_supported(n), "binary_auc_bucket: n out of range");
-  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  hipStream_t st_ = stream_for(x);
-  tea::BucketAucArgs a;
-  a.x = x.data_ptr<float>();
-  a.t = t.data_ptr();
-  a.t_dt = dt_of(t);
-  a.n = n;
-  a.B = tea::bucket_auc_buckets(n);
-  a.S = 4 * a.B;
-  a.nbins = 2 * a.B + 2;
-  // zeroed, self-cleaning: cursor [nbins] u32 | posmass [nbins] f64 | done
-  char* z = static_cast<char*>(zeroed_workspace(x, st_, 4096 * 4 + 4096 * 8 + 64, 8));
-  a.cursor = reinterpret_cast<uint32_t*>(z);
-  a.posmass = reinterpret_cast<double*>(z + 4096 * 4);
-  a.done = reinterpret_cast<unsigned*>(z + 4096 * 12);
-  const int64_t tiles = tea::bucket_auc_tiles(n);
-  const int64_t stack_bytes = tea::bucket_auc_stack_items(n) * 16;
-  const int64_t bytes = stack_bytes + 5 * n * 4 + a.B * 4 + a.nbins * 16 + tiles * 12 + tiles * a.nbins * 4 + 256;
-  char* ws = static_cast<char*>(scratch_workspace(x, st_, bytes, 2));
-  a.stack = ws;
-  ws += stack_bytes;
-  a.slots = reinterpret_cast<double*>(ws);
-  ws += ((a.nbins * 16 + 15) / 16) * 16;
-  a.keys_out = reinterpret_cast<uint32_t*>(ws);
-  a.t_out = reinterpret_cast<float*>(a.keys_out + n);
-  a.keys_tmp = reinterpret_cast<uint32_t*>(a.t_out + n);
-  a.t_tmp = reinterpret_cast<float*>(a.keys_tmp + n);
-  a.sp = reinterpret_cast<uint32_t*>(a.t_tmp + n);
-  a.spc = a.sp + a.B;
-  a.tileoff = a.spc + tiles * 3;
-  a.binrank = a.tileoff + tiles * a.nbins;
-  a.out_roc = out_roc.has_value() ? out_roc->data_ptr<double>() : nullptr;
-  a.out_pr = out_pr.has_value() ? out_pr->data_ptr<double>() : nullptr;
-  check_launch(tea::launch_bucket_auc(a, st_), "binary_auc_bucket");
-}
-
 // binned AUROC / AUPRC from [T, rows] float32 counts in one launch
 void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>& fn,
                      const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc,
@@ -1395,10 +1339,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("num_correct"), py::arg("num_total") = py::none(), py::arg("total") = 0.0);
   m.def("transpose_f32", &transpose_f32, "LDS-tiled [n, c] -> [c, n] float32 transpose", py::arg("x"),
         py::arg("out"));
-  m.def("binary_auc_bucket", &binary_auc_bucket,
-        "K3b one-row unweighted binary AUROC / AUPRC by buckets (x [n] f32, t [n], outs [1] f64)", py::arg("x"),
-        py::arg("t"), py::arg("out_roc") = py::none(), py::arg("out_pr") = py::none());
-  m.def("bucket_auc_ok", &bucket_auc_ok, "whether K3b handles n samples", py::arg("n"));
   m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
         py::arg("x"), py::arg("out_sorted"), py::arg("out_order"), py::arg("payload") = py::none(),
         py::arg("payload_kind") = 0);
@@ -1562,7 +1502,6 @@ TORCH_LIBRARY(torcheval_amd, m) {
   m.def("perplexity_sums(Tensor input, Tensor target, int? ignore_index, Tensor(a!) out, Tensor(b!)? err, "
         "bool deterministic) -> ()");
   m.def("transpose_f32(Tensor x, Tensor(a!) out) -> ()");
-  m.def("binary_auc_bucket(Tensor x, Tensor t, Tensor(a!)? out_roc, Tensor(b!)? out_pr) -> ()");
   m.def("cls_counts(Tensor input, Tensor target, int k, int num_classes, Tensor(a!)? micro_correct, "
         "Tensor(b!)? micro_total, Tensor(c!)? cls_correct, Tensor(d!)? cls_label, Tensor(e!)? cls_pred, "
         "Tensor(f!)? confusion, Tensor(g!)? err) -> ()");
@@ -1592,7 +1531,6 @@ TORCH_LIBRARY_IMPL(torcheval_amd, CUDA, m) {
   m.impl("perplexity_sums", &op_perplexity_sums);
   m.impl("transpose_f32", &op_transpose_f32);
   m.impl("cls_counts", &op_cls_counts);
-  m.impl("binary_auc_bucket", &binary_auc_bucket);
 }
 
 TORCH_LIBRARY_IMPL(torcheval_amd, CPU, m) {

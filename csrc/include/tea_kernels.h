@@ -407,36 +407,6 @@ int64_t radix_sort_tiles(int64_t rows, int64_t n);
 int64_t radix_sort_groups(int64_t tiles);
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream);
 int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream);
-// ------------------------------------------------------------------ K3b bucketed AUROC / AUPRC
-struct BucketAucArgs {
-  const float* x = nullptr;  // [n] scores
-  const void* t = nullptr;   // [n] targets (f32 / i64 / i32 / u8 / bool)
-  DType t_dt = DType::f32;
-  int64_t n = 0;
-  int B = 0;      // bucket_auc_buckets(n): splitters + 1 (power of two)
-  int S = 0;      // 4 * B sampled scores
-  int nbins = 0;  // 2 * B + 2: NaN, +inf, 2B - 1 regular bins (between / equal-to splitter), -inf
-  uint32_t* sp = nullptr;        // [B] scratch
-  uint32_t* cursor = nullptr;    // [nbins] zeroed, left zeroed (bin counts after the hist pass)
-  double* posmass = nullptr;     // [nbins] zeroed, left zeroed
-  unsigned* done = nullptr;      // [1] zeroed, left zeroed (blocks of the local pass finished)
-  uint32_t* tileoff = nullptr;   // [tiles, nbins] scratch: each tile's reserved run per bin (4096-sample tiles)
-  uint32_t* spc = nullptr;       // [tiles, 3] scratch: special-bin counts per tile
-  uint32_t* binrank = nullptr;   // [n] scratch: bin << 12 | in-tile rank, from the hist pass
-  uint32_t* keys_out = nullptr;  // [n] scratch (bin-partitioned keys; source index in special bins)
-  float* t_out = nullptr;        // [n] scratch
-  uint32_t* keys_tmp = nullptr;  // [n] scratch (bins larger than the LDS stage)
-  float* t_tmp = nullptr;        // [n] scratch
-  double* slots = nullptr;       // [B + 1, 2] scratch: per-block (U, AP)
-  void* stack = nullptr;         // [bucket_auc_stack_items(n)] x 16 B scratch: pending ranges of big bins
-  double* out_roc = nullptr;     // [1] AUROC or null
-  double* out_pr = nullptr;      // [1] AUPRC or null
-};
-int bucket_auc_buckets(int64_t n);
-bool bucket_auc_supported(int64_t n);
-int64_t bucket_auc_tiles(int64_t n);
-int64_t bucket_auc_stack_items(int64_t n);
-int launch_bucket_auc(const BucketAucArgs& a, hipStream_t stream);
 // ------------------------------------------------------------------ K10b retrieval top-k
 struct RetrievalArgs {
   const float* x = nullptr;        // [n] scores

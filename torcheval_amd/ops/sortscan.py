@@ -1,12 +1,11 @@
 """K3 sort-and-scan wrappers (csrc/kernels/sortscan.hip): exact tie-aware AUROC / AUPRC.
 
 Pipeline per call: one segmented device sort of the scores (descending, one row per task /
-class) followed by the four-launch K3 scan.  One unweighted row of 32K..4M samples instead goes
-through K3b (csrc/kernels/bucketauc.hip): splitters, bin counts, scatter into bins and per-bin
-terms - no global sort.  No host synchronisation anywhere.
+class) followed by the four-launch K3 scan.  No host synchronisation anywhere.  (A bucketed
+no-global-sort variant, K3b, was built and measured slower at every size - see
+profiles/README.md, round 3 - and removed.)
 """
 
-import os
 from typing import Optional, Tuple
 
 import torch
@@ -16,7 +15,6 @@ from torcheval_amd.ops import native
 
 PAYLOAD_TARGET, PAYLOAD_LABEL = 1, 2
 _TARGET_PAYLOAD = (torch.float32, torch.int64, torch.int32, torch.uint8, torch.bool)
-_BUCKET_SCORES = (torch.float32, torch.float16, torch.bfloat16)  # f16 / bf16 -> f32 is exact
 
 
 def _sort_rows(
@@ -47,12 +45,6 @@ def _sort_rows(
     return s, idx, 0
 
 
-def _bucket_ok(n: int) -> bool:
-    """K3b (csrc/kernels/bucketauc.hip) takes one unweighted row of 32K..4M samples;
-    ``TORCHEVAL_AMD_K3B=0`` forces the K3a sort + K3 scan (A/B switch)."""
-    return os.environ.get("TORCHEVAL_AMD_K3B", "1") != "0" and bool(native().bucket_auc_ok(n))
-
-
 def binary_auc(
     input: torch.Tensor,
     target: torch.Tensor,
@@ -69,14 +61,6 @@ def binary_auc(
         w = weight if weight.dim() == 2 else weight.unsqueeze(0)
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
-    if w is None and x.shape[0] == 1 and x.dtype in _BUCKET_SCORES and _bucket_ok(x.shape[1]):
-        # K3b: one unweighted row by buckets, no global sort (4 launches instead of K3a + K3's 13)
-        xs = x[0].float() if x.dtype != torch.float32 else x[0]
-        ts = t[0] if t.dtype in _TARGET_PAYLOAD else t[0].float()
-        out_roc = torch.empty(1, dtype=torch.float64, device=x.device) if roc else None
-        out_pr = torch.empty(1, dtype=torch.float64, device=x.device) if pr else None
-        native().binary_auc_bucket(xs.contiguous(), ts.contiguous(), out_roc, out_pr)
-        return out_roc, out_pr
     s, idx, kind = _sort_rows(x, t if w is None else None, PAYLOAD_TARGET)
     rows = s.shape[0]
     out_roc = torch.empty(rows, dtype=torch.float64, device=x.device) if roc else None
