@@ -30,6 +30,7 @@ namespace {
 
 using namespace k3;
 constexpr int kFuseTiles = 1536;     // (<= 4) rows up to this many tiles skip the tile_scan launch
+constexpr int kFusePer = kFuseTiles / kT;  // preceding-tile totals per thread in the fused prefix
 
 template <bool DIRECT>
 __global__ __launch_bounds__(kT) void tile_sums_kernel(AucScanArgs a) {
@@ -153,14 +154,33 @@ __device__ void finalize_row(const AucScanArgs& a, int r, int ntiles, bool fused
   const D2* ta = reinterpret_cast<const D2*>(a.tarea) + static_cast<int64_t>(r) * ntiles;
   const D2* ts = reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
   double roc = 0.0, pr = 0.0, p = 0.0, q = 0.0;
-  for (int t = threadIdx.x; t < ntiles; t += kT) {
-    const D2 v = ta[t];
-    roc += v.x;
-    pr += v.y;
-    if (fused) {
-      const D2 u = ts[t];
-      p += u.x;
-      q += u.y;
+  if (ntiles <= kFuseTiles) {  // every load in flight together
+    D2 v[kFusePer], w[kFusePer];
+#pragma unroll
+    for (int u = 0; u < kFusePer; ++u) {
+      const int t = u * kT + static_cast<int>(threadIdx.x);
+      const int tc = t < ntiles ? t : 0;
+      v[u] = ta[tc];
+      w[u] = fused ? ts[tc] : D2{0.0, 0.0};
+    }
+#pragma unroll
+    for (int u = 0; u < kFusePer; ++u) {
+      const bool ok = u * kT + static_cast<int>(threadIdx.x) < ntiles;
+      roc += ok ? v[u].x : 0.0;
+      pr += ok ? v[u].y : 0.0;
+      p += ok ? w[u].x : 0.0;
+      q += ok ? w[u].y : 0.0;
+    }
+  } else {
+    for (int t = threadIdx.x; t < ntiles; t += kT) {
+      const D2 v = ta[t];
+      roc += v.x;
+      pr += v.y;
+      if (fused) {
+        const D2 u = ts[t];
+        p += u.x;
+        q += u.y;
+      }
     }
   }
   D2 tot, pn;
@@ -224,11 +244,21 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   nk_last = (live && i0 + kPer < a.n) ? nk_last : K(0);
   double pa = 0.0, pb = 0.0;
   if constexpr (FUSED) {
+    // the preceding tiles' totals: every load in flight together (clamped index, masked after),
+    // where a strided loop paid one round trip per 256 tiles
     const D2* ts = reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
-    for (int t = threadIdx.x; t < static_cast<int>(blockIdx.x); t += kT) {
-      const D2 q = ts[t];
-      pa += q.x;
-      pb += q.y;
+    const int upto = static_cast<int>(blockIdx.x);
+    D2 q[kFusePer];
+#pragma unroll
+    for (int u = 0; u < kFusePer; ++u) {
+      const int t = u * kT + static_cast<int>(threadIdx.x);
+      q[u] = ts[t < upto ? t : 0];
+    }
+#pragma unroll
+    for (int u = 0; u < kFusePer; ++u) {
+      const bool ok = u * kT + static_cast<int>(threadIdx.x) < upto;
+      pa += ok ? q[u].x : 0.0;
+      pb += ok ? q[u].y : 0.0;
     }
   } else {  // tile_scan's table (one broadcast load; a block scan here cost 53 -> 62 us at 100 x 100k)
     const D2 q = reinterpret_cast<const D2*>(a.tstart)[static_cast<int64_t>(r) * ntiles + blockIdx.x];
