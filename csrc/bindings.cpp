@@ -1355,6 +1355,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("m"), py::arg("lam"), py::arg("status"));
   tea_register_runtime(m);
   tea_register_cpu_metrics(m);
+  tea_register_rccl(m);
 }
 
 // ---------------------------------------------------------------- torch dispatcher registration

@@ -33,7 +33,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 import torch.distributed as dist
 
-from torcheval_amd.parallel import collectives
+from torcheval_amd.parallel import collectives, rccl_direct
 from torcheval_amd.parallel.distributed import backend_of
 
 # Groups up to this size (summed over the gather region) ride the single all-gather.
@@ -294,10 +294,13 @@ def _reduce_gathered(rows: torch.Tensor, segs, ws: int, row_bytes: int) -> torch
     return out
 
 
-def _all_reduce_group(t: torch.Tensor, op: str, group) -> None:
+def _all_reduce_group(t: torch.Tensor, op: str, group, comm: Optional[int] = None) -> None:
     if t.dtype == torch.bool:  # logical or / and through uint8 max / min
         t = t.view(torch.uint8)
         op = "min" if op == "min" else "max"
+    if comm is not None:  # direct RCCL on the current stream (parallel/rccl_direct.py)
+        rccl_direct.all_reduce(comm, t, op)
+        return
     work = dist.all_reduce(t, op=_RCCL_OP[op], group=group, async_op=collectives._issue_async(True))
     if work is not None:
         collectives._wait(work)
@@ -309,7 +312,7 @@ class _Plan:
     the send view, the receive size, the segment table and where each state lands."""
 
     __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large", "fused",
-                 "rank", "flag_src")
+                 "rank", "flag_src", "comm")
 
     def __init__(self, sb: StateBuffer, group, ws: int, metric) -> None:
         from torch.distributed.distributed_c10d import _get_default_group
@@ -346,6 +349,9 @@ class _Plan:
         )
         self.rank = dist.get_rank(group) if self.fused else 0
         self.flag_src = sb.flag_view(sb.buf) if self.fused else None
+        # RCCL without torch.distributed's per-call host cost (created collectively here: every
+        # rank builds this plan at the same sync)
+        self.comm = rccl_direct.comm_for(self.pg, ws, sb.device) if self.nccl else None
 
 
 def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
@@ -360,9 +366,18 @@ def _gather(plan: _Plan, src: torch.Tensor) -> torch.Tensor:
     """One all-gather of the raw gather region; RCCL: straight into one [ws * row] buffer."""
     if plan.nccl and collectives.current_sync_timeout() is None:
         out = torch.empty(plan.ws * plan.row_bytes, dtype=torch.uint8, device=src.device)
-        dist.all_gather_into_tensor(out, src, group=plan.group)
+        if plan.comm is not None:
+            rccl_direct.all_gather(plan.comm, src, out)
+        else:
+            dist.all_gather_into_tensor(out, src, group=plan.group)
         return out
     return collectives.all_gather_fixed_async(src, plan.group, plan.ws, blocking=True).wait()
+
+
+def _direct(plan: _Plan) -> Optional[int]:
+    """The plan's direct communicator when the sync may use it (no sync timeout requested:
+    timeouts need torch.distributed's watchdog)."""
+    return plan.comm if collectives.current_sync_timeout() is None else None
 
 
 def _sync_one(m, sb: StateBuffer, plan: _Plan):
@@ -375,13 +390,13 @@ def _sync_one(m, sb: StateBuffer, plan: _Plan):
         words = sb.flag_words
         snap = torch.empty(sb.reduce_end + ws * words * 8, dtype=torch.uint8, device=sb.device)
         native().snapshot_flags(sb.buf[: sb.reduce_end], snap, plan.flag_src, words, plan.rank, ws)
-        _all_reduce_group(snap.view(torch.float32), "sum", plan.group)
+        _all_reduce_group(snap.view(torch.float32), "sum", plan.group, _direct(plan))
         merged_err = torch.empty(words, dtype=torch.int32, device=sb.device)
         native().merge_flag_slots(snap[sb.reduce_end :].view(torch.float32), merged_err, words, ws)
     elif plan.large:
         snap = sb.buf[: sb.reduce_end].clone()
         for off, nb, dtype, op in plan.large:
-            _all_reduce_group(snap[off : off + nb].view(dtype), op, plan.group)
+            _all_reduce_group(snap[off : off + nb].view(dtype), op, plan.group, _direct(plan))
     merged = None
     if plan.src is not None and not plan.fused:
         merged = _gather(plan, plan.src)
