@@ -89,3 +89,22 @@ def test_sync_matches_torch_distributed(pg, monkeypatch, direct):
                 assert torch.equal(a, b)
         else:
             assert torch.equal(g_, w_)
+
+
+@pytest.mark.parametrize("direct", ["1", "0"])
+def test_collection_sync_matches_local(pg, monkeypatch, direct):
+    from torcheval_amd.metrics.toolkit import sync_and_compute_collection
+
+    monkeypatch.setenv("TORCHEVAL_AMD_DIRECT_RCCL", direct)
+    acc, cm, bap = _metrics()
+    coll = {"acc": acc, "cm": cm, "bap": bap}
+    with collectives_at_world_size_1():
+        got = sync_and_compute_collection(coll)
+    for k, m in coll.items():
+        w = m.compute()
+        g_ = got[k]
+        if isinstance(w, tuple):
+            for a, b in zip(g_, w):
+                assert torch.equal(a, b)
+        else:
+            assert torch.equal(g_, w)

@@ -467,6 +467,11 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
     nccl = backend_of(group) == "nccl"
     if nccl and dev.type != "cuda":
         return None
+    comm = None
+    if nccl and collectives.current_sync_timeout() is None:
+        from torch.distributed.distributed_c10d import _get_default_group
+
+        comm = rccl_direct.comm_for(group if group is not None else _get_default_group(), ws, dev)
 
     # 1. large groups: snapshot + all_reduce (in place on the snapshot)
     reduced: List[Optional[torch.Tensor]] = []
@@ -475,7 +480,7 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
             snap = sb.buf[: sb.reduce_end].clone()
             for g in sb.groups:
                 if g.off < sb.reduce_end:
-                    _all_reduce_group(snap[g.off : g.off + g.nbytes].view(g.dtype), g.op, group)
+                    _all_reduce_group(snap[g.off : g.off + g.nbytes].view(g.dtype), g.op, group, comm)
             reduced.append(snap)
         else:
             reduced.append(None)
@@ -486,7 +491,11 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
     if regions:
         send = regions[0] if len(regions) == 1 else torch.cat(regions)
         row_bytes = send.numel()
-        gathered = collectives.all_gather_fixed_async(send, group, ws, blocking=True).wait()
+        if comm is not None:
+            gathered = torch.empty(ws * row_bytes, dtype=torch.uint8, device=dev)
+            rccl_direct.all_gather(comm, send, gathered)
+        else:
+            gathered = collectives.all_gather_fixed_async(send, group, ws, blocking=True).wait()
         if ws == 1:
             merged_small = gathered
         else:
