@@ -13,6 +13,7 @@
 // Replaces, for the fast sync path, reference torcheval/metrics/toolkit.py:371-391 (pickled
 // all_gather_object per sync).
 #include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <dlfcn.h>
 #include <pybind11/pybind11.h>
@@ -144,6 +145,7 @@ void rccl_all_gather(int64_t handle, const at::Tensor& src, at::Tensor dst) {
                   src.scalar_type() == dst.scalar_type() && src.device() == dst.device(),
               "rccl_direct: all_gather needs contiguous device tensors of one dtype");
   TORCH_CHECK(src.numel() > 0 && dst.numel() % src.numel() == 0, "rccl_direct: all_gather size mismatch");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(src.device());
   check(api().all_gather(src.data_ptr(), dst.data_ptr(), static_cast<size_t>(src.numel()), dtype_of(src),
                          comm_of(handle), stream_of(src)),
         "ncclAllGather");
@@ -155,6 +157,7 @@ void rccl_all_reduce(int64_t handle, at::Tensor t, int64_t op) {
   TORCH_CHECK(op >= 0 && op <= 2, "rccl_direct: op must be 0 (sum), 1 (max) or 2 (min)");
   if (t.numel() == 0) return;
   const ncclRedOp_t rop = op == 0 ? ncclSum : op == 1 ? ncclMax : ncclMin;
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(t.device());
   check(api().all_reduce(t.data_ptr(), t.data_ptr(), static_cast<size_t>(t.numel()), dtype_of(t), rop,
                          comm_of(handle), stream_of(t)),
         "ncclAllReduce");
