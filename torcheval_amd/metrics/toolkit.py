@@ -22,6 +22,7 @@ from datetime import timedelta
 
 from torcheval_amd.parallel.collectives import skip_collectives, sync_timeout
 from torcheval_amd.parallel.distributed import PGWrapper
+from torcheval_amd.parallel.state_buffer import start_fast_sync
 from torcheval_amd.parallel.state_sync import (
     PendingSync,
     start_sync_collection,
@@ -105,8 +106,12 @@ def get_synced_metric_async(
     if skip_collectives(world_size):
         return SyncFuture(None, clone_metric(metric) if single else {k: clone_metric(m) for k, m in metric.items()}, single)
     coll = {"_": metric} if single else metric
+    group = process_group if process_group else dist.group.WORLD
     with trace_range("torcheval_amd.start_sync"), sync_timeout(timeout):
-        pending = start_sync_collection(coll, process_group if process_group else dist.group.WORLD, world_size)
+        # state-buffer metrics: snapshot now, the collectives on the engine's side HIP stream
+        pending = start_fast_sync(coll, group, world_size) if timeout is None else None
+        if pending is None:
+            pending = start_sync_collection(coll, group, world_size)
     return SyncFuture(pending, None, single, timeout)
 
 

@@ -455,6 +455,32 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
         if plan.nccl and sb.device.type != "cuda":
             return None
         return {key: _sync_one(m, sb, plan)}
+    issue = _fast_issue(metrics, group, ws, side=False)
+    return None if issue is None else _fast_finish(issue)
+
+
+_SIDE_STREAMS: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    """The sync engine's dedicated HIP stream on ``dev`` (one per device, created once)."""
+    s = _SIDE_STREAMS.get(dev.index)
+    if s is None:
+        s = _SIDE_STREAMS[dev.index] = torch.cuda.Stream(device=dev)
+    return s
+
+
+class _FastIssue:
+    """A fast sync between issue and finish: the snapshots, the receive buffer and (async) the
+    event the side stream records after its collectives."""
+
+    __slots__ = ("metrics", "sbs", "reduced", "gathered", "ws", "row_bytes", "done", "dev", "keep")
+
+
+def _fast_issue(metrics, group, ws: int, side: bool) -> Optional[_FastIssue]:
+    """Snapshot + issue the collectives of a state-buffer collection.  ``side``: the
+    collectives go on the engine's side stream (direct RCCL only) after an event recorded
+    on the current stream, so later updates on the compute stream overlap them."""
     sbs = []
     for m in metrics.values():
         sb = buffer_of(m)
@@ -472,32 +498,64 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
         from torch.distributed.distributed_c10d import _get_default_group
 
         comm = rccl_direct.comm_for(group if group is not None else _get_default_group(), ws, dev)
+    if side and comm is None:
+        return None
 
-    # 1. large groups: snapshot + all_reduce (in place on the snapshot)
-    reduced: List[Optional[torch.Tensor]] = []
-    for sb in sbs:
-        if sb.reduce_end:
-            snap = sb.buf[: sb.reduce_end].clone()
+    # snapshots (the live buffers keep changing under later updates on the async path)
+    reduced: List[Optional[torch.Tensor]] = [sb.buf[: sb.reduce_end].clone() if sb.reduce_end else None for sb in sbs]
+    regions = [sb.buf[sb.gather_off : sb.gather_off + sb.gather_bytes] for sb in sbs if sb.gather_bytes]
+    send = None
+    if regions:
+        if len(regions) > 1:
+            send = torch.cat(regions)
+        else:  # zero-copy send on the blocking path
+            send = regions[0].clone() if side else regions[0]
+    row_bytes = send.numel() if send is not None else 0
+    gathered = torch.empty(ws * row_bytes, dtype=torch.uint8, device=dev) if (send is not None and comm is not None) else None
+
+    def collectives_now() -> Optional[torch.Tensor]:
+        # 1. large groups: all_reduce in place on the snapshots
+        for sb, snap in zip(sbs, reduced):
+            if snap is None:
+                continue
             for g in sb.groups:
                 if g.off < sb.reduce_end:
                     _all_reduce_group(snap[g.off : g.off + g.nbytes].view(g.dtype), g.op, group, comm)
-            reduced.append(snap)
-        else:
-            reduced.append(None)
-
-    # 2. the gather regions: ONE all-gather (zero-copy send for a single metric)
-    regions = [sb.buf[sb.gather_off : sb.gather_off + sb.gather_bytes] for sb in sbs if sb.gather_bytes]
-    merged_small: Optional[torch.Tensor] = None
-    if regions:
-        send = regions[0] if len(regions) == 1 else torch.cat(regions)
-        row_bytes = send.numel()
+        # 2. the gather regions: ONE all-gather
+        if send is None:
+            return None
         if comm is not None:
-            gathered = torch.empty(ws * row_bytes, dtype=torch.uint8, device=dev)
             rccl_direct.all_gather(comm, send, gathered)
-        else:
-            gathered = collectives.all_gather_fixed_async(send, group, ws, blocking=True).wait()
+            return gathered
+        return collectives.all_gather_fixed_async(send, group, ws, blocking=True).wait()
+
+    issue = _FastIssue()
+    issue.metrics, issue.sbs, issue.reduced, issue.ws, issue.row_bytes, issue.dev = metrics, sbs, reduced, ws, row_bytes, dev
+    issue.keep = send  # referenced until finish: the side stream reads it
+    issue.done = None
+    if side:
+        ready = torch.cuda.Event()
+        ready.record()
+        stream = _side_stream(dev)
+        stream.wait_event(ready)
+        with torch.cuda.stream(stream):
+            issue.gathered = collectives_now()
+        issue.done = torch.cuda.Event()
+        issue.done.record(stream)
+    else:
+        issue.gathered = collectives_now()
+    return issue
+
+
+def _fast_finish(issue: _FastIssue) -> Dict[str, "object"]:
+    """The merged metrics of an issued fast sync (shallow copies viewing the merged buffers)."""
+    if issue.done is not None:
+        torch.cuda.current_stream(issue.dev).wait_event(issue.done)
+    metrics, sbs, ws = issue.metrics, issue.sbs, issue.ws
+    merged_small: Optional[torch.Tensor] = None
+    if issue.gathered is not None:
         if ws == 1:
-            merged_small = gathered
+            merged_small = issue.gathered
         else:
             offs, counts, dts, ops = [], [], [], []
             base = 0
@@ -510,12 +568,12 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
                 dts += d
                 ops += p
                 base += sb.gather_bytes
-            merged_small = _reduce_gathered(gathered, (offs, counts, dts, ops), ws, row_bytes)
+            merged_small = _reduce_gathered(issue.gathered, (offs, counts, dts, ops), ws, issue.row_bytes)
 
     # 3. the merged metrics: shallow copies whose states view the merged buffers
     out = {}
     base = 0
-    for (key, m), sb, snap in zip(metrics.items(), sbs, reduced):
+    for (key, m), sb, snap in zip(metrics.items(), sbs, issue.reduced):
         r = copy.copy(m)
         r._tea_sb = None
         for g in sb.groups:
@@ -533,6 +591,23 @@ def fast_sync(metrics, group, ws: int) -> Optional[Dict[str, "object"]]:
             base += sb.gather_bytes
         out[key] = r
     return out
+
+
+class FastPendingSync:
+    """``PendingSync``-compatible handle of an async state-buffer sync on the side stream."""
+
+    def __init__(self, issue: _FastIssue) -> None:
+        self._issue = issue
+
+    def finish(self) -> Dict[str, "object"]:
+        return _fast_finish(self._issue)
+
+
+def start_fast_sync(metrics, group, ws: int) -> Optional[FastPendingSync]:
+    """Async form of :func:`fast_sync`: snapshot now, collectives on the engine's side HIP
+    stream (direct RCCL), merge at ``finish()``.  None when not eligible."""
+    issue = _fast_issue(metrics, group, ws, side=True)
+    return None if issue is None else FastPendingSync(issue)
 
 
 def plan_summary(metric) -> Optional[dict]:
