@@ -151,15 +151,22 @@ void rccl_all_gather(int64_t handle, const at::Tensor& src, at::Tensor dst) {
         "ncclAllGather");
 }
 
-// in place; op 0 sum, 1 max, 2 min
-void rccl_all_reduce(int64_t handle, at::Tensor t, int64_t op) {
+// op 0 sum, 1 max, 2 min; in place, or into `out` (same dtype and size) when given
+void rccl_all_reduce(int64_t handle, at::Tensor t, int64_t op, const c10::optional<at::Tensor>& out) {
   TORCH_CHECK(t.is_cuda() && t.is_contiguous(), "rccl_direct: all_reduce needs a contiguous device tensor");
   TORCH_CHECK(op >= 0 && op <= 2, "rccl_direct: op must be 0 (sum), 1 (max) or 2 (min)");
+  void* recv = t.data_ptr();
+  if (out.has_value()) {
+    TORCH_CHECK(out->is_cuda() && out->is_contiguous() && out->scalar_type() == t.scalar_type() &&
+                    out->numel() == t.numel() && out->device() == t.device(),
+                "rccl_direct: all_reduce out must match the input");
+    recv = out->data_ptr();
+  }
   if (t.numel() == 0) return;
   const ncclRedOp_t rop = op == 0 ? ncclSum : op == 1 ? ncclMax : ncclMin;
   c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(t.device());
-  check(api().all_reduce(t.data_ptr(), t.data_ptr(), static_cast<size_t>(t.numel()), dtype_of(t), rop,
-                         comm_of(handle), stream_of(t)),
+  check(api().all_reduce(t.data_ptr(), recv, static_cast<size_t>(t.numel()), dtype_of(t), rop, comm_of(handle),
+                         stream_of(t)),
         "ncclAllReduce");
 }
 
@@ -174,13 +181,14 @@ void tea_register_rccl(pybind11::module_& m) {
   m.def("rccl_comm_destroy", &rccl_comm_destroy, "ncclCommDestroy of a handle", py::arg("handle"));
   m.def("rccl_all_gather", &rccl_all_gather, "ncclAllGather on the current stream", py::arg("handle"),
         py::arg("src"), py::arg("dst"));
-  m.def("rccl_all_reduce", &rccl_all_reduce, "in-place ncclAllReduce on the current stream (op 0/1/2 = sum/max/min)",
-        py::arg("handle"), py::arg("t"), py::arg("op"));
+  m.def("rccl_all_reduce", &rccl_all_reduce,
+        "ncclAllReduce on the current stream (op 0/1/2 = sum/max/min), in place or into out", py::arg("handle"),
+        py::arg("t"), py::arg("op"), py::arg("out") = py::none());
 }
 
 TORCH_LIBRARY_FRAGMENT(torcheval_amd, m) {
   m.def("rccl_all_gather(int handle, Tensor src, Tensor(a!) dst) -> ()");
-  m.def("rccl_all_reduce(int handle, Tensor(a!) t, int op) -> ()");
+  m.def("rccl_all_reduce(int handle, Tensor(a!) t, int op, Tensor(b!)? out=None) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(torcheval_amd, CUDA, m) {

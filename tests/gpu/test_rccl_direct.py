@@ -52,10 +52,26 @@ def test_primitives(pg):
         for op in ("sum", "max", "min"):
             rccl_direct.all_reduce(h, t, op)
             assert torch.equal(t, ref)  # one rank: every reduction is the identity
+    o = torch.full((1001,), -1.0, device=DEV)
+    s_ = torch.randn(1001, device=DEV)
+    rccl_direct.all_reduce(h, s_, "sum", out=o)  # out of place: the send buffer is untouched
+    assert torch.equal(o, s_)
     # dispatcher forms
     torch.ops.torcheval_amd.rccl_all_gather(h, src, out)
     torch.ops.torcheval_amd.rccl_all_reduce(h, t, 0)
     torch.cuda.synchronize()
+
+
+def test_accuracy_plan_uses_one_all_reduce(pg):
+    from torcheval_amd.metrics.toolkit import sync_and_compute
+    from torcheval_amd.parallel import state_buffer as sbm
+
+    acc, _, _ = _metrics()
+    with collectives_at_world_size_1():
+        v = sync_and_compute(acc)
+        plan = sbm._plan_for(sbm.buffer_of(acc), dist.group.WORLD, 1, acc)
+    assert plan.single is not None and plan.comm is not None
+    assert torch.equal(v, acc.compute())
 
 
 def _metrics():

@@ -62,10 +62,11 @@ def all_gather(handle: int, src: torch.Tensor, out: torch.Tensor) -> None:
     native().rccl_all_gather(handle, src, out)
 
 
-def all_reduce(handle: int, t: torch.Tensor, op: str) -> None:
+def all_reduce(handle: int, t: torch.Tensor, op: str, out: Optional[torch.Tensor] = None) -> None:
+    """In place, or (``out``) out of place: the send buffer is left untouched."""
     from torcheval_amd.ops import native
 
-    native().rccl_all_reduce(handle, t, _OPS[op])
+    native().rccl_all_reduce(handle, t, _OPS[op], out)
 
 
 def destroy_all() -> None:

@@ -312,7 +312,7 @@ class _Plan:
     the send view, the receive size, the segment table and where each state lands."""
 
     __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large", "fused",
-                 "rank", "flag_src", "comm")
+                 "rank", "flag_src", "comm", "single")
 
     def __init__(self, sb: StateBuffer, group, ws: int, metric) -> None:
         from torch.distributed.distributed_c10d import _get_default_group
@@ -352,6 +352,13 @@ class _Plan:
         # RCCL without torch.distributed's per-call host cost (created collectively here: every
         # rank builds this plan at the same sync)
         self.comm = rccl_direct.comm_for(self.pg, ws, sb.device) if self.nccl else None
+        # the whole gather region is ONE float / int SUM group and no flag (MulticlassAccuracy's
+        # counters): one out-of-place all_reduce replaces all_gather + the seg_reduce launch
+        gath = [g for g in sb.groups if g.off >= sb.gather_off]
+        self.single = None
+        if (self.comm is not None and not sb.flag_words and len(gath) == 1 and gath[0].off == sb.gather_off
+                and gath[0].op == "sum" and gath[0].dtype != torch.bool):
+            self.single = (gath[0].dtype, gath[0].nbytes)
 
 
 def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
@@ -399,9 +406,15 @@ def _sync_one(m, sb: StateBuffer, plan: _Plan):
             _all_reduce_group(snap[off : off + nb].view(dtype), op, plan.group, _direct(plan))
     merged = None
     if plan.src is not None and not plan.fused:
-        merged = _gather(plan, plan.src)
-        if ws > 1:
-            merged = _reduce_gathered(merged, plan.segs, ws, plan.row_bytes)
+        comm = _direct(plan)
+        if plan.single is not None and comm is not None:
+            dtype, nb = plan.single
+            merged = torch.empty(plan.row_bytes, dtype=torch.uint8, device=sb.device)
+            rccl_direct.all_reduce(comm, plan.src[:nb].view(dtype), "sum", out=merged[:nb].view(dtype))
+        else:
+            merged = _gather(plan, plan.src)
+            if ws > 1:
+                merged = _reduce_gathered(merged, plan.segs, ws, plan.row_bytes)
     r = object.__new__(type(m))  # a shallow copy (copy.copy costs ~4x this)
     d = r.__dict__
     getstate = getattr(type(m), "__getstate__", None)
