@@ -237,6 +237,7 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         def run():
             for i in range(50):
                 m.update_activations(acts[i % 4], i % 2 == 0)
+            m.real_cov_sum, m.fake_cov_sum  # reading the states folds the staged rows in (K8)
         return run
 
     def merge_runs():

@@ -11,6 +11,7 @@ import sys
 
 import torch
 
+os.environ.setdefault("TORCHEVAL_AMD_FID_STAGE_ROWS", "0")  # K8 once per FID update (no staging)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from torcheval_amd import metrics as M  # noqa: E402
