@@ -14,7 +14,7 @@
 
 int main(int argc, char** argv) {
   const int64_t d = 2048;
-  const int64_t ns[] = {1000, 50000};
+  const int64_t ns[] = {1000, 8192, 50000};
   for (int64_t n : ns) {
     float *act, *cov, *cs;
     CK(hipMalloc(&act, n * d * 4));

@@ -36,6 +36,13 @@
 //  * the epilogue stages the tile in LDS (96 x 97, conflict-free transposed read) and updates
 //    C[I, J] and the mirrored C[J, I] with coalesced rows; one block owns each output tile, so
 //    no atomics anywhere.
+// v6 (round 3): the products run on bf16 MFMA (v_mfma_f32_16x16x32_bf16, 16x the FP32 MFMA
+// rate) through an exact three-way bf16 split of each FP32 operand (split3, six products per
+// pair), each 64-row stage summed into fresh accumulators that are added to the running ones
+// on the VALU.  Against the FP32-MFMA form (kept: TORCHEVAL_AMD_K8_EXACT=1) it is 1.05-1.15x
+// faster and more accurate (max error vs fp64 at 50000 x 2048: 1.0e-6 vs 7.7e-6 of max |C|,
+// profiles/k8_split_bf16_sweep_r3.json).  The MFMA pipe is now ~30 % busy: the split's VALU
+// (each wave re-splits the operands it reads; ~290 VALU per wave per stage) is the limit.
 // Rejected in v2 (kept for the record, MI355X, 1000 x 2048): in-block split-K with 2 x 2
 // register blocking of 32 x 32 MFMAs (118 us, 176 VGPRs), BK = 64 (104 us), 8 x 8 super-tile
 // enumeration (86 us), 2-4 stage register prefetch (83-84 us), k-contiguous LDS operands
@@ -68,6 +75,32 @@ static_assert(kStage % (4 * kThreads) == 0, "stage must split evenly into wave-w
 static_assert(kT * kCPad + 2 * kT <= 2 * kBufs * kStage, "epilogue tile + column sums must fit");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// Exact three-way bf16 split of 8 FP32 values into the packed fragments of a
+// v_mfma_f32_16x16x32_bf16 operand: x = x1 + x2 + x3 with x1 = x truncated to its top 8
+// significand bits, x2 = the next 8 of x - x1, x3 = x - x1 - x2 (<= 8 bits, so exact in bf16).
+// Both differences are exact (the subtrahend shares the minuend's leading bits).  Element 2q of
+// a fragment is the low half of dword q, 2q + 1 the high half (v_perm_b32 of the two upper halves).
+__device__ __forceinline__ void split3(const float (&v)[8], u32x4& p1, u32x4& p2, u32x4& p3) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned u0 = __float_as_uint(v[2 * q]), u1 = __float_as_uint(v[2 * q + 1]);
+    const float r0 = v[2 * q] - __uint_as_float(u0 & 0xffff0000u);
+    const float r1 = v[2 * q + 1] - __uint_as_float(u1 & 0xffff0000u);
+    const unsigned w0 = __float_as_uint(r0), w1 = __float_as_uint(r1);
+    const float s0 = r0 - __uint_as_float(w0 & 0xffff0000u);
+    const float s1 = r1 - __uint_as_float(w1 & 0xffff0000u);
+    p1[q] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+    p2[q] = __builtin_amdgcn_perm(w1, w0, 0x07060302u);
+    p3[q] = __builtin_amdgcn_perm(__float_as_uint(s1), __float_as_uint(s0), 0x07060302u);
+  }
+}
+
+__device__ __forceinline__ f32x4 mfma_bf16(const u32x4& a, const u32x4& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+}
 
 // Operand image of one stage: LDS row r (= sample b0 + r) holds the tile's 96 columns rotated
 // by rot(r) floats.  The four rows one ds_read_b32 touches (r = 4q + lk) then start at banks
@@ -89,6 +122,11 @@ __device__ __forceinline__ void tile_coords(int t, int T, int& ti, int& tj) {
   tj = row + rem;
 }
 
+// kX3: the products run on bf16 MFMA through the exact three-way split (split3) - six products
+// per operand pair (x1y1, x1y2, x2y1, x2y2, x1y3, x3y1; the dropped x2y3, x3y2, x3y3 are below
+// 2^-23 |xy|), i.e. FP32-level products at 6/16 of the FP32 MFMA pipe time.  !kX3: exact FP32
+// products on v_mfma_f32_16x16x4_f32.
+template <bool kX3>
 __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T, int tiles, int items, int64_t chunk) {
   const int nb = gridDim.x;
   int item = blockIdx.x;
@@ -162,6 +200,64 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
     offA[m] = (4 * par + lk) * kT + (wr * 48 + 16 * m + li + rl) % kT;
     offB[m] = (4 * par + lk) * kT + (wc * 48 + 16 * m + li + rl) % kT;
   }
+  // bf16 split path: wave parity par takes the stage's rows [32 par, 32 par + 32); fragment
+  // element j of lane group lk is row 32 par + 4 j + lk (the k order inside an MFMA only has to
+  // agree between the two operands), so the four rows one ds_read_b32 touches are consecutive
+  // and carry the four distinct rotations, as in the FP32 path
+  int offA3[3], offB3[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    offA3[m] = (32 * par + lk) * kT + (wr * 48 + 16 * m + li + rl) % kT;
+    offB3[m] = (32 * par + lk) * kT + (wc * 48 + 16 * m + li + rl) % kT;
+  }
+  auto mma_stage_x3 = [&](int buf) {
+    const float* cI = sI + buf * kStage;
+    const float* cJ = sJr + buf * kStage;
+    float av[3][8], bv[3][8];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        av[m][j] = cI[offA3[m] + 4 * j * kT];
+        bv[m][j] = cJ[offB3[m] + 4 * j * kT];
+      }
+    u32x4 a1[3], a2[3], a3[3], b1[3], b2[3], b3[3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      split3(av[m], a1[m], a2[m], a3[m]);
+      split3(bv[m], b1[m], b2[m], b3[m]);
+    }
+    // term-major order: nine independent accumulators between two dependent MFMAs.  The stage
+    // sums into fresh accumulators that are added to the running ones on the VALU (one RNE
+    // rounding per stage): chaining all six split products of every row into the running sum
+    // would round each small term against the whole-K magnitude (measured: 4x the FP32 path's
+    // error at K = 50000; per-stage partials put it below that path)
+    f32x4 sacc[3][3];
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a3[m], b1[n], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a1[m], b3[n], sacc[m][n]);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a2[m], b2[n], sacc[m][n]);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a2[m], b1[n], sacc[m][n]);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a1[m], b2[n], sacc[m][n]);
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+#pragma unroll
+      for (int n = 0; n < 3; ++n) acc[m][n] += mfma_bf16(a1[m], b1[n], sacc[m][n]);
+  };
   auto mma_stage = [&](int buf) {
     const float* cI = sI + buf * kStage;
     const float* cJ = sJr + buf * kStage;
@@ -269,7 +365,8 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
       col_stage(buf);
     } else {
       __builtin_amdgcn_sched_barrier(0);
-      mma_stage(buf);
+      if constexpr (kX3) mma_stage_x3(buf);
+      else mma_stage(buf);
       __builtin_amdgcn_sched_barrier(0);
     }
     wait_next(more);
@@ -301,10 +398,12 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
   __syncthreads();
   float colsum = 0.f;
   if (diag) {
-    // quadrant (1, 0) = quadrant (0, 1) transposed; the column sums of the two row parities
-    for (int e = threadIdx.x; e < 48 * 48; e += kThreads) {
-      const int r = 48 + e / 48, c = e % 48;
-      sC[r * kCPad + c] = sC[c * kCPad + r];
+    // the lower triangle = the upper transposed: quadrant (1, 0) was never computed, and on the
+    // split path the diagonal quadrants' (i, j) and (j, i) sum the same split products in a
+    // different order, so the mirror keeps the result exactly symmetric
+    for (int e = threadIdx.x; e < kT * kT; e += kThreads) {
+      const int r = e / kT, c = e % kT;
+      if (r > c) sC[r * kCPad + c] = sC[c * kCPad + r];
     }
     if (threadIdx.x < kT) colsum = sCol[threadIdx.x] + sCol[kT + threadIdx.x];
     __syncthreads();
@@ -408,6 +507,11 @@ int cu_count() {
 
 }  // namespace
 
+bool fid_cov_exact() {
+  const char* e = std::getenv("TORCHEVAL_AMD_K8_EXACT");
+  return e != nullptr && e[0] == '1';
+}
+
 int fid_cov_split(int64_t n, int64_t d) {
   if (const char* e = std::getenv("TORCHEVAL_AMD_K8_SPLIT")) {
     const int s = std::atoi(e);
@@ -441,11 +545,17 @@ int launch_fid_cov(const FidCovArgs& a, hipStream_t stream) {
   const int64_t chunk = ((stages + split - 1) / split) * kBK;
   const int items = tiles * split;
   const int grid = (items + 7) / 8 * 8;
-  static const bool lds_ok = hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel),
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kSmemBytes) == hipSuccess;
+  static const bool lds_ok =
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kSmemBytes) == hipSuccess &&
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                          kSmemBytes) == hipSuccess;
   if (!lds_ok) return -3;
   if (a.zeros == nullptr || a.ld % 4 != 0 || a.ld < a.d || a.row_stride % 4 != 0) return -1;
-  hipLaunchKernelGGL(fid_syrk_kernel, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
+  if (fid_cov_exact())
+    hipLaunchKernelGGL(fid_syrk_kernel<false>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
+  else
+    hipLaunchKernelGGL(fid_syrk_kernel<true>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
   int rc = static_cast<int>(hipGetLastError());
   if (rc || split == 1) return rc;
   hipLaunchKernelGGL(fid_fixup_kernel, dim3(tiles * 9), dim3(kFixThreads), 0, stream, a, T, tiles);

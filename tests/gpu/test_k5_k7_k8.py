@@ -161,6 +161,43 @@ def test_k8_split_k_matches_fp64(n, d, split, monkeypatch):
     assert torch.equal(again.cpu(), cov.cpu())  # deterministic for a given split
 
 
+@pytest.mark.parametrize("n,d", [(1000, 2048), (333, 300), (64, 128)])
+def test_k8_split_bf16_exact_on_integers(n, d, monkeypatch):
+    """Small-integer activations: every product and partial sum is exact in FP32, so the bf16
+    three-way-split path must reproduce the integer result bit for bit (catches any fragment
+    k-order / lane-map mistake), in both MFMA modes."""
+    g = torch.Generator().manual_seed(n + 3 * d)
+    act = torch.randint(-8, 9, (n, d), generator=g).float()
+    want = (act.long().T @ act.long()).float()
+    for exact in ("0", "1"):
+        monkeypatch.setenv("TORCHEVAL_AMD_K8_EXACT", exact)
+        cov = torch.zeros(d, d, device=DEV)
+        s = torch.zeros(d, device=DEV)
+        native().fid_cov_update(act.to(DEV), cov, s)
+        assert torch.equal(cov.cpu(), want), exact
+        assert torch.equal(s.cpu(), act.sum(0)), exact
+
+
+@pytest.mark.parametrize("scale", [1.0, 1e-3, 1e4])
+def test_k8_split_bf16_error_matches_fp32_mfma(scale, monkeypatch):
+    """The bf16 split path's error against fp64 stays at the FP32-MFMA path's level (the
+    dropped split products are below 2^-23 |xy|), over a wide dynamic range of activations."""
+    g = torch.Generator().manual_seed(11)
+    act = (torch.randn(1000, 2048, generator=g) * torch.exp(torch.randn(1, 2048, generator=g) * 2)) * scale
+    ref = act.double().T @ act.double()
+    errs = {}
+    for exact in ("0", "1"):
+        monkeypatch.setenv("TORCHEVAL_AMD_K8_EXACT", exact)
+        cov = torch.zeros(2048, 2048, device=DEV)
+        native().fid_cov_update(act.to(DEV), cov, None)
+        d = (cov.cpu().double() - ref).abs()
+        # per-element error relative to sum_k |x_ik x_jk|, the scale of FP32 rounding
+        bound = act.double().abs().T @ act.double().abs()
+        errs[exact] = float((d / bound).max())
+    assert errs["0"] < 4 * errs["1"] + 1e-7, errs
+    assert errs["0"] < 2e-6, errs
+
+
 def test_k8_strided_activations():
     g = torch.Generator().manual_seed(3)
     big = torch.randn(50, 2048 + 32, generator=g)
