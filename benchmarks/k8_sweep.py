@@ -2,8 +2,9 @@
 
     python benchmarks/k8_sweep.py [--d 2048 768] [--k 1000 50000] [--splits 0 1 2 3] [--modes x3 exact]
 
-split 0 = the launcher's own choice; mode x3 = bf16 MFMA on the exact three-way split (the
-default), exact = FP32 MFMA (``TORCHEVAL_AMD_K8_EXACT=1``).  Prints one JSON line per (D, K, split): K8 time, the
+split 0 = the launcher's own choice; mode x3 = bf16 MFMA on the exact three-way split staged
+once per block (the default), x3w = the same split done per wave (``TORCHEVAL_AMD_K8_MODE=1``),
+exact = FP32 MFMA (``TORCHEVAL_AMD_K8_EXACT=1``).  Prints one JSON line per (D, K, split): K8 time, the
 rocBLAS/hipBLASLt ``act.T @ act`` time, the effective FP32-MFMA rate of K8 on the
 upper-triangle FLOPs it does (96 x 96 tiles, diagonal tiles full), and the max relative error
 against an fp64 product of the same activations."""
@@ -37,7 +38,7 @@ def main():
     ap.add_argument("--d", type=int, nargs="+", default=[2048])
     ap.add_argument("--k", type=int, nargs="+", default=[128, 1000, 4096, 50000])
     ap.add_argument("--splits", type=int, nargs="+", default=[0])
-    ap.add_argument("--modes", nargs="+", default=["x3", "exact"])
+    ap.add_argument("--modes", nargs="+", default=["x3", "x3w", "exact"])
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     rows = []
@@ -56,10 +57,12 @@ def main():
             t_lib = timeit(lib_update)
             ref = act.double().T @ act.double()
             for mode, sp in [(m, sp) for m in args.modes for sp in args.splits]:
+                os.environ.pop("TORCHEVAL_AMD_K8_EXACT", None)
+                os.environ.pop("TORCHEVAL_AMD_K8_MODE", None)
                 if mode == "exact":
                     os.environ["TORCHEVAL_AMD_K8_EXACT"] = "1"
-                else:
-                    os.environ.pop("TORCHEVAL_AMD_K8_EXACT", None)
+                elif mode == "x3w":
+                    os.environ["TORCHEVAL_AMD_K8_MODE"] = "1"
                 if sp > 0:
                     os.environ["TORCHEVAL_AMD_K8_SPLIT"] = str(sp)
                 else:
@@ -78,6 +81,7 @@ def main():
                 print(json.dumps(row), flush=True)
     os.environ.pop("TORCHEVAL_AMD_K8_SPLIT", None)
     os.environ.pop("TORCHEVAL_AMD_K8_EXACT", None)
+    os.environ.pop("TORCHEVAL_AMD_K8_MODE", None)
     if args.out:
         with open(args.out, "w") as f:
             json.dump(rows, f, indent=1)

@@ -345,8 +345,9 @@ struct FidCovArgs {
 // split-K factor the launcher would pick for [n, d] on this device (env TORCHEVAL_AMD_K8_SPLIT
 // overrides) and the scratch it needs
 int fid_cov_split(int64_t n, int64_t d);
-// products on FP32 MFMA (env TORCHEVAL_AMD_K8_EXACT=1) instead of the exact bf16 three-way split
-bool fid_cov_exact();
+// K8 product path: 2 = bf16 MFMA on the exact three-way split, staged once per block (default);
+// 1 = the same split done per wave (TORCHEVAL_AMD_K8_MODE=1); 0 = FP32 MFMA (TORCHEVAL_AMD_K8_EXACT=1)
+int fid_cov_mode();
 int64_t fid_cov_workspace_bytes(int64_t d, int split);
 int launch_fid_cov(const FidCovArgs& a, hipStream_t stream);
 

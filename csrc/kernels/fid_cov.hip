@@ -39,10 +39,14 @@
 // v6 (round 3): the products run on bf16 MFMA (v_mfma_f32_16x16x32_bf16, 16x the FP32 MFMA
 // rate) through an exact three-way bf16 split of each FP32 operand (split3, six products per
 // pair), each 64-row stage summed into fresh accumulators that are added to the running ones
-// on the VALU.  Against the FP32-MFMA form (kept: TORCHEVAL_AMD_K8_EXACT=1) it is 1.05-1.15x
-// faster and more accurate (max error vs fp64 at 50000 x 2048: 1.0e-6 vs 7.7e-6 of max |C|,
-// profiles/k8_split_bf16_sweep_r3.json).  The MFMA pipe is now ~30 % busy: the split's VALU
-// (each wave re-splits the operands it reads; ~290 VALU per wave per stage) is the limit.
+// on the VALU - more accurate than the FP32-MFMA form (max error vs fp64 at 50000 x 2048:
+// 1.0e-6 vs 7.5e-6 of max |C|).  The block splits every staged element once (kMode 2): each
+// thread loads 8-row column pieces of the next stage with raw buffer loads (out-of-range
+// offsets read 0), splits them while this stage's MFMAs issue (one basic block per stage,
+// sched_group_barrier interleave) and stores the planes in fragment order, so a fragment is
+// one ds_read_b128.  1000 x 2048: 44 us (FP32 form 54 us, hipBLASLt GEMM 76 us); 8192 x 2048:
+// 250 us (326, GEMM 481) - profiles/k8_split_bf16_sweep_r3.json.  The per-wave split (kMode 1,
+// each element split by two waves, VALU-bound) and the FP32 form (kMode 0) stay selectable.
 // Rejected in v2 (kept for the record, MI355X, 1000 x 2048): in-block split-K with 2 x 2
 // register blocking of 32 x 32 MFMAs (118 us, 176 VGPRs), BK = 64 (104 us), 8 x 8 super-tile
 // enumeration (86 us), 2-4 stage register prefetch (83-84 us), k-contiguous LDS operands
@@ -72,7 +76,7 @@ constexpr int kCPad = kT + 1;
 constexpr int kBufs = 3;                    // LDS stages: two LDS-DMA stages in flight
 constexpr int kSmemBytes = 2 * kBufs * kStage * 4;  // 144 KB: one block per CU
 static_assert(kStage % (4 * kThreads) == 0, "stage must split evenly into wave-wide LDS-DMA pieces");
-static_assert(kT * kCPad + 2 * kT <= 2 * kBufs * kStage, "epilogue tile + column sums must fit");
+static_assert(kT * kCPad + 8 * kT <= 2 * kBufs * kStage, "epilogue tile + column sums must fit");
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -122,11 +126,18 @@ __device__ __forceinline__ void tile_coords(int t, int T, int& ti, int& tj) {
   tj = row + rem;
 }
 
-// kX3: the products run on bf16 MFMA through the exact three-way split (split3) - six products
-// per operand pair (x1y1, x1y2, x2y1, x2y2, x1y3, x3y1; the dropped x2y3, x3y2, x3y3 are below
-// 2^-23 |xy|), i.e. FP32-level products at 6/16 of the FP32 MFMA pipe time.  !kX3: exact FP32
-// products on v_mfma_f32_16x16x4_f32.
-template <bool kX3>
+// kMode 1 and 2: the products run on bf16 MFMA through the exact three-way split (split3) - six
+// products per operand pair (x1y1, x1y2, x2y1, x2y2, x1y3, x3y1; the dropped x2y3, x3y2, x3y3
+// are below 2^-23 |xy|), i.e. FP32-level products at 6/16 of the FP32 MFMA pipe time.
+//  * kMode 2 (default): the block splits each staged element once.  Every thread loads whole
+//    8-row column pieces of the next stage into registers (global loads, one stage ahead),
+//    splits them and writes the three bf16 planes to LDS in MFMA fragment order (k-contiguous:
+//    plane[k / 8][column][k % 8]), so a fragment is one ds_read_b128 and the split's VALU is
+//    spread over all 8 waves with no duplication.
+//  * kMode 1: LDS-DMA fp32 staging as in kMode 0; each wave splits the operands it reads
+//    (every element is split by two waves: the VALU is the limit).
+//  * kMode 0: exact FP32 products on v_mfma_f32_16x16x4_f32.
+template <int kMode>
 __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T, int tiles, int items, int64_t chunk) {
   const int nb = gridDim.x;
   int item = blockIdx.x;
@@ -321,7 +332,8 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
   constexpr int kPer4 = (kT * kSeg4 + kThreads - 1) / kThreads;     // 5
   const bool vec4 = a.d % 4 == 0;
   float4 cpre[kPer4], mpre[kPer4];
-  if (a.split == 1 && vec4) {
+  auto prefetch_c = [&]() {
+    if (!(a.split == 1 && vec4)) return;
 #pragma unroll
     for (int q = 0; q < kPer4; ++q) {
       const int e = threadIdx.x + kThreads * q;
@@ -334,7 +346,9 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
       cpre[q] = make_float4(in ? x.x : 0.f, in ? x.y : 0.f, in ? x.z : 0.f, in ? x.w : 0.f);
       mpre[q] = make_float4(min_ ? y.x : 0.f, min_ ? y.y : 0.f, min_ ? y.z : 0.f, min_ ? y.w : 0.f);
     }
-  }
+  };
+  // kMode 2 keeps its next stage in registers during the loop: its C reads go after the loop
+  if constexpr (kMode != 2) prefetch_c();
 
   // ---- K loop: three LDS stages, two LDS-DMA stages in flight behind the MFMAs.  The end of
   // stage s waits only for stage s + 1's pieces (a counted vmcnt leaves stage s + 2's in
@@ -350,6 +364,138 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
     __builtin_amdgcn_s_barrier();
   };
   static_assert(kGlds == 3, "the counted waits above assume 3 pieces per operand per stage");
+
+  // ---- kMode 2: register-staged columns, split once per element into LDS bf16 planes
+  constexpr int kPlaneB = 8 * kT * 16;  // one plane of one operand: [8 k-groups][96 columns] x 16 B
+  constexpr int kOpB = 3 * kPlaneB;      // 36 KB
+  constexpr int kBufB = 2 * kOpB;        // 72 KB per stage, two stages = kSmemBytes
+  static_assert(2 * kBufB <= kSmemBytes, "two plane stages must fit the LDS allocation");
+  constexpr int kUnits = 3;              // (operand, k-group, column) units per thread
+  static_assert(kUnits * kThreads == 2 * 8 * kT, "units must cover both operands' 8 x 96 pieces");
+  float cs2[kUnits] = {0.f, 0.f, 0.f};   // diagonal tiles: per-unit column sums (operand I)
+  if constexpr (kMode == 2) {
+    char* lds = reinterpret_cast<char*>(smem);
+    // raw buffer loads over this item's K range: a byte offset at or past num_records reads 0,
+    // which masks the rows past the range; an invalid unit (a column past the width, or the
+    // J operand of a diagonal tile) starts at 2^31 (the launcher keeps the range below 2^31 B)
+    // (a split-K item past the end has an empty range: num_records 0, every load reads 0)
+    const uint32_t rs4 = static_cast<uint32_t>(a.row_stride) * 4u;
+    const int64_t krows = k1 > k0 ? k1 - k0 : 0;
+    const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.act + (krows ? k0 * a.row_stride : 0)), 0, static_cast<int>(krows * rs4), 0x00020000);
+    uint32_t uvo[kUnits];
+    int uoff[kUnits];
+    bool ucs[kUnits];
+#pragma unroll
+    for (int q = 0; q < kUnits; ++q) {
+      const int u = (w * kUnits + q) * 64 + lane;
+      const int op = u / (8 * kT), g = (u / kT) % 8, col = u % kT;
+      const int64_t x0 = op ? J0 : I0;
+      const bool ok = x0 + col < a.ld && !(diag && op == 1);
+      uvo[q] = ok ? static_cast<uint32_t>(8 * g) * rs4 + static_cast<uint32_t>(x0 + col) * 4u : 0x80000000u;
+      uoff[q] = op * kOpB + (g * kT + col) * 16;
+      ucs[q] = diag && op == 0;
+    }
+    float v[kUnits][8];
+    auto load = [&](int64_t b0) {
+      const uint32_t st = static_cast<uint32_t>(b0 - k0) * rs4;
+#pragma unroll
+      for (int q = 0; q < kUnits; ++q)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          v[q][j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rsrc, uvo[q] + st + j * rs4, 0, 0));
+    };
+    auto split_store = [&](int b) {
+#pragma unroll
+      for (int q = 0; q < kUnits; ++q) {
+        float t = 0.f;  // (branch-free: a divergent branch would split the stage's block)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t += v[q][j];
+        cs2[q] += ucs[q] ? t : 0.f;
+        u32x4 p1, p2, p3;
+        split3(v[q], p1, p2, p3);
+        char* dst = lds + b * kBufB + uoff[q];
+        *reinterpret_cast<u32x4*>(dst) = p1;
+        *reinterpret_cast<u32x4*>(dst + kPlaneB) = p2;
+        *reinterpret_cast<u32x4*>(dst + 2 * kPlaneB) = p3;
+      }
+    };
+    // fragment reads: block column c, k-group 4 par + lk -> one ds_read_b128 per plane
+    const int fa = ((4 * par + lk) * kT + wr * 48 + li) * 16;
+    const int fb = (diag ? 0 : kOpB) + ((4 * par + lk) * kT + wc * 48 + li) * 16;
+    auto mma_planes = [&](int b) {
+      const char* base = lds + b * kBufB;
+      u32x4 a1[3], a2[3], a3[3], b1[3], b2[3], b3[3];
+#pragma unroll
+      for (int m = 0; m < 3; ++m) {
+        const char* pa = base + fa + m * 16 * 16;
+        const char* pb = base + fb + m * 16 * 16;
+        a1[m] = *reinterpret_cast<const u32x4*>(pa);
+        a2[m] = *reinterpret_cast<const u32x4*>(pa + kPlaneB);
+        a3[m] = *reinterpret_cast<const u32x4*>(pa + 2 * kPlaneB);
+        b1[m] = *reinterpret_cast<const u32x4*>(pb);
+        b2[m] = *reinterpret_cast<const u32x4*>(pb + kPlaneB);
+        b3[m] = *reinterpret_cast<const u32x4*>(pb + 2 * kPlaneB);
+      }
+      f32x4 sacc[3][3];
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a3[m], b1[n], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a1[m], b3[n], sacc[m][n]);
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a2[m], b2[n], sacc[m][n]);
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a2[m], b1[n], sacc[m][n]);
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) sacc[m][n] = mfma_bf16(a1[m], b2[n], sacc[m][n]);
+#pragma unroll
+      for (int m = 0; m < 3; ++m)
+#pragma unroll
+        for (int n = 0; n < 3; ++n) acc[m][n] += mfma_bf16(a1[m], b1[n], sacc[m][n]);
+    };
+    load(k0);
+    split_store(0);
+    load(k0 + kBK);
+    __syncthreads();
+    int b = 0;
+    // One basic block per stage, so the next stage's split (VALU), LDS stores and global loads
+    // can be interleaved with this stage's MFMAs (in-order issue: VALU placed after 54 MFMAs
+    // would wait for all of them to issue).  Past the K range the loads read the zero line and
+    // the last stores land in a buffer nobody reads (the loop's final barrier orders them
+    // before the epilogue reuses the LDS).  Every wave runs the MFMAs: on a diagonal tile the
+    // quadrant (1, 0) result is discarded by the mirror, and the column sums come from the
+    // staging units instead.
+    for (int64_t b0 = k0; b0 < k1; b0 += kBK) {
+      __builtin_amdgcn_sched_barrier(0);
+      mma_planes(b);
+      split_store(b ^ 1);  // the other stage's readers all passed the previous barrier
+      load(b0 + 2 * kBK);
+#if TEA_K8_SCHED
+      __builtin_amdgcn_sched_group_barrier(0x100, 18, 0);  // fragment reads
+#pragma unroll
+      for (int i = 0; i < 54; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);  // three VALU of the next stage's split
+      }
+      __builtin_amdgcn_sched_group_barrier(0x200, 9, 0);   // plane stores
+      __builtin_amdgcn_sched_group_barrier(0x020, 24, 0);  // next loads
+#endif
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      b ^= 1;
+    }
+    prefetch_c();
+  } else {
   issue(0, k0);
   const bool two = k0 + kBK < k1;
   if (two) issue(1, k0 + kBK);
@@ -365,18 +511,19 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
       col_stage(buf);
     } else {
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (kX3) mma_stage_x3(buf);
+      if constexpr (kMode == 1) mma_stage_x3(buf);
       else mma_stage(buf);
       __builtin_amdgcn_sched_barrier(0);
     }
     wait_next(more);
     buf = buf == 2 ? 0 : buf + 1;
   }
+  }  // kMode 0 / 1
 
   // ---- sum the two k-parity halves of each quadrant in LDS (96 x 97 floats, reusing the
   // operand buffers; the loop's last barrier retired every operand read)
   float* sC = smem;
-  float* sCol = smem + kCPad * kT;  // [2][kT]: the column-sum waves' partials
+  float* sCol = smem + kCPad * kT;  // [2][kT] (kMode 2: [8][kT]): the column-sum partials
   auto to_lds = [&](bool add) {
 #pragma unroll
     for (int m = 0; m < 3; ++m)
@@ -388,7 +535,15 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
           sC[idx] = add ? sC[idx] + acc[m][n][r] : acc[m][n][r];
         }
   };
-  if (col_wave) {
+  if constexpr (kMode == 2) {
+    if (diag) {  // sCol [8 k-groups][kT]: unit (0, g, col) -> sCol[g * kT + col]
+#pragma unroll
+      for (int q = 0; q < kUnits; ++q) {
+        const int u = (w * kUnits + q) * 64 + lane;
+        if (u < 8 * kT) sCol[u] = cs2[q];
+      }
+    }
+  } else if (col_wave) {
     sCol[par * kT + lane] = colsum0;
     if (lane < kT - 64) sCol[par * kT + 64 + lane] = colsum1;
   }
@@ -405,7 +560,14 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
       const int r = e / kT, c = e % kT;
       if (r > c) sC[r * kCPad + c] = sC[c * kCPad + r];
     }
-    if (threadIdx.x < kT) colsum = sCol[threadIdx.x] + sCol[kT + threadIdx.x];
+    if (threadIdx.x < kT) {
+      if constexpr (kMode == 2) {
+#pragma unroll
+        for (int g = 0; g < 8; ++g) colsum += sCol[g * kT + threadIdx.x];
+      } else {
+        colsum = sCol[threadIdx.x] + sCol[kT + threadIdx.x];
+      }
+    }
     __syncthreads();
   }
 
@@ -507,9 +669,12 @@ int cu_count() {
 
 }  // namespace
 
-bool fid_cov_exact() {
+int fid_cov_mode() {
   const char* e = std::getenv("TORCHEVAL_AMD_K8_EXACT");
-  return e != nullptr && e[0] == '1';
+  if (e != nullptr && e[0] == '1') return 0;
+  const char* m = std::getenv("TORCHEVAL_AMD_K8_MODE");
+  if (m != nullptr && (m[0] == '0' || m[0] == '1')) return m[0] - '0';
+  return 2;
 }
 
 int fid_cov_split(int64_t n, int64_t d) {
@@ -545,17 +710,27 @@ int launch_fid_cov(const FidCovArgs& a, hipStream_t stream) {
   const int64_t chunk = ((stages + split - 1) / split) * kBK;
   const int items = tiles * split;
   const int grid = (items + 7) / 8 * 8;
-  static const bool lds_ok =
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel<true>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          kSmemBytes) == hipSuccess &&
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&fid_syrk_kernel<false>), hipFuncAttributeMaxDynamicSharedMemorySize,
-                          kSmemBytes) == hipSuccess;
+  auto opt_in = [](const void* f) {
+    return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kSmemBytes) == hipSuccess;
+  };
+  static const bool lds_ok = opt_in(reinterpret_cast<const void*>(&fid_syrk_kernel<0>)) &&
+                             opt_in(reinterpret_cast<const void*>(&fid_syrk_kernel<1>)) &&
+                             opt_in(reinterpret_cast<const void*>(&fid_syrk_kernel<2>));
   if (!lds_ok) return -3;
   if (a.zeros == nullptr || a.ld % 4 != 0 || a.ld < a.d || a.row_stride % 4 != 0) return -1;
-  if (fid_cov_exact())
-    hipLaunchKernelGGL(fid_syrk_kernel<false>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
-  else
-    hipLaunchKernelGGL(fid_syrk_kernel<true>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
+  int mode = fid_cov_mode();
+  // kMode 2 addresses an item's K range (+ two stages of overrun) with 32-bit buffer offsets
+  if (mode == 2 && (chunk + 2 * kBK) * a.row_stride * 4 >= (int64_t{1} << 31)) mode = 1;
+  switch (mode) {
+    case 0:
+      hipLaunchKernelGGL(fid_syrk_kernel<0>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
+      break;
+    case 1:
+      hipLaunchKernelGGL(fid_syrk_kernel<1>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
+      break;
+    default:
+      hipLaunchKernelGGL(fid_syrk_kernel<2>, dim3(grid), dim3(kThreads), kSmemBytes, stream, a, T, tiles, items, chunk);
+  }
   int rc = static_cast<int>(hipGetLastError());
   if (rc || split == 1) return rc;
   hipLaunchKernelGGL(fid_fixup_kernel, dim3(tiles * 9), dim3(kFixThreads), 0, stream, a, T, tiles);

@@ -161,7 +161,19 @@ def test_k8_split_k_matches_fp64(n, d, split, monkeypatch):
     assert torch.equal(again.cpu(), cov.cpu())  # deterministic for a given split
 
 
-@pytest.mark.parametrize("n,d", [(1000, 2048), (333, 300), (64, 128)])
+K8_MODES = ("shared", "wave", "exact")  # kMode 2 (default), 1, 0 of fid_cov.hip
+
+
+def _k8_mode(monkeypatch, mode: str) -> None:
+    monkeypatch.delenv("TORCHEVAL_AMD_K8_EXACT", raising=False)
+    monkeypatch.delenv("TORCHEVAL_AMD_K8_MODE", raising=False)
+    if mode == "exact":
+        monkeypatch.setenv("TORCHEVAL_AMD_K8_EXACT", "1")
+    elif mode == "wave":
+        monkeypatch.setenv("TORCHEVAL_AMD_K8_MODE", "1")
+
+
+@pytest.mark.parametrize("n,d", [(1000, 2048), (333, 300), (64, 128), (130, 2048)])
 def test_k8_split_bf16_exact_on_integers(n, d, monkeypatch):
     """Small-integer activations: every product and partial sum is exact in FP32, so the bf16
     three-way-split path must reproduce the integer result bit for bit (catches any fragment
@@ -169,13 +181,13 @@ def test_k8_split_bf16_exact_on_integers(n, d, monkeypatch):
     g = torch.Generator().manual_seed(n + 3 * d)
     act = torch.randint(-8, 9, (n, d), generator=g).float()
     want = (act.long().T @ act.long()).float()
-    for exact in ("0", "1"):
-        monkeypatch.setenv("TORCHEVAL_AMD_K8_EXACT", exact)
+    for mode in K8_MODES:
+        _k8_mode(monkeypatch, mode)
         cov = torch.zeros(d, d, device=DEV)
         s = torch.zeros(d, device=DEV)
         native().fid_cov_update(act.to(DEV), cov, s)
-        assert torch.equal(cov.cpu(), want), exact
-        assert torch.equal(s.cpu(), act.sum(0)), exact
+        assert torch.equal(cov.cpu(), want), mode
+        assert torch.equal(s.cpu(), act.sum(0)), mode
 
 
 @pytest.mark.parametrize("scale", [1.0, 1e-3, 1e4])
@@ -186,16 +198,17 @@ def test_k8_split_bf16_error_matches_fp32_mfma(scale, monkeypatch):
     act = (torch.randn(1000, 2048, generator=g) * torch.exp(torch.randn(1, 2048, generator=g) * 2)) * scale
     ref = act.double().T @ act.double()
     errs = {}
-    for exact in ("0", "1"):
-        monkeypatch.setenv("TORCHEVAL_AMD_K8_EXACT", exact)
+    bound = act.double().abs().T @ act.double().abs()
+    for mode in K8_MODES:
+        _k8_mode(monkeypatch, mode)
         cov = torch.zeros(2048, 2048, device=DEV)
         native().fid_cov_update(act.to(DEV), cov, None)
         d = (cov.cpu().double() - ref).abs()
         # per-element error relative to sum_k |x_ik x_jk|, the scale of FP32 rounding
-        bound = act.double().abs().T @ act.double().abs()
-        errs[exact] = float((d / bound).max())
-    assert errs["0"] < 4 * errs["1"] + 1e-7, errs
-    assert errs["0"] < 2e-6, errs
+        errs[mode] = float((d / bound).max())
+    for mode in ("shared", "wave"):
+        assert errs[mode] < 2 * errs["exact"] + 1e-7, errs
+        assert errs[mode] < 2e-6, errs
 
 
 def test_k8_strided_activations():
