@@ -21,7 +21,11 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&cov, d * d * 4));
     CK(hipMalloc(&cs, d * 4));
     std::vector<float> h(n * d);
-    for (size_t i = 0; i < h.size(); ++i) h[i] = static_cast<float>((i * 2654435761u) % 1000) / 1000.f - 0.5f;
+    uint64_t st = 0x9e3779b97f4a7c15ull;  // full-mantissa uniform values in [-1, 1)
+    for (size_t i = 0; i < h.size(); ++i) {
+      st = st * 6364136223846793005ull + 1442695040888963407ull;
+      h[i] = static_cast<float>(static_cast<int32_t>(st >> 32)) * 4.656612873e-10f;
+    }
     CK(hipMemcpy(act, h.data(), n * d * 4, hipMemcpyHostToDevice));
     CK(hipMemset(cov, 0, d * d * 4));
     tea::FidCovArgs a;

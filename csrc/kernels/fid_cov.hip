@@ -44,7 +44,9 @@
 // thread loads 8-row column pieces of the next stage with raw buffer loads (out-of-range
 // offsets read 0), splits them while this stage's MFMAs issue (one basic block per stage,
 // sched_group_barrier interleave) and stores the planes in fragment order, so a fragment is
-// one ds_read_b128.  1000 x 2048: 44 us (FP32 form 54 us, hipBLASLt GEMM 76 us); 8192 x 2048:
+// one ds_read_b128.  Measured and dropped: a second register stage (loads two stages ahead)
+// was 0-5 % slower; the loop is then bound by the per-CU load rate (48 KB per stage per CU,
+// ~10 B/cycle/CU; without the loads the loop runs 24 % faster).  1000 x 2048: 44 us (FP32 form 54 us, hipBLASLt GEMM 76 us); 8192 x 2048:
 // 250 us (326, GEMM 481) - profiles/k8_split_bf16_sweep_r3.json.  The per-wave split (kMode 1,
 // each element split by two waves, VALU-bound) and the FP32 form (kMode 0) stay selectable.
 // Rejected in v2 (kept for the record, MI355X, 1000 x 2048): in-block split-K with 2 x 2
@@ -479,7 +481,9 @@ __global__ __launch_bounds__(kThreads) void fid_syrk_kernel(FidCovArgs a, int T,
       __builtin_amdgcn_sched_barrier(0);
       mma_planes(b);
       split_store(b ^ 1);  // the other stage's readers all passed the previous barrier
+#ifndef TEA_K8_NO_STAGE_LOADS  // (csrc/bench/k8_variants.hip: the loop without its global loads)
       load(b0 + 2 * kBK);
+#endif
 #if TEA_K8_SCHED
       __builtin_amdgcn_sched_group_barrier(0x100, 18, 0);  // fragment reads
 #pragma unroll
