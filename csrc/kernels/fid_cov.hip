@@ -692,7 +692,9 @@ int fid_cov_split(int64_t n, int64_t d) {
   if (tiles * 4 >= cus * 3) return 1;  // the triangle fills >= 3/4 of the CUs already
   const int64_t stages = (n + kBK - 1) / kBK;
   int64_t s = cus / tiles;               // one item per CU
-  s = std::min<int64_t>(s, stages / 2);  // keep >= 2 stages (128 rows) per item
+  // keep >= 4 stages (256 rows) per item: at K = 1000, D = 512 / 768 a split of 4 beats the
+  // 7-8 that "one item per CU" gives (22.6 vs 24.6 us, 24.4 vs 26.2; profiles/k8_smalld_splits_r3.json)
+  s = std::min<int64_t>(s, stages / 4);
   return static_cast<int>(std::max<int64_t>(s, 1));
 }
 
