@@ -51,7 +51,19 @@ def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
         src = dist.get_global_rank(group, 0) if group is not None else 0
         dist.broadcast(dev_uid, src=src, group=group)
         uid = dev_uid.cpu()
-    handle = int(native().rccl_comm_init(uid, ws, rank, device.index if device.index is not None else 0))
+    try:
+        handle: Optional[int] = int(native().rccl_comm_init(uid, ws, rank, device.index if device.index is not None else 0))
+    except RuntimeError:
+        handle = None
+    if ws > 1:
+        # every rank must take the same path: one failed init sends the whole group back to
+        # torch.distributed (a rank-dependent choice would pair a direct collective with a
+        # torch.distributed one and hang)
+        ok = torch.tensor([1 if handle is not None else 0], dtype=torch.int32, device=device)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+        if int(ok.item()) == 0 and handle is not None:
+            native().rccl_comm_destroy(handle)
+            handle = None
     _COMMS[id(group)] = (group, ws, handle)
     return handle
 
@@ -76,6 +88,8 @@ def destroy_all() -> None:
     if not native_loaded():
         return
     for _, _, handle in list(_COMMS.values()):
+        if handle is None:
+            continue
         try:
             native().rccl_comm_destroy(handle)
         except RuntimeError:
