@@ -213,6 +213,7 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   __shared__ D2 lds[kT / 64];
   __shared__ double s_bound[3];    // TP before the entering group; TP, FP at the leaving group's tail
   __shared__ int s_flags[2];
+  __shared__ int s_fb[2];          // a straddling group longer than the window: binary search
   __shared__ int s_hmax[kT / 64], s_tmin[kT / 64];
   __shared__ int64_t s_pos;
 
@@ -334,8 +335,51 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
   if (lane_id() == 63) t_excl = kTile;
   t_excl = min(t_excl, tmin_after);
 
-  // tie groups straddling the tile edges (block-uniform branches, rare)
-  if (s_flags[0]) {
+  // tie groups straddling the tile edges (block-uniform branches).  Not rare: 1M uniform f32
+  // scores give ~3 % equal neighbours, so ~60 of ~1000 tiles have a straddling group, and the
+  // kernel lasts as long as its slowest block.  A group that ends (starts) within kWin samples
+  // beyond the edge is resolved from ONE window load: wave 0 (head side) / wave 1 (tail side)
+  // load the kWin keys and (a, b) past the edge, the equal ones are the group's part there, and
+  // their sums correct the tile's own prefix (TP before the group = TP before the tile - their
+  // a; TP / FP at the group's tail = TP / FP at the tile's end + their a / b).  Only a group
+  // covering the whole window falls back to the binary search + partial-tile reduction (~20
+  // dependent global round trips: it made the kernel 19 us at 1M samples).
+  constexpr int kWin = 64;
+  if (threadIdx.x == 0) s_fb[0] = s_fb[1] = 0;
+  __syncthreads();
+  if (s_flags[0] && w == 0) {
+    const K v0 = __shfl(key[0], 0, 64);  // key(base): thread 0's first sample
+    const int64_t i = base - kWin + lane_id();  // base >= kTile > kWin on this path
+    const K kk = key_at<K>(a, r, i);
+    const float2 ab_i = load_ab<DIRECT>(a, ab, r, i);
+    const bool eq = kk == v0;
+    const unsigned long long m = __ballot(eq);
+    const double sa = wave_sum(eq ? static_cast<double>(ab_i.x) : 0.0);
+    if (lane_id() == 0) {
+      if (m & 1ull) s_fb[0] = 1;  // the group may reach further back
+      else s_bound[0] = t0.x - sa;
+    }
+  }
+  if (s_flags[1] && w == 1) {
+    const K v1 = key_at<K>(a, r, base + tile_n - 1);
+    const int64_t i = base + tile_n + lane_id();
+    const bool valid = i < a.n;
+    const K kk = key_at<K>(a, r, valid ? i : a.n - 1);
+    const float2 ab_i = load_ab<DIRECT>(a, ab, r, valid ? i : a.n - 1);
+    const bool eq = valid && kk == v1;
+    const unsigned long long m = __ballot(eq);
+    const double sa = wave_sum(eq ? static_cast<double>(ab_i.x) : 0.0);
+    const double sb = wave_sum(eq ? static_cast<double>(ab_i.y) : 0.0);
+    if (lane_id() == 0) {
+      if (m >> 63) s_fb[1] = 1;  // the group may reach further on
+      else {
+        s_bound[1] = t0.x + tot.x + sa;
+        s_bound[2] = t0.y + tot.y + sb;
+      }
+    }
+  }
+  __syncthreads();
+  if (s_fb[0]) {
     if (threadIdx.x == 0) s_pos = first_equal<K>(a, r, 0, base, key_at<K>(a, r, base));
     __syncthreads();
     const int64_t hpos = s_pos;
@@ -345,7 +389,7 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
     if (threadIdx.x == 0) s_bound[0] = hs.x + part.x;
     __syncthreads();
   }
-  if (s_flags[1]) {
+  if (s_fb[1]) {
     if (threadIdx.x == 0)
       s_pos = last_equal<K>(a, r, base + tile_n, a.n, key_at<K>(a, r, base + tile_n - 1));
     __syncthreads();

@@ -41,6 +41,26 @@ def test_k3_binary_matches_cpu(n, levels):
     torch.testing.assert_close(pr_g.cpu(), pr_c, rtol=1e-9, atol=1e-12)
 
 
+@pytest.mark.parametrize("weighted", [False, True])
+def test_k3_tie_groups_at_the_window_edges(weighted):
+    """Tie groups of every length around the 64-sample window that resolves a group straddling a
+    1024-sample tile edge (1-3, 62-66, 127-129, 1000+): the window path, its fallback to the
+    binary search, and groups spanning whole tiles, against the CPU fp64 reference."""
+    g = torch.Generator().manual_seed(17 + weighted)
+    sizes = torch.tensor([1, 2, 3, 62, 63, 64, 65, 66, 127, 128, 129, 1500])
+    reps = sizes[torch.randint(0, len(sizes), (2500,), generator=g)]
+    vals = torch.randperm(len(reps), generator=g).float() / len(reps)
+    x = torch.repeat_interleave(vals, reps)
+    x = x[torch.randperm(len(x), generator=g)]
+    n = len(x)
+    t = torch.randint(0, 2, (n,), generator=g)
+    w = torch.rand(n, generator=g) if weighted else None
+    roc_c, pr_c = binary_areas(x, t, w, roc=True, pr=True)
+    roc_g, pr_g = binary_areas(x.to(DEV), t.to(DEV), None if w is None else w.to(DEV), roc=True, pr=True)
+    torch.testing.assert_close(roc_g.cpu(), roc_c, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(pr_g.cpu(), pr_c, rtol=1e-9, atol=1e-12)
+
+
 def test_k3_all_equal_scores_and_degenerate():
     for x, t in [
         (torch.full((20000,), 0.5), torch.randint(0, 2, (20000,))),
