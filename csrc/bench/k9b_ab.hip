@@ -29,7 +29,7 @@ int main() {
     return 1;
   hipMemset(gran, 0, gbytes);
   hipMemcpy(dA, h.data(), (size_t)n * n * 8, hipMemcpyHostToDevice);
-  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.gran = gran; a.ctl = ctl;
+  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.slots = gran; a.ctl = ctl;
   for (int it = 0; it < 4; ++it) {
     hipEvent_t e0, e1;
     hipEventCreate(&e0);

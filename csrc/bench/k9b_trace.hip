@@ -46,9 +46,8 @@ int main() {
   CK(hipMemset(trace, 0, 2 * 16 * 8 * 8));
   CK(hipMemcpy(dA, h.data(), (size_t)n * n * 8, hipMemcpyHostToDevice));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(tea::g_symeig_trace), &trace, sizeof(trace)));
-  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.gran = gran; a.ctl = ctl;
+  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.slots = gran; a.ctl = ctl;
   for (int it = 0; it < 3; ++it) {
-    a.tag_base = (unsigned)(it + 1) << 12;
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));

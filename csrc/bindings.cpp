@@ -982,28 +982,14 @@ int64_t sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) {
   a.a = m.data_ptr<double>();
   a.n = n;
   a.ld = tea::symeig_slot_stride(n);
-  // layout: ctl (2 KB), d [ld], e [ld], then 4 granule planes [n-2, ld].  The granules must
-  // never match a phase tag by accident: the block is zeroed whenever the workspace call
-  // (re)allocates it (its own "fresh" flag, not a pointer map that a recycled address could
-  // fool) and again whenever the 20-bit launch counter in the tags wraps, so a stale granule
-  // can never carry a tag of the current launch.  Only this op writes the block.
-  const int64_t bytes = 2048 + (2 * a.ld + 4 * (n - 2) * a.ld) * (int64_t)sizeof(double);
-  {
-    static std::mutex mu;
-    static unsigned launches = 0;
-    std::lock_guard<std::mutex> lock(mu);
-    bool fresh = false;
-    char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3, &fresh));
-    launches = launches % 0xFFFFFu + 1u;
-    if (fresh || launches == 1u)
-      TORCH_CHECK(hipMemsetAsync(ws, 0, bytes, stream) == hipSuccess, "sym_eigvals: workspace memset failed");
-    a.tag_base = launches << 12;  // phase tags tag_base | (q + 1), q + 1 < 4096
-    a.ctl = reinterpret_cast<unsigned*>(ws);
-  }
-  char* ws = reinterpret_cast<char*>(a.ctl);
+  // layout: ctl (2 KB), d [ld], e [ld], then the 2 hand-off slot planes (sentinel-filled by
+  // the launcher on every call, so no state carries over between launches)
+  const int64_t bytes = 2048 + 2 * a.ld * (int64_t)sizeof(double) + tea::symeig_slot_bytes(n);
+  char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3));
+  a.ctl = reinterpret_cast<unsigned*>(ws);
   a.d = reinterpret_cast<double*>(ws + 2048);
   a.e = a.d + a.ld;
-  a.gran = reinterpret_cast<unsigned long long*>(a.e + a.ld);
+  a.slots = reinterpret_cast<unsigned long long*>(a.e + a.ld);
   a.lam = lam.data_ptr<double>();
   const int rc = tea::launch_symeig(a, stream);
   if (rc == 1 || rc == 3) return rc;

@@ -441,14 +441,14 @@ struct SymEigArgs {
   double* d = nullptr;        // [n] tridiagonal diagonal (workspace)
   double* e = nullptr;        // [n] off-diagonal (workspace)
   double* lam = nullptr;      // [n] eigenvalues, ascending
-  unsigned long long* gran = nullptr;  // 4 planes of [n - 2, ld] tagged hand-off granules
-                                       // (zero when first allocated)
-  unsigned tag_base = 0;      // non-zero, multiple of 4096, different for every launch
+  unsigned long long* slots = nullptr;  // 2 planes of [n - 2, ld] hand-off slots,
+                                        // symeig_slot_bytes(n) (sentinel-filled by the launcher)
   unsigned* ctl = nullptr;    // 128 B: ctl[1] abort word (zeroed by the launcher)
 };
 // 0 when the LDS-resident one-launch reduction fits this device (grid / rows per block out)
 int symeig_plan(int64_t n, int* grid, int* rows_per_block);
 int64_t symeig_slot_stride(int64_t n);
+int64_t symeig_slot_bytes(int64_t n);
 // 0 launched, 1 unsupported size, 2 HIP error, 3 cooperative launch refused
 int launch_symeig(const SymEigArgs& a, hipStream_t stream);
 

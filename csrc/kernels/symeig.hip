@@ -18,12 +18,16 @@
 //   row j+1 itself (so row j+1 is never re-published), derives the next reflector v_{j+1}
 //   redundantly, and then ONE LDS pass over its rows both applies A -= v_j w_j^T + w_j v_j^T
 //   and accumulates the next p_{j+1} = tau_{j+1} A v_{j+1}.
-// Hand-offs follow the guide's write-through form: payload stored with agent-scope
-// (write-through) stores into a slot used by exactly one phase, drained, then one relaxed
-// counter add per workgroup; consumers poll the counter and read the payload with agent-scope
-// loads (L1 bypass), so no acquire fence per phase.  Every spin is bounded: a timed-out
-// workgroup raises an abort word that every poller checks, the grid drains, and the host
-// falls back to rocSOLVER when the status word is non-zero.
+// Hand-offs: every handed-off double has its own 8-byte slot, used by exactly one phase of the
+// launch; the launcher fills the slot planes with all-one bytes (a NaN pattern no stored value
+// carries: every NaN is canonicalised to the default quiet NaN on the way out), the producer
+// writes each value with ONE agent-scope (write-through) store, and consumers poll their slots
+// with agent-scope loads until none is the sentinel - the data IS the flag: no drain, no
+// counter, no fence.  (Round 2's form carried {32-bit phase tag, 32-bit half} granules, two per
+// double; the sentinel form halves the bytes the 256 consumers re-read every column:
+// 16.99 -> 16.25 ms at D = 2048, profiles/symeig_handoff_ab_r3.json.)  Every spin is bounded:
+// a timed-out workgroup raises an abort word that every poller checks, the grid drains, and
+// the host falls back to rocSOLVER when the status word is non-zero.
 //
 // The tridiagonal eigenvalues then come from ``tridiag_eigvals_kernel``: one wave per
 // eigenvalue index (16 or 64 lanes), multisection of the Gershgorin interval with Sturm counts
@@ -65,25 +69,21 @@ __device__ unsigned long long* g_symeig_trace;
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 typedef __attribute__((address_space(1))) unsigned gu32;
 
-// Hand-offs are 8-byte granules {tag, 32 bits of payload}: a double travels as a hi and a lo
-// granule in two planes.  One agent-scope (write-through) store each; the consumer polls the
-// granules themselves with agent-scope loads until every tag is the phase's, so the data IS
-// the flag: no drain, no counter, no fence.
-__device__ __forceinline__ void put(unsigned long long* g, int64_t plane, int64_t i, double x,
-                                    unsigned tag) {
-  const unsigned long long t = static_cast<unsigned long long>(tag) << 32;
-  __hip_atomic_store((gu64*)(g + i), t | static_cast<unsigned>(__double2hiint(x)), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store((gu64*)(g + plane + i), t | static_cast<unsigned>(__double2loint(x)),
-                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// the sentinel every slot holds until its phase stores it
+constexpr unsigned long long kSentBits = ~0ull;
+
+__device__ __forceinline__ void put(unsigned long long* g, int64_t i, double x) {
+  const unsigned long long b =
+      x != x ? 0x7ff8000000000000ull : static_cast<unsigned long long>(__double_as_longlong(x));
+  __hip_atomic_store((gu64*)(g + i), b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __forceinline__ unsigned long long get(unsigned long long* g) {
   return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__device__ __forceinline__ double join(unsigned long long hi, unsigned long long lo) {
-  return __hiloint2double(static_cast<int>(static_cast<unsigned>(hi)), static_cast<int>(static_cast<unsigned>(lo)));
+__device__ __forceinline__ double as_double(unsigned long long b) {
+  return __longlong_as_double(static_cast<long long>(b));
 }
 
 template <int Ctrl>
@@ -192,23 +192,21 @@ __device__ __forceinline__ void make_v(const double (&a)[C], const Reflector& h,
   }
 }
 
-// One workgroup per CU; dynamic LDS = R * n doubles (the owned rows).  Granule planes of
-// [n - 2, ld] each at gran + {0, 1, 2, 3} * plane: p_q hi / lo, then row q+1 (as updated
-// through step q-1) hi / lo; phase q's tag is tag_base | (q + 1) (tag_base changes every launch,
-// the workspace is zeroed when allocated, so no stale granule matches).  ctl[1] = abort word,
-// zeroed by the launcher.
+// One workgroup per CU; dynamic LDS = R * n doubles (the owned rows).  Slot planes of
+// [n - 2, ld] each at slots + {0, 1} * plane: p_q, then row q+1 (as updated through step q-1);
+// all sentinel-filled by the launcher.  ctl[1] = abort word, zeroed by the launcher.
 template <int C, int RM>
 __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restrict__ A, int n,
                                                            int R, int64_t ld, double* d_out,
-                                                           double* e_out, unsigned long long* gran,
-                                                           unsigned tag_base, unsigned* ctl) {
+                                                           double* e_out, unsigned long long* slots,
+                                                           unsigned* ctl) {
   extern __shared__ double rows[];
   __shared__ double red[3][16 * RM];
   __shared__ double bc[2][4];  // single-element broadcasts riding on the reductions' barriers
   __shared__ double vw[2][RM];
   const int64_t plane = (int64_t)(n - 2) * ld;
-  unsigned long long* const gp0 = gran;              // p planes
-  unsigned long long* const gr0 = gran + 2 * plane;  // row planes
+  unsigned long long* const gp0 = slots;          // p plane
+  unsigned long long* const gr0 = slots + plane;  // row plane
 
   const int t = threadIdx.x;
   const int row0 = blockIdx.x * R;
@@ -244,12 +242,12 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       }
     }
     const double pt = block_sum_own<RM>(acc, red[2]);
-    if (t < nrows && row0 + t >= 1) put(gp0, plane, row0 + t, h.tau * pt, tag_base | 1u);
+    if (t < nrows && row0 + t >= 1) put(gp0, row0 + t, h.tau * pt);
     if (1 >= row0 && 1 < row0 + nrows) {
 #pragma unroll
       for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
-        if (k >= 1 && k < n) put(gr0, plane, k, rows[(1 - row0) * n + k], tag_base | 1u);
+        if (k >= 1 && k < n) put(gr0, k, rows[(1 - row0) * n + k]);
       }
     }
   }
@@ -258,11 +256,10 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
   // pass measured slower - 19.4 vs 17.9 ms at D = 2048: the branches split the batched loads.)
   for (int j = 0; j <= n - 3; ++j) {
     // ---- w_j from the gathered p_j; row j+1 updated through step j.  Each thread polls the
-    // granules of ITS columns until all carry this phase's tag (bounded; any abort ends the
+    // slots of ITS columns until none holds the sentinel (bounded; any abort ends the
     // block at the reduction barrier below)
     unsigned long long* const gp = gp0 + (int64_t)j * ld;
     unsigned long long* const gr = gr0 + (int64_t)j * ld;
-    const unsigned tag = tag_base | (unsigned)(j + 1);
     bool aborted = false;
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
@@ -270,12 +267,10 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
         if (k >= j + 1 && k < n) {
-          const unsigned long long x0 = get(gp + k), x1 = get(gp + plane + k);
-          const unsigned long long y0 = get(gr + k), y1 = get(gr + plane + k);
-          ok = ok && (unsigned)(x0 >> 32) == tag && (unsigned)(x1 >> 32) == tag &&
-               (unsigned)(y0 >> 32) == tag && (unsigned)(y1 >> 32) == tag;
-          w[s] = join(x0, x1);
-          a[s] = join(y0, y1);
+          const unsigned long long x0 = get(gp + k), y0 = get(gr + k);
+          ok = ok && x0 != kSentBits && y0 != kSentBits;
+          w[s] = as_double(x0);
+          a[s] = as_double(y0);
         } else {
           w[s] = 0.0;
           a[s] = 0.0;
@@ -370,18 +365,17 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     // the owner of row j+2 publishes the row before the p reduction (each thread re-reads
     // only the LDS words it wrote itself)
     SYM_TRACE(j, 3);
-    const unsigned tag1 = tag_base | (unsigned)(j + 2);
     const int ro = (j + 2) - row0;
     if (ro >= 0 && ro < nrows) {
 #pragma unroll
       for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
-        if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, plane, k, rows[ro * n + k], tag1);
+        if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, k, rows[ro * n + k]);
       }
     }
     const double pt = block_sum_own<RM>(acc, red[2]);
     SYM_TRACE(j, 4);
-    if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, plane, row0 + t, hn.tau * pt, tag1);
+    if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, row0 + t, hn.tau * pt);
 #pragma unroll
     for (int s = 0; s < C; ++s) v[s] = vn[s];
     h = hn;
@@ -497,6 +491,8 @@ int symeig_plan(int64_t n, int* grid, int* rows_per_block) {
 
 int64_t symeig_slot_stride(int64_t n) { return (n + 15) / 16 * 16; }
 
+int64_t symeig_slot_bytes(int64_t n) { return 2 * (n - 2) * symeig_slot_stride(n) * (int64_t)sizeof(unsigned long long); }
+
 int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   int G = 0, R = 0;
   if (symeig_plan(a.n, &G, &R) != 0) return 1;
@@ -509,14 +505,14 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
     return 2;
   if (hipMemsetAsync(a.ctl, 0, kCtlBytes, stream) != hipSuccess) return 2;
+  if (hipMemsetAsync(a.slots, 0xff, (size_t)symeig_slot_bytes(a.n), stream) != hipSuccess) return 2;
   const double* A = a.a;
   int n = (int)a.n;
   int64_t ld = a.ld;
   double *d = a.d, *e = a.e;
-  unsigned long long* gran = a.gran;
-  unsigned tag_base = a.tag_base;
+  unsigned long long* slots = a.slots;
   unsigned* ctl = a.ctl;
-  void* args[] = {&A, &n, &R, &ld, &d, &e, &gran, &tag_base, &ctl};
+  void* args[] = {&A, &n, &R, &ld, &d, &e, &slots, &ctl};
   if (hipLaunchCooperativeKernel(kern, dim3(G),
                                  dim3(kThreads), args, lds, stream) != hipSuccess)
     return 3;
