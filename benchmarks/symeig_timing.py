@@ -47,6 +47,25 @@ def main() -> None:
     s1, s2 = torch.cov(a1.T.double()), torch.cov(a2.T.double())
     mu1, mu2 = a1.double().mean(0), a2.double().mean(0)
     res["fid_compute_d2048_ms_min_med"] = _time(lambda: frechet_distance(mu1, s1, mu2, s2).item())
+    # where the rest of the compute goes: the blocked Cholesky (K9c diagonal blocks + GEMMs),
+    # one K9c diagonal block alone, and the two triangular products
+    from torcheval_amd.metrics.image.fid import cholesky_ex
+
+    res["cholesky_d2048_ms_min_med"] = _time(lambda: cholesky_ex(s1)[1].item())
+    res["rocsolver_cholesky_d2048_ms_min_med"] = _time(lambda: torch.linalg.cholesky_ex(s1)[1].item())
+    blk = s1[:64, :64].contiguous()
+    linv = torch.empty(64 * 64, dtype=torch.float64, device=dev)
+    info = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def _blocks(reps=32):
+        for _ in range(reps):
+            native().potrf_block(blk.clone(), 0, 64, linv, info)
+        torch.cuda.synchronize()
+
+    ms = _time(_blocks)
+    res["k9c_block64_us_min_med"] = [ms[0] * 1e3 / 32, ms[1] * 1e3 / 32]
+    L = cholesky_ex(s1)[0]
+    res["lt_s2_l_d2048_ms_min_med"] = _time(lambda: (L.T @ s2 @ L).sum().item())
     print(json.dumps(res))
 
 

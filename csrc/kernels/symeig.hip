@@ -530,8 +530,8 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
 // covariance (metrics/image/fid.py).  rocSOLVER's potrf at D = 2048 spent ~2.7 ms in 17
 // potf2 launches (~160 us each) and ~1.7 ms in its forward-substitution trsm
 // (profiles/rocprof_k9b_symeig_r2.csv); here one workgroup factors a b x b (b <= 64) diagonal
-// block in LDS (potf2, LAPACK semantics: a non-positive pivot records info = column + 1 and
-// stops) and inverts the factor in LDS, so the panel below becomes one GEMM with the inverse
+// block in registers (potf2, LAPACK semantics: a non-positive pivot records info = column + 1 and
+// stops) and inverts the factor alongside, so the panel below becomes one GEMM with the inverse
 // and the trailing update one GEMM (rocBLAS/hipBLASLt FP64 MFMA) - no trsm, no small-kernel
 // chains.
 namespace tea {
@@ -539,84 +539,97 @@ namespace {
 
 constexpr int kPotrfB = 64;
 
+// Register-resident: thread (ti, tj) of a 16 x 16 grid holds L[ti + 16 x][tj + 16 y] and the
+// same entries of X (x, y < 4) in registers for the whole factorisation, and the column loop is
+// unrolled so the pivot's register slot (j >> 4) is a compile-time index.  Per column ONE
+// barrier: the threads holding column j of L / row j of X put their 4 values into an LDS
+// snapshot (double-buffered, so the next column's writes never race this column's reads), every
+// thread reads the snapshot entries its rows and columns need, and updates its 16 + 16 entries
+// in registers (right-looking potf2 on the lower triangle, the same elimination applied to the
+// identity).  Round 2's form kept L and X in LDS and re-read / re-wrote them every column: ~80
+// LDS operations per thread per column, 76 us per 64 x 64 block.
 __global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda, int k0, int b,
                                                           double* Linv, int* info) {
-  __shared__ double L[kPotrfB][kPotrfB + 1];
-  __shared__ double X[kPotrfB][kPotrfB + 1];
-  __shared__ int s_bad;
+  __shared__ double s_col[2][kPotrfB];  // column j of L (unscaled), per step parity
+  __shared__ double s_xr[2][kPotrfB];   // row j of X (unscaled)
   const int t = threadIdx.x;
-  // 16 x 16 thread grid over the block: thread (ti, tj) owns rows ti + 16 x, columns tj + 16 y
   const int ti = t >> 4, tj = t & 15;
   double* blk = A + (int64_t)k0 * lda + k0;
+  double L[4][4], X[4][4];
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-      const int i = ti + 16 * x, j = tj + 16 * y;
-      if (i < b && j < b) {
-        L[i][j] = j <= i ? blk[(int64_t)i * lda + j] : 0.0;
-        X[i][j] = i == j ? 1.0 : 0.0;
-      }
+      const int i = ti + 16 * x, k = tj + 16 * y;
+      L[x][y] = (i < b && k <= i) ? blk[(int64_t)i * lda + k] : 0.0;
+      X[x][y] = (i == k && i < b) ? 1.0 : 0.0;
     }
-  if (t == 0) s_bad = 0;
-  __syncthreads();
-  // right-looking potf2 on the lower triangle with ONE barrier per column: the update of
-  // step j reads column j of L and row j of X unscaled (scaling folded in as 1/d), and the
-  // scaling of column j / row j is deferred into step j+1's phase, which touches neither
-  // (three barriers per column took 90 -> 76 us per block; see git history)
-  double rp_prev = 0.0, sq_prev = 0.0;
-  for (int j = 0; j < b; ++j) {
-    __syncthreads();  // step j-1's updates (and its deferred scaling) are visible
-    const double d = L[j][j];
-    if (!(d > 0.0)) {  // not positive definite (or NaN): LAPACK info, then stop
-      if (t == 0) {
-        s_bad = 1;
-        if (*info == 0) *info = k0 + j + 1;
-      }
-      break;
-    }
-    const double sq = sqrt(d);
-    const double rp = 1.0 / sq, rd = rp * rp;
-    if (j > 0) {  // deferred: finish column j-1 of L and row j-1 of L^{-1}
-      const int jp = j - 1;
-      if (t < b && t >= jp) L[t][jp] = t == jp ? sq_prev : L[t][jp] * rp_prev;
-      if (t <= jp) X[jp][t] *= rp_prev;
-    }
+  // fully unrolled (no early exit: a break kept the loop rolled, and the pivot slot then went
+  // through dynamic register indexing - 164 us per block); the element updates are selects
+  bool bad = false;
+#pragma clang loop unroll(full)
+  for (int j = 0; j < kPotrfB; ++j) {
+    if (j < b && !bad) {  // block-uniform
+      const int q = j >> 4, c = j & 15, buf = j & 1;
+      if (tj == c) {
 #pragma unroll
-    for (int x = 0; x < 4; ++x) {
-      const int i = ti + 16 * x;
-      if (i > j && i < b) {
-        const double lij = L[i][j] * rd;
+        for (int x = 0; x < 4; ++x) s_col[buf][ti + 16 * x] = L[x][q];
+      }
+      if (ti == c) {
+#pragma unroll
+        for (int y = 0; y < 4; ++y) s_xr[buf][tj + 16 * y] = X[q][y];
+      }
+      __syncthreads();
+      const double d = s_col[buf][j];
+      if (!(d > 0.0)) {  // not positive definite (or NaN): LAPACK info, then stop
+        if (t == 0 && *info == 0) *info = k0 + j + 1;
+        bad = true;
+      } else {
+        const double sq = sqrt(d);
+        const double rs = 1.0 / sq, rd = rs * rs;
+        double ci[4], ck[4], xr[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) ci[x] = s_col[buf][ti + 16 * x] * rd;
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-          const int k = tj + 16 * y;
-          if (k > j && k <= i) L[i][k] -= lij * L[k][j];
-          if (k <= j) X[i][k] -= lij * X[j][k];  // the same elimination applied to I
+          ck[y] = s_col[buf][tj + 16 * y];
+          xr[y] = s_xr[buf][tj + 16 * y];
+        }
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const int i = ti + 16 * x;
+#pragma unroll
+          for (int y = 0; y < 4; ++y) {
+            const int k = tj + 16 * y;
+            const double lu = fma(-ci[x], ck[y], L[x][y]);
+            const double xu = fma(-ci[x], xr[y], X[x][y]);
+            L[x][y] = (i > j && k > j && k <= i) ? lu : L[x][y];
+            X[x][y] = (i > j && k <= j) ? xu : X[x][y];
+          }
+        }
+        // finish column j of L and row j of X (the snapshot the other threads read is unscaled)
+        if (tj == c) {
+#pragma unroll
+          for (int x = 0; x < 4; ++x) {
+            const int i = ti + 16 * x;
+            L[x][q] = i > j ? L[x][q] * rs : (i == j ? sq : L[x][q]);
+          }
+        }
+        if (ti == c) {
+#pragma unroll
+          for (int y = 0; y < 4; ++y) X[q][y] = tj + 16 * y <= j ? X[q][y] * rs : X[q][y];
         }
       }
     }
-    rp_prev = rp;
-    sq_prev = sq;
   }
-  __syncthreads();
-  if (s_bad == 0) {  // the last column / row
-    const int jp = b - 1;
-    if (t == jp) L[jp][jp] = sq_prev;
-    if (t <= jp) X[jp][t] *= rp_prev;
-  }
-  __syncthreads();
-  const bool bad = s_bad != 0;
-  // X now holds L^{-1}: every elimination step of the factorisation was applied to the
-  // identity as well (rank-1 row updates in the same barrier phases; no separate
-  // 64-step substitution, which took ~half of the kernel's 90 us)
 #pragma unroll
   for (int x = 0; x < 4; ++x)
 #pragma unroll
     for (int y = 0; y < 4; ++y) {
-      const int i = ti + 16 * x, j = tj + 16 * y;
-      if (i < b && j < b) {
-        blk[(int64_t)i * lda + j] = j <= i ? L[i][j] : 0.0;
-        Linv[(int64_t)i * b + j] = bad ? 0.0 : X[i][j];
+      const int i = ti + 16 * x, k = tj + 16 * y;
+      if (i < b && k < b) {
+        blk[(int64_t)i * lda + k] = k <= i ? L[x][y] : 0.0;
+        Linv[(int64_t)i * b + k] = bad ? 0.0 : X[x][y];
       }
     }
 }
