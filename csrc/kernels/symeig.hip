@@ -401,14 +401,20 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e2, in
 
 constexpr int kEigMaxN = 2560;
 
-// L lanes per eigenvalue index i (ascending): L-point multisection of [lo, hi] keeping
-// count(a) <= i < count(b).
-template <int L>
-__global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double* __restrict__ d_in,
-                                                                   const double* __restrict__ e_in,
-                                                                   int n, double* lam) {
-  __shared__ double d[kEigMaxN], e2[kEigMaxN];
-  __shared__ double red[3][kWaves];
+// Sturm-count grid: kGrid points evenly spaced inside the Gershgorin interval, one count per
+// lane in one launch (1024 waves, about the time of one multisection round).  Every eigenvalue
+// then starts from the grid cell that holds it (a binary search of the counts) instead of the
+// whole interval: log16(65536) = 4 of the ~13 sixteen-point rounds, for one round's time.
+constexpr int kGrid = 65536;
+
+struct Bounds {
+  double a, b, pivmin, span;
+};
+
+// d, e^2 into LDS and the widened Gershgorin interval (block-cooperative; every kernel that
+// calls it computes bitwise the same bounds, so grid points match across launches)
+__device__ Bounds tridiag_setup(const double* __restrict__ d_in, const double* __restrict__ e_in, int n,
+                                double* d, double* e2, double (*red)[kWaves]) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   double lo = DBL_MAX, hi = -DBL_MAX, emax = 0.0;
   for (int k = t; k < n; k += kThreads) {
@@ -441,11 +447,41 @@ __global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double*
     hi = fmax(hi, red[1][w]);
     emax = fmax(emax, red[2][w]);
   }
-  const double pivmin = DBL_MIN * fmax(1.0, emax);
-  const double span = fmax(fabs(lo), fabs(hi));
-  // widen so count(lo) = 0 and count(hi) = n hold despite rounding
-  double a = lo - 2.0 * DBL_EPSILON * span * n - 2.0 * pivmin;
-  double b = hi + 2.0 * DBL_EPSILON * span * n + 2.0 * pivmin;
+  Bounds r;
+  r.pivmin = DBL_MIN * fmax(1.0, emax);
+  r.span = fmax(fabs(lo), fabs(hi));
+  // widen so count(a) = 0 and count(b) = n hold despite rounding
+  r.a = lo - 2.0 * DBL_EPSILON * r.span * n - 2.0 * r.pivmin;
+  r.b = hi + 2.0 * DBL_EPSILON * r.span * n + 2.0 * r.pivmin;
+  return r;
+}
+
+__device__ __forceinline__ double grid_x(const Bounds& q, int g) {
+  return q.a + (q.b - q.a) * (double)(g + 1) / (double)(kGrid + 1);
+}
+
+__global__ __launch_bounds__(kThreads) void sturm_grid_kernel(const double* __restrict__ d_in,
+                                                              const double* __restrict__ e_in, int n,
+                                                              int* counts) {
+  __shared__ double d[kEigMaxN], e2[kEigMaxN];
+  __shared__ double red[3][kWaves];
+  const Bounds q = tridiag_setup(d_in, e_in, n, d, e2, red);
+  const int g = blockIdx.x * kThreads + threadIdx.x;
+  if (g < kGrid) counts[g] = sturm_count(d, e2, n, grid_x(q, g), q.pivmin);
+}
+
+// L lanes per eigenvalue index i (ascending): L-point multisection of the eigenvalue's grid cell
+// keeping count(a) <= i < count(b).
+template <int L>
+__global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double* __restrict__ d_in,
+                                                                   const double* __restrict__ e_in,
+                                                                   int n, const int* __restrict__ counts,
+                                                                   double* lam) {
+  __shared__ double d[kEigMaxN], e2[kEigMaxN];
+  __shared__ double red[3][kWaves];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const Bounds q = tridiag_setup(d_in, e_in, n, d, e2, red);
+  const double pivmin = q.pivmin, span = q.span;
   // L lanes per eigenvalue, 64 / L eigenvalues per wave.  L = 16 (D >= 1536): 16-point
   // sections need ~13 rounds instead of ~9 for 64 points, but 2.8x less Sturm work in all
   // (1.63 vs 1.86 ms at D = 2048); smaller D keeps L = 64 for occupancy (0.29 vs 0.39 ms at 512).
@@ -454,6 +490,15 @@ __global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double*
   const int idx = (blockIdx.x * kWaves + wave) * kPer + grp;
   if ((blockIdx.x * kWaves + wave) * kPer >= n) return;  // whole wave idle; no barrier below
   bool done = idx >= n;
+  // the grid cell: g* = first grid index whose count exceeds idx (count at the top end = n)
+  int glo = 0, ghi = kGrid;
+  while (glo < ghi) {
+    const int mid = (glo + ghi) >> 1;
+    if (counts[mid] > idx) ghi = mid;
+    else glo = mid + 1;
+  }
+  double a = glo == 0 ? q.a : grid_x(q, glo - 1);
+  double b = glo == kGrid ? q.b : grid_x(q, glo);
   for (int round = 0; round < 20; ++round) {
     const double width = b - a;
     // absolute tolerance eps * ||T|| (the accuracy any backward-stable solver delivers)
@@ -491,6 +536,8 @@ int symeig_plan(int64_t n, int* grid, int* rows_per_block) {
 
 int64_t symeig_slot_stride(int64_t n) { return (n + 15) / 16 * 16; }
 
+int64_t symeig_grid_bytes() { return (int64_t)kGrid * sizeof(int); }
+
 int64_t symeig_slot_bytes(int64_t n) { return 2 * (n - 2) * symeig_slot_stride(n) * (int64_t)sizeof(unsigned long long); }
 
 int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
@@ -516,10 +563,11 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   if (hipLaunchCooperativeKernel(kern, dim3(G),
                                  dim3(kThreads), args, lds, stream) != hipSuccess)
     return 3;
+  sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
   if (n >= 1536)
-    tridiag_eigvals_kernel<16><<<(n + kWaves * 4 - 1) / (kWaves * 4), kThreads, 0, stream>>>(d, e, n, a.lam);
+    tridiag_eigvals_kernel<16><<<(n + kWaves * 4 - 1) / (kWaves * 4), kThreads, 0, stream>>>(d, e, n, a.grid, a.lam);
   else
-    tridiag_eigvals_kernel<64><<<(n + kWaves - 1) / kWaves, kThreads, 0, stream>>>(d, e, n, a.lam);
+    tridiag_eigvals_kernel<64><<<(n + kWaves - 1) / kWaves, kThreads, 0, stream>>>(d, e, n, a.grid, a.lam);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
