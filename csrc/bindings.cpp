@@ -360,12 +360,16 @@ static tea::AucScanArgs scan_args(const Tensor& sorted, const Tensor& order, con
   else a.order32 = order.data_ptr<int32_t>();
   a.order_stride = order.stride(0);
   tg = target;
+  // with a payload (kinds 1, 2) the sort carried the targets / labels and no kernel reads
+  // `target` (tea_scan.h sample_ab): no layout copy for it (a transposed [n, L] multilabel
+  // target used to cost one strided ATen transpose per launch here)
+  const bool read_target = payload_kind == 0;
   if (class_mode) {
     TORCH_CHECK(tg.dim() == 1 && tg.size(0) == n, who, ": class-mode target must be [n]");
-    tg = tg.contiguous();
+    if (read_target) tg = tg.contiguous();
   } else {
     TORCH_CHECK(tg.dim() == 2 && tg.size(0) == rows && tg.size(1) == n, who, ": target must be [rows, n]");
-    if (tg.stride(1) != 1) tg = tg.contiguous();
+    if (read_target && tg.stride(1) != 1) tg = tg.contiguous();
     a.target_stride = tg.stride(0);
   }
   a.target = tg.data_ptr();

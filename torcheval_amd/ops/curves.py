@@ -72,7 +72,7 @@ def multiclass_pr_curves(input: torch.Tensor, target: torch.Tensor) -> Curves:
 
 def multilabel_pr_curves(input: torch.Tensor, target: torch.Tensor) -> Curves:
     """Per-label PR curves of [n, L] scores vs [n, L] {0, 1} targets (positives: target == 1)."""
-    pos = (target == 1).to(torch.uint8).t()
+    pos = (target == 1).t()  # [L, n] view; _sort_rows lays it out once (fast transpose)
     return _curves(_rows_major(input), pos, PAYLOAD_TARGET, False, input.dtype)
 
 
@@ -97,6 +97,6 @@ def binary_rafp(input: torch.Tensor, target: torch.Tensor, min_precision: float)
 
 def multilabel_rafp(input: torch.Tensor, target: torch.Tensor, min_precision: float) -> Tuple[torch.Tensor, torch.Tensor]:
     """Per-label (max recall [L], |best threshold| [L]) of [n, L] data, sync-free."""
-    pos = (target == 1).to(torch.uint8).t()
+    pos = (target == 1).t()  # [L, n] view; _sort_rows lays it out once (fast transpose)
     return _rafp(_rows_major(input), pos, PAYLOAD_TARGET, False, min_precision,
                  torch.promote_types(input.dtype, torch.float32))

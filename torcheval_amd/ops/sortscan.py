@@ -17,6 +17,18 @@ PAYLOAD_TARGET, PAYLOAD_LABEL = 1, 2
 _TARGET_PAYLOAD = (torch.float32, torch.int64, torch.int32, torch.uint8, torch.bool)
 
 
+def _rows_f32(v: torch.Tensor) -> torch.Tensor:
+    """A [rows, n] operand with unit stride along samples, as float32 values.  The transposed
+    view of a row-major [n, rows] tensor (multilabel scores / targets) goes through the LDS-tiled
+    ``transpose_f32`` (ATen's strided copy of such a view is ~10x slower)."""
+    if v.dim() == 2 and v.stride(-1) != 1 and v.stride(0) == 1 and v.t().is_contiguous() and v.numel() > 0:
+        src = v.t() if v.dtype == torch.float32 else v.t().float()
+        out = torch.empty(v.shape, dtype=torch.float32, device=v.device)
+        native().transpose_f32(src, out)
+        return out
+    return v if v.dtype == torch.float32 and v.stride(-1) == 1 else v.float().contiguous()
+
+
 def _sort_rows(
     x: torch.Tensor, payload: Optional[torch.Tensor] = None, payload_kind: int = 0
 ) -> Tuple[torch.Tensor, torch.Tensor, int]:
@@ -31,12 +43,14 @@ def _sort_rows(
         x = x.float()  # f16/bf16 -> f32 is exact and order preserving
     if x.dtype == torch.float32 and x.shape[-1] < 2**31:
         if x.stride(-1) != 1:
-            x = x.contiguous()
+            x = _rows_f32(x)
         s = torch.empty(x.shape, dtype=torch.float32, device=x.device)
         idx = torch.empty(x.shape, dtype=torch.int32, device=x.device)
         kind = payload_kind if payload is not None else 0
-        if kind == PAYLOAD_TARGET and payload.dtype not in _TARGET_PAYLOAD:
-            payload = payload.float()
+        if kind == PAYLOAD_TARGET and (payload.dtype not in _TARGET_PAYLOAD or
+                                       (payload.dim() == 2 and payload.stride(-1) != 1)):
+            # K3a converts a target payload to its f32 value anyway
+            payload = _rows_f32(payload)
         elif kind == PAYLOAD_LABEL and payload.dtype not in (torch.int64, torch.int32):
             payload = payload.long()
         native().sort_desc(x, s, idx, payload, kind)
