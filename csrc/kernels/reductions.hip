@@ -161,6 +161,33 @@ __global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
     for (int e = 0; e < V; ++e) lds[k * V + e][threadIdx.x] = acc[k][e];
   lds_w[threadIdx.x] = (cg == 0 && active) ? wsum : 0.0;  // one column group counts weights
   __syncthreads();
+  if (a.mse_mode == 2) {
+    // functional MSE, uniform average: with per-row weights every column divides by the same
+    // weight total, so mean_j(sse_j / sw) = (sum_j sse_j) / (d sw) and the block only hands
+    // on {its sse summed over its columns, its weight total} - no per-column partials, no
+    // per-column finalize (mse_scalar_kernel folds these pairs)
+    double tot = 0.0;
+    if (threadIdx.x < CG) {  // CG <= 64: wave 0
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        double s = 0.0;
+        for (int r = 0; r < RPP; ++r) s += lds[e][r * CG + threadIdx.x];
+        tot += (c0 + threadIdx.x) * V + e < d ? s : 0.0;
+      }
+    }
+    if (threadIdx.x < 64) {
+      tot = wave_sum(tot);
+      if (threadIdx.x == 0) {
+        double sw = 0.0;
+        if (blockIdx.y == 0)
+          for (int r = 0; r < kB; ++r) sw += lds_w[r];
+        double* pair = a.ws + 2 * (static_cast<int64_t>(blockIdx.x) * gridDim.y + blockIdx.y);
+        pair[0] = tot;
+        pair[1] = sw;
+      }
+    }
+    return;
+  }
   if (threadIdx.x < CG) {
 #pragma unroll
     for (int k = 0; k < kStats; ++k) {
@@ -190,6 +217,38 @@ __global__ __launch_bounds__(kB) void moments_partial_kernel(MomentsArgs a) {
 // last-block-done fold would need an agent-scope release fence per block, which
 // tea_fold.h measured at +47 us for a 2048-block grid).
 constexpr int kFG = 64, kFC = kB / kFG;  // 4 columns x 64 partial groups: 250 blocks at d = 1000 (32 x 8: 125)
+
+// functional MSE (uniform average): fold the partial kernel's {sse, weight} pairs in a fixed
+// order, then the reference's float32 sse / (clamp(|sw|, eps) sign(sw)) averaged over columns
+// (mean_squared_error.py:100-111), as one quotient
+__global__ __launch_bounds__(kB) void mse_scalar_kernel(const double* pairs, int64_t npairs, int64_t d,
+                                                        float* out) {
+  __shared__ double lds[2][kB / 64];
+  double s = 0.0, w = 0.0;
+  for (int64_t p = threadIdx.x; p < npairs; p += kB) {
+    s += pairs[2 * p];
+    w += pairs[2 * p + 1];
+  }
+  s = wave_sum(s);
+  w = wave_sum(w);
+  if (lane_id() == 0) {
+    lds[0][threadIdx.x >> 6] = s;
+    lds[1][threadIdx.x >> 6] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double st = 0.0, wt = 0.0;
+    for (int q = 0; q < kB / 64; ++q) {
+      st += lds[0][q];
+      wt += lds[1][q];
+    }
+    const float sw = static_cast<float>(wt);
+    const float eps = 2.220446049250313e-16f;
+    const float sgn = sw > 0.f ? 1.f : (sw < 0.f ? -1.f : 0.f);
+    const double den = static_cast<double>(fmaxf(fabsf(sw), eps) * sgn) * static_cast<double>(d);
+    *out = static_cast<float>(st / den);
+  }
+}
 
 // final scalar of the fused functional computes, in a fixed order (per-thread strided sums +
 // LDS tree): MSE / R2 uniform mean (modes 2, 4), R2 variance-weighted sum (mode 5); then the
@@ -402,6 +461,11 @@ int launch_column_moments(const MomentsArgs& a, hipStream_t stream) {
     hipLaunchKernelGGL(moments_partial_kernel<4>, dim3(P, ct), dim3(kB), 0, stream, a);
   else
     hipLaunchKernelGGL(moments_partial_kernel<1>, dim3(P, ct), dim3(kB), 0, stream, a);
+  if (a.mse_mode == 2) {  // the scalar MSE needs no per-column statistics (sse / sw left unwritten)
+    hipLaunchKernelGGL(mse_scalar_kernel, dim3(1), dim3(kB), 0, stream, a.ws, static_cast<int64_t>(P) * ct, a.d,
+                       a.mse_out);
+    return static_cast<int>(hipGetLastError());
+  }
   const unsigned fb = static_cast<unsigned>(column_moments_finalize_blocks(a.d));
   const bool scalar = a.mse_mode == 2 || a.mse_mode == 4 || a.mse_mode == 5;
   if (a.mse_mode && (!a.overwrite || !a.sse || (scalar && !a.mse_part_f))) return -2;

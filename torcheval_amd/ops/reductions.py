@@ -40,8 +40,9 @@ def column_moments(
 def mse_fused(
     x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor], raw_values: bool
 ) -> torch.Tensor:
-    """Functional mean_squared_error in two launches (+1 for the column mean): K5 partials,
-    then a finalize that also divides by the clamped signed weight total."""
+    """Functional mean_squared_error in two launches: K5 partials, then a finalize that also
+    divides by the clamped signed weight total (raw values: per column; uniform average: one
+    single-block fold of per-block {sse, weight} pairs, sum_j sse_j / (d sw))."""
     d = x.shape[1] if x.dim() == 2 else 1
     x2 = x[:, None] if x.dim() == 1 else x
     t2 = t[:, None] if t.dim() == 1 else t
