@@ -7,16 +7,16 @@
 // launches of ~5 us (latrd gemv / dot / update kernels, one group per column of the
 // Householder reduction) plus the tridiagonal solver: the chip idles between tiny launches.
 //
-// MI355X design: the whole D x D FP64 matrix lives in LDS across the chip for the whole
-// reduction (2048 x 2048 x 8 B = 32 MiB = 256 CUs x 128 KB of their 160 KB), one cooperative
-// launch of one workgroup per CU.  Workgroup g owns R consecutive rows; the matrix never goes
+// MI355X design: the whole D x D FP64 matrix lives on chip for the whole reduction, in the
+// vector registers of one workgroup per CU (2048 x 2048 x 8 B = 32 MiB = 256 CUs x 128 KB;
+// each thread holds 8 rows x 8 columns), one cooperative launch.  Workgroup g owns R consecutive rows; the matrix never goes
 // back to HBM.  Householder tridiagonalisation (unblocked, LAPACK sytd2 semantics) with ONE
 // grid-wide hand-off per column:
 //   phase j publishes p_j = tau_j A v_j for the owned rows (8 B each) and, from the owner of
 //   row j+1, that row as updated through step j-1; after the barrier every workgroup holds
 //   the full p_j and row j+1, forms w_j = p_j - (tau_j/2)(p_j . v_j) v_j, applies step j to
 //   row j+1 itself (so row j+1 is never re-published), derives the next reflector v_{j+1}
-//   redundantly, and then ONE LDS pass over its rows both applies A -= v_j w_j^T + w_j v_j^T
+//   redundantly, and then ONE register pass over its rows both applies A -= v_j w_j^T + w_j v_j^T
 //   and accumulates the next p_{j+1} = tau_{j+1} A v_{j+1}.
 // Hand-offs: every handed-off double has its own 8-byte slot, used by exactly one phase of the
 // launch; the launcher fills the slot planes with all-one bytes (a NaN pattern no stored value
@@ -47,7 +47,7 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kWaves = kThreads / 64;
 constexpr int kMaxCols = 10;   // columns per thread: n <= 2560
-constexpr int kMaxRows = 10;   // rows per workgroup (LDS: R * n * 8 <= 160 KB)
+constexpr int kMaxRows = 10;   // rows per workgroup (registers: R x C doubles per thread)
 constexpr unsigned kSpinLimit = 1u << 18;
 constexpr size_t kCtlBytes = 128;  // ctl[1] = abort word
 
@@ -192,7 +192,22 @@ __device__ __forceinline__ void make_v(const double (&a)[C], const Reflector& h,
   }
 }
 
-// One workgroup per CU; dynamic LDS = R * n doubles (the owned rows).  Slot planes of
+// element s of owned row r for a run-time r (the publishing owner only): a select chain over the
+// register-resident rows
+template <int C, int RM>
+__device__ __forceinline__ double row_elem(const double (&rw)[RM][C], int r, int s_) {
+  double x = 0.0;
+#pragma unroll
+  for (int q = 0; q < RM; ++q) {
+#pragma unroll
+    for (int s = 0; s < C; ++s) x = (q == r && s == s_) ? rw[q][s] : x;
+  }
+  return x;
+}
+
+// One workgroup per CU; each thread holds its columns (t + 256 s) of the workgroup's R owned
+// rows in registers for the whole reduction (round 2 kept them in LDS: the per-column pass was
+// LDS-bandwidth bound, ~16 B of LDS traffic per element per column).  Slot planes of
 // [n - 2, ld] each at slots + {0, 1} * plane: p_q, then row q+1 (as updated through step q-1);
 // all sentinel-filled by the launcher.  ctl[1] = abort word, zeroed by the launcher.
 template <int C, int RM>
@@ -200,7 +215,6 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
                                                            int R, int64_t ld, double* d_out,
                                                            double* e_out, unsigned long long* slots,
                                                            unsigned* ctl) {
-  extern __shared__ double rows[];
   __shared__ double red[3][16 * RM];
   __shared__ double bc[2][4];  // single-element broadcasts riding on the reductions' barriers
   __shared__ double vw[2][RM];
@@ -211,7 +225,14 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
   const int t = threadIdx.x;
   const int row0 = blockIdx.x * R;
   const int nrows = min(R, n - row0);
-  for (int idx = t; idx < nrows * n; idx += kThreads) rows[idx] = A[(int64_t)row0 * n + idx];
+  double rw[RM][C];  // owned row r, column t + s * kThreads
+#pragma unroll
+  for (int r = 0; r < RM; ++r)
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int k = t + s * kThreads;
+      rw[r][s] = (r < nrows && k < n) ? A[(int64_t)(row0 + r) * n + k] : 0.0;
+    }
 
   double a[C], v[C], w[C], vn[C];
 #pragma unroll
@@ -237,7 +258,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
 #pragma unroll
         for (int s = 0; s < C; ++s) {
           const int k = t + s * kThreads;
-          if (k < n) acc[r] += rows[r * n + k] * v[s];
+          if (k < n) acc[r] += rw[r][s] * v[s];
         }
       }
     }
@@ -247,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
 #pragma unroll
       for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
-        if (k >= 1 && k < n) put(gr0, k, rows[(1 - row0) * n + k]);
+        if (k >= 1 && k < n) put(gr0, k, row_elem<C, RM>(rw, 1 - row0, s));
       }
     }
   }
@@ -329,7 +350,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
 #pragma unroll
         for (int s = 0; s < C; ++s) {
           const int k = t + s * kThreads;
-          if (k == n - 1) d_out[n - 1] = rows[r * n + k] - 2.0 * vw[0][r] * vw[1][r];
+          if (k == n - 1) d_out[n - 1] = row_elem<C, RM>(rw, r, s) - 2.0 * vw[0][r] * vw[1][r];
         }
       }
       break;
@@ -344,33 +365,31 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       e_out[j + 1] = hn.beta;
     }
 
-    // ---- one LDS pass: apply step j to the owned rows, accumulate p_{j+1}
+    // ---- one register pass: apply step j to the owned rows, accumulate p_{j+1}.  No column
+    // test: below column j+1 (and past n) w_j, v_j and v_{j+1} are zero, so those entries are
+    // left as they are and add nothing
     double acc[RM];
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
       acc[r] = 0.0;
-      if (r < nrows && row0 + r >= j + 1) {
+      if (r < nrows && row0 + r >= j + 1) {  // block-uniform
         const double vi = vw[0][r], wi = vw[1][r];
 #pragma unroll
         for (int s = 0; s < C; ++s) {
-          const int k = t + s * kThreads;
-          if (k >= j + 1 && k < n) {
-            const double x = rows[r * n + k] - (vi * w[s] + wi * v[s]);
-            rows[r * n + k] = x;
-            acc[r] += x * vn[s];
-          }
+          const double x = rw[r][s] - (vi * w[s] + wi * v[s]);
+          rw[r][s] = x;
+          acc[r] += x * vn[s];
         }
       }
     }
-    // the owner of row j+2 publishes the row before the p reduction (each thread re-reads
-    // only the LDS words it wrote itself)
+    // the owner of row j+2 publishes the row before the p reduction
     SYM_TRACE(j, 3);
     const int ro = (j + 2) - row0;
     if (ro >= 0 && ro < nrows) {
 #pragma unroll
       for (int s = 0; s < C; ++s) {
         const int k = t + s * kThreads;
-        if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, k, rows[ro * n + k]);
+        if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, k, row_elem<C, RM>(rw, ro, s));
       }
     }
     const double pt = block_sum_own<RM>(acc, red[2]);
@@ -528,7 +547,7 @@ int symeig_plan(int64_t n, int* grid, int* rows_per_block) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 2;
   int64_t R = (n + cus - 1) / cus;
   if (R > kMaxRows) return 1;
-  if (R * n * (int64_t)sizeof(double) > 152 * 1024) return 1;
+  if (R * n * (int64_t)sizeof(double) > 160 * 1024) return 1;  // <= 10 x 10 doubles per thread
   *grid = (int)((n + R - 1) / R);
   *rows_per_block = (int)R;
   return 0;
@@ -543,14 +562,15 @@ int64_t symeig_slot_bytes(int64_t n) { return 2 * (n - 2) * symeig_slot_stride(n
 int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   int G = 0, R = 0;
   if (symeig_plan(a.n, &G, &R) != 0) return 1;
-  const size_t lds = (size_t)R * a.n * sizeof(double);
-  // n <= 2048 with <= 8 rows per block (the FID case) gets the 8 x 8 instance: no dead column
-  // slots or reduction lanes
-  const void* kern = (a.n <= 8 * kThreads && R <= 8)
-                         ? reinterpret_cast<const void*>(&tridiag_kernel<8, 8>)
-                         : reinterpret_cast<const void*>(&tridiag_kernel<kMaxCols, kMaxRows>);
-  if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-    return 2;
+  // the smallest instance holding ceil(n / 256) columns and R rows per thread: every register
+  // slot is live (the pass has no per-element column test), e.g. 8 x 8 for the FID's D = 2048
+  const int need = (int)max((a.n + kThreads - 1) / kThreads, (int64_t)R);
+  const void* kern = need <= 2   ? reinterpret_cast<const void*>(&tridiag_kernel<2, 2>)
+                     : need <= 4 ? reinterpret_cast<const void*>(&tridiag_kernel<4, 4>)
+                     : need <= 6 ? reinterpret_cast<const void*>(&tridiag_kernel<6, 6>)
+                     : need <= 8 ? reinterpret_cast<const void*>(&tridiag_kernel<8, 8>)
+                     : need <= 9 ? reinterpret_cast<const void*>(&tridiag_kernel<9, 9>)
+                                 : reinterpret_cast<const void*>(&tridiag_kernel<kMaxCols, kMaxRows>);
   if (hipMemsetAsync(a.ctl, 0, kCtlBytes, stream) != hipSuccess) return 2;
   if (hipMemsetAsync(a.slots, 0xff, (size_t)symeig_slot_bytes(a.n), stream) != hipSuccess) return 2;
   const double* A = a.a;
@@ -560,8 +580,7 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   unsigned long long* slots = a.slots;
   unsigned* ctl = a.ctl;
   void* args[] = {&A, &n, &R, &ld, &d, &e, &slots, &ctl};
-  if (hipLaunchCooperativeKernel(kern, dim3(G),
-                                 dim3(kThreads), args, lds, stream) != hipSuccess)
+  if (hipLaunchCooperativeKernel(kern, dim3(G), dim3(kThreads), args, 0, stream) != hipSuccess)
     return 3;
   sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
   if (n >= 1536)
