@@ -367,7 +367,8 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
 
     // ---- one register pass: apply step j to the owned rows, accumulate p_{j+1}.  No column
     // test: below column j+1 (and past n) w_j, v_j and v_{j+1} are zero, so those entries are
-    // left as they are and add nothing
+    // left as they are and add nothing.  (Deferring the update past the p hand-off, with p
+    // corrected for it as LAPACK latrd does, measured no faster: 14.74 vs 14.69 ms at D = 2048.)
     double acc[RM];
 #pragma unroll
     for (int r = 0; r < RM; ++r) {
@@ -432,6 +433,12 @@ struct Bounds {
 
 // d, e^2 into LDS and the widened Gershgorin interval (block-cooperative; every kernel that
 // calls it computes bitwise the same bounds, so grid points match across launches)
+// min / max that propagate NaN (fmin / fmax drop it): a NaN anywhere in the tridiagonal makes
+// the interval NaN, so every eigenvalue comes out NaN (torch's eigvalsh of a NaN matrix does
+// not return finite numbers either) instead of a bisection over garbage counts
+__device__ __forceinline__ double nan_min(double a, double b) { return (a != a || b != b) ? a + b : fmin(a, b); }
+__device__ __forceinline__ double nan_max(double a, double b) { return (a != a || b != b) ? a + b : fmax(a, b); }
+
 __device__ Bounds tridiag_setup(const double* __restrict__ d_in, const double* __restrict__ e_in, int n,
                                 double* d, double* e2, double (*red)[kWaves]) {
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -442,14 +449,14 @@ __device__ Bounds tridiag_setup(const double* __restrict__ d_in, const double* _
     const double ep = k > 0 ? fabs(e_in[k - 1]) : 0.0;
     d[k] = dk;
     e2[k] = ek * ek;
-    lo = fmin(lo, dk - ek - ep);
-    hi = fmax(hi, dk + ek + ep);
+    lo = nan_min(lo, dk - ek - ep);
+    hi = nan_max(hi, dk + ek + ep);
     emax = fmax(emax, ek * ek);
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, o, 64));
-    hi = fmax(hi, __shfl_xor(hi, o, 64));
+    lo = nan_min(lo, __shfl_xor(lo, o, 64));
+    hi = nan_max(hi, __shfl_xor(hi, o, 64));
     emax = fmax(emax, __shfl_xor(emax, o, 64));
   }
   if (lane == 0) {
@@ -462,8 +469,8 @@ __device__ Bounds tridiag_setup(const double* __restrict__ d_in, const double* _
   hi = red[1][0];
   emax = red[2][0];
   for (int w = 1; w < kWaves; ++w) {
-    lo = fmin(lo, red[0][w]);
-    hi = fmax(hi, red[1][w]);
+    lo = nan_min(lo, red[0][w]);
+    hi = nan_max(hi, red[1][w]);
     emax = fmax(emax, red[2][w]);
   }
   Bounds r;
@@ -547,7 +554,6 @@ int symeig_plan(int64_t n, int* grid, int* rows_per_block) {
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 2;
   int64_t R = (n + cus - 1) / cus;
   if (R > kMaxRows) return 1;
-  if (R * n * (int64_t)sizeof(double) > 160 * 1024) return 1;  // <= 10 x 10 doubles per thread
   *grid = (int)((n + R - 1) / R);
   *rows_per_block = (int)R;
   return 0;

@@ -124,3 +124,27 @@ def test_blocked_cholesky_reports_non_pd(n, bad):
     _, ref_info = torch.linalg.cholesky_ex(m)
     assert int(info) != 0 and int(ref_info) != 0
     assert int(info) <= bad + 1
+
+
+@pytest.mark.parametrize("n", [2049, 2304, 2560])
+def test_largest_instances(n):
+    # the 9 x 9 and 10 x 10 register instances (n > 2048): more rows and columns per thread
+    m = _spd(n, n)
+    ref = torch.linalg.eigvalsh(m)
+    got = _native_eig(m.to(DEV))
+    torch.testing.assert_close(got, ref, rtol=0, atol=float(1e-12 * n * ref.abs().max()))
+
+
+@pytest.mark.parametrize("payload", ["default", "all_ones"])
+def test_nan_entries_do_not_stall_the_hand_off(payload):
+    # a NaN is canonicalised before it is handed off, so no stored value can equal the
+    # all-one-bytes sentinel of an unpublished slot - not even a NaN input that carries
+    # exactly that bit pattern; the launch completes (status 0) and the eigenvalues are NaN
+    m = _spd(300, 3)
+    bad = torch.tensor([-1], dtype=torch.int64).view(torch.float64)[0] if payload == "all_ones" else float("nan")
+    m[10, 20] = m[20, 10] = bad
+    lam = torch.empty(300, dtype=torch.float64, device=DEV)
+    status = torch.zeros(1, dtype=torch.int32, device=DEV)
+    assert native().sym_eigvals(m.to(DEV), lam, status) == 0
+    assert int(status.item()) == 0
+    assert torch.isnan(lam.cpu()).all()
