@@ -324,6 +324,39 @@ __global__ __launch_bounds__(kRT) void transpose_kernel(const float* in, int64_t
   }
 }
 
+// The same transpose with 16-B accesses both ways (in 16-B aligned with ld_in % 4 == 0, out
+// with n % 4 == 0): a thread loads 4 consecutive columns of a row and stores 4 consecutive
+// samples of an output row (4 strided LDS reads).  One 4-byte access per element made the
+// [100k, 100] case 28 us (~2.8 TB/s; profiles/rocprof_multiclass_auroc_100k_x100_kernel_stats_r3.csv).
+__global__ __launch_bounds__(kRT) void transpose4_kernel(const float* in, int64_t n, int64_t c, int64_t ld_in,
+                                                         float* out) {
+  __shared__ float t[64][65];
+  const int64_t i0 = static_cast<int64_t>(blockIdx.x) * 64, c0 = static_cast<int64_t>(blockIdx.y) * 64;
+  const int q = threadIdx.x & 15, ty = threadIdx.x >> 4;  // 16 threads x 4 values per 64-wide row
+  float4 v[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {  // every load issued before any LDS store
+    const int64_t i = i0 + ty + 16 * p, cc = c0 + 4 * q;
+    v[p] = (i < n && cc < c) ? *reinterpret_cast<const float4*>(in + i * ld_in + cc) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = ty + 16 * p;
+    t[r][4 * q] = v[p].x;
+    t[r][4 * q + 1] = v[p].y;
+    t[r][4 * q + 2] = v[p].z;
+    t[r][4 * q + 3] = v[p].w;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int r = ty + 16 * p;  // output row c0 + r, samples i0 + 4q .. 4q + 3
+    const int64_t cc = c0 + r, i = i0 + 4 * q;
+    if (cc < c && i < n)
+      *reinterpret_cast<float4*>(out + cc * n + i) = make_float4(t[4 * q][r], t[4 * q + 1][r], t[4 * q + 2][r], t[4 * q + 3][r]);
+  }
+}
+
 }  // namespace
 
 int radix_sort_rounds(int64_t rows, int64_t n) { return rows * n >= kBigSort ? 16 : 8; }
@@ -338,7 +371,11 @@ int64_t radix_sort_groups(int64_t tiles) { return (tiles + kGroup - 1) / kGroup;
 int launch_transpose_f32(const float* in, int64_t n, int64_t c, int64_t ld_in, float* out, hipStream_t stream) {
   if (n <= 0 || c <= 0) return 0;
   const dim3 grid(static_cast<unsigned>((n + 63) / 64), static_cast<unsigned>((c + 63) / 64));
-  hipLaunchKernelGGL(transpose_kernel, grid, dim3(kRT), 0, stream, in, n, c, ld_in, out);
+  // 16-B path: c and n multiples of 4 (whole float4s never straddle the edge), aligned rows
+  const bool v4 = c % 4 == 0 && n % 4 == 0 && ld_in % 4 == 0 && reinterpret_cast<uintptr_t>(in) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(out) % 16 == 0;
+  if (v4) hipLaunchKernelGGL(transpose4_kernel, grid, dim3(kRT), 0, stream, in, n, c, ld_in, out);
+  else hipLaunchKernelGGL(transpose_kernel, grid, dim3(kRT), 0, stream, in, n, c, ld_in, out);
   return static_cast<int>(hipGetLastError());
 }
 

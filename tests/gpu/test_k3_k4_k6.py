@@ -282,11 +282,13 @@ def test_k3a_strided_rows():
     torch.testing.assert_close(s, torch.sort(x, dim=-1, descending=True).values, rtol=0, atol=0)
 
 
-@pytest.mark.parametrize("n,c", [(1, 1), (63, 65), (100_000, 100), (4097, 3)])
-def test_tiled_transpose(n, c):
+@pytest.mark.parametrize("n,c", [(1, 1), (63, 65), (100_000, 100), (4097, 3), (4100, 68), (8, 4), (132, 256)])
+@pytest.mark.parametrize("strided", [False, True])
+def test_tiled_transpose(n, c, strided):
+    # (n, c multiples of 4 with aligned rows take the 16-B kernel, ragged tiles included)
     from torcheval_amd.ops import native
 
-    x = torch.randn(n, c, device=DEV)
+    x = torch.randn(n, c + 8, device=DEV)[:, :c] if strided else torch.randn(n, c, device=DEV)
     out = torch.empty(c, n, device=DEV)
     native().transpose_f32(x, out)
     assert torch.equal(out, x.t().contiguous())
