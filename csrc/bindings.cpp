@@ -964,7 +964,7 @@ void fid_cov_update(const Tensor& act_in, const Tensor& cov, const optional<Tens
 
 
 // ---------------------------------------------------------------- K9b symmetric eigenvalues
-// Eigenvalues (ascending) of a symmetric FP64 [n, n] matrix by the LDS-resident one-launch
+// Eigenvalues (ascending) of a symmetric FP64 [n, n] matrix by the on-chip (register-resident) one-launch
 // Householder reduction + multisection (csrc/kernels/symeig.hip).  Returns 0 when launched
 // (then status[0] != 0 after the stream reaches it means the grid aborted and lam is
 // invalid), non-zero when this device / size is not handled (nothing launched).
@@ -1342,7 +1342,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("potrf_block", &potrf_block, "K9c diagonal-block FP64 Cholesky + inverse (blocked Cholesky step)",
         py::arg("a"), py::arg("k0"), py::arg("b"), py::arg("linv"), py::arg("info"));
   m.def("potrf_block_size", &tea::potrf_block_size, "K9c block size");
-  m.def("sym_eigvals", &sym_eigvals, "K9b eigenvalues of a symmetric float64 matrix (LDS-resident Householder + multisection)",
+  m.def("sym_eigvals", &sym_eigvals, "K9b eigenvalues of a symmetric float64 matrix (on-chip Householder + multisection)",
         py::arg("m"), py::arg("lam"), py::arg("status"));
   tea_register_runtime(m);
   tea_register_cpu_metrics(m);

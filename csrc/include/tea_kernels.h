@@ -446,7 +446,7 @@ struct SymEigArgs {
   unsigned* ctl = nullptr;    // 128 B: ctl[1] abort word (zeroed by the launcher)
   int* grid = nullptr;        // symeig_grid_bytes(): Sturm counts of the eigenvalue search grid
 };
-// 0 when the LDS-resident one-launch reduction fits this device (grid / rows per block out)
+// 0 when the on-chip one-launch reduction fits this device (grid / rows per block out)
 int symeig_plan(int64_t n, int* grid, int* rows_per_block);
 int64_t symeig_slot_stride(int64_t n);
 int64_t symeig_slot_bytes(int64_t n);

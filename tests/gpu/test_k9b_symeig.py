@@ -1,4 +1,4 @@
-"""K9b symmetric eigenvalues (LDS-resident Householder reduction + multisection) vs CPU fp64
+"""K9b symmetric eigenvalues (on-chip Householder reduction + multisection) vs CPU fp64
 ``torch.linalg.eigvalsh``, and the FID compute built on it."""
 
 import pytest

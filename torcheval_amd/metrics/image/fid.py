@@ -119,9 +119,9 @@ def cholesky_ex(s: Tensor) -> "tuple[Tensor, Tensor]":
 def sym_eigvalsh(m: Tensor) -> Tensor:
     """Eigenvalues (ascending) of a symmetric FP64 matrix.
 
-    On ROCm, K9b (``csrc/kernels/symeig.hip``): the matrix stays in LDS across the chip for
-    the whole Householder reduction (one cooperative launch, one hand-off per column) and a
-    multisection kernel finds the tridiagonal's eigenvalues - instead of rocSOLVER's
+    On ROCm, K9b (``csrc/kernels/symeig.hip``): the matrix stays on chip (the registers of one
+    workgroup per CU) for the whole Householder reduction (one cooperative launch, one
+    hand-off per column) and a multisection kernel finds the tridiagonal's eigenvalues - instead of rocSOLVER's
     ~7000 small launches.  Sizes the kernel does not take (n > 2560, n < 3), a grid the device
     cannot co-schedule, or an aborted grid fall back to ``torch.linalg.eigvalsh``."""
     if use_native(m) and m.dtype == torch.float64 and m.dim() == 2 and 3 <= m.shape[0] <= 2560:
