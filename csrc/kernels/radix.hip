@@ -293,6 +293,34 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     *a.dirty = static_cast<uint32_t>(a.rows * a.ngroups * kBins);  // for the next sort's pass 0
   const int64_t tn64 = a.n - tbase;
   const int tn = static_cast<int>(tn64 < kRTile ? tn64 : kRTile);
+  if (tn == kRTile) {
+    // full tile: every LDS read of the write-out issued before the dependent ones and all the
+    // stores after (a rolled loop paid sk -> base / tstart -> store round trips per element)
+    uint32_t kk[kRounds], vv[kRounds];
+    int32_t pb[kRounds];  // base - tile start of the element's digit (may be negative)
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      kk[j] = sk[threadIdx.x + j * kRT];
+      vv[j] = sv[threadIdx.x + j * kRT];
+    }
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      const uint32_t d = (kk[j] >> shift) & 0xffu;
+      pb[j] = static_cast<int32_t>(base[d]) - static_cast<int32_t>(tstart[d]);
+    }
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      const int64_t pos = row * a.n + static_cast<int64_t>(pb[j]) + (threadIdx.x + j * kRT);
+      if (last) {
+        a.out_sorted[pos] = key2f_desc(kk[j]);
+        a.out_order[pos] = static_cast<int32_t>(vv[j]);
+      } else {
+        keys_out[pos] = kk[j];
+        vals_out[pos] = vv[j];
+      }
+    }
+    return;
+  }
   for (int p = threadIdx.x; p < tn; p += kRT) {
     const uint32_t key = sk[p];
     const uint32_t d = (key >> shift) & 0xffu;
