@@ -20,6 +20,7 @@ from torcheval_amd.ops.classification import (
     cls_counts,
     cls_counts_supported,
     multilabel_counts,
+    native_cls,
     native_multilabel,
 )
 
@@ -154,6 +155,12 @@ def _multiclass_accuracy_update(
         buf = torch.zeros(2, num_classes, dtype=torch.float32, device=dev)
         cls_counts(input, target, k=k, num_classes=num_classes,
                    cls_correct=buf[0], cls_label=buf[1])
+        return buf[0], buf[1]
+    if average != "micro" and not input.is_cuda and native_cls(input, target, num_classes=num_classes):
+        # small CPU batches: the host twin of K1 fills both class histograms in one C++ call
+        # (the ATen chain is argmax, eq, two scatter_adds and their zero / ones tensors)
+        buf = torch.zeros(2, num_classes, dtype=torch.float32)
+        cls_counts(input, target, k=k, num_classes=num_classes, cls_correct=buf[0], cls_label=buf[1])
         return buf[0], buf[1]
     return _multiclass_accuracy_update_aten(input, target, average, num_classes, k)
 
