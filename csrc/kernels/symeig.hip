@@ -638,7 +638,7 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda
       X[x][y] = (i == k && i < b) ? 1.0 : 0.0;
     }
   // fully unrolled (no early exit: a break kept the loop rolled, and the pivot slot then went
-  // through dynamic register indexing - 164 us per block); the element updates are selects
+  // through dynamic register indexing - 164 us per block)
   bool bad = false;
 #pragma clang loop unroll(full)
   for (int j = 0; j < kPotrfB; ++j) {
@@ -658,26 +658,30 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda
         if (t == 0 && *info == 0) *info = k0 + j + 1;
         bad = true;
       } else {
-        const double sq = sqrt(d);
-        const double rs = 1.0 / sq, rd = rs * rs;
+        // 1/sqrt(d) from the hardware estimate + two Newton steps (a handful of FMAs on the
+        // per-column critical path instead of the IEEE sqrt and division sequences)
+        double rs = __builtin_amdgcn_rsq(d);
+        rs = fma(0.5 * rs, fma(-d * rs, rs, 1.0), rs);
+        rs = fma(0.5 * rs, fma(-d * rs, rs, 1.0), rs);
+        const double sq = d * rs, rd = rs * rs;
+        // masked coefficients instead of per-element selects: rows i <= j and columns k <= j
+        // take zero.  Entries above the diagonal (k > i) take updates too: they are never read
+        // (a column snapshot's rows above its pivot are masked here) and are zeroed on output.
+        // X needs no column mask: row j of X is zero past column j.
         double ci[4], ck[4], xr[4];
 #pragma unroll
-        for (int x = 0; x < 4; ++x) ci[x] = s_col[buf][ti + 16 * x] * rd;
+        for (int x = 0; x < 4; ++x) ci[x] = ti + 16 * x > j ? s_col[buf][ti + 16 * x] * rd : 0.0;
 #pragma unroll
         for (int y = 0; y < 4; ++y) {
-          ck[y] = s_col[buf][tj + 16 * y];
+          ck[y] = tj + 16 * y > j ? s_col[buf][tj + 16 * y] : 0.0;
           xr[y] = s_xr[buf][tj + 16 * y];
         }
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
-          const int i = ti + 16 * x;
 #pragma unroll
           for (int y = 0; y < 4; ++y) {
-            const int k = tj + 16 * y;
-            const double lu = fma(-ci[x], ck[y], L[x][y]);
-            const double xu = fma(-ci[x], xr[y], X[x][y]);
-            L[x][y] = (i > j && k > j && k <= i) ? lu : L[x][y];
-            X[x][y] = (i > j && k <= j) ? xu : X[x][y];
+            L[x][y] = fma(-ci[x], ck[y], L[x][y]);
+            X[x][y] = fma(-ci[x], xr[y], X[x][y]);
           }
         }
         // finish column j of L and row j of X (the snapshot the other threads read is unscaled)
