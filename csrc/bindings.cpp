@@ -96,8 +96,8 @@ void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, in
 }
 
 // Scratch that kernels overwrite before reading (no zeroing contract): per (device, stream,
-// slot), grown on demand.  ``fresh`` (optional) reports whether this call (re)allocated it.
-void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot, bool* fresh = nullptr) {
+// slot), grown on demand.
+void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot) {
   static std::mutex mu;
   static std::unordered_map<uint64_t, Tensor> cache;
   const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
@@ -109,9 +109,6 @@ void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, i
                           at::TensorOptions().dtype(at::kByte).device(like.device()));
     if (it == cache.end()) it = cache.emplace(key, ws).first;
     else it->second = ws;
-    if (fresh) *fresh = true;
-  } else if (fresh) {
-    *fresh = false;
   }
   return it->second.data_ptr();
 }
