@@ -58,15 +58,20 @@ __device__ __forceinline__ uint32_t load_key(const RadixArgs& a, const uint32_t*
   return keys_in[row * a.n + i];
 }
 
-// lanes (among `active`) holding the same 8-bit digit as this lane
+// lanes (among `active`) holding the same 8-bit digit as this lane.  Per bit: one signed
+// bit-field extract (0 / -1), the ballot, and an xnor + and per 32-bit half - the select form
+// (`bit ? ones : ~ones`) compiled to ~9 VALU per bit, and at 10M keys the downsweep is
+// VALU-bound on this match (SQ_INSTS_VALU ~2350 per wave, profiles/pmc_k3_multiclass_10m_r3.txt)
 __device__ __forceinline__ uint64_t match_digit(uint32_t d, uint64_t active) {
-  uint64_t peers = active;
+  uint32_t lo = static_cast<uint32_t>(active), hi = static_cast<uint32_t>(active >> 32);
 #pragma unroll
   for (int b = 0; b < 8; ++b) {
-    const uint64_t ones = __ballot((d >> b) & 1u);
-    peers &= ((d >> b) & 1u) ? ones : ~ones;
+    const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(d), b, 1));
+    const uint64_t ones = __ballot(m != 0u);
+    lo &= ~(static_cast<uint32_t>(ones) ^ m);
+    hi &= ~(static_cast<uint32_t>(ones >> 32) ^ m);
   }
-  return peers;
+  return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
 // pass-0 payload carried instead of the source index, converted per element from the
