@@ -611,29 +611,34 @@ namespace tea {
 namespace {
 
 constexpr int kPotrfB = 64;
+// 16 x 16 threads, 4 x 4 entries each (4 waves): ~35 us per 64 x 64 block.  Measured
+// alternatives: 32 x 32 threads with 2 x 2 entries 38 us (the 16-wave barrier costs more than
+// the FMAs it spreads), one wave with 8 x 8 entries 79 us (VALU-bound, spills to AGPRs)
+constexpr int kPG = 16;
+constexpr int kPE = kPotrfB / kPG;
 
-// Register-resident: thread (ti, tj) of a 16 x 16 grid holds L[ti + 16 x][tj + 16 y] and the
-// same entries of X (x, y < 4) in registers for the whole factorisation, and the column loop is
-// unrolled so the pivot's register slot (j >> 4) is a compile-time index.  Per column ONE
-// barrier: the threads holding column j of L / row j of X put their 4 values into an LDS
-// snapshot (double-buffered, so the next column's writes never race this column's reads), every
-// thread reads the snapshot entries its rows and columns need, and updates its 16 + 16 entries
+// Register-resident: thread (ti, tj) of a kPG x kPG grid holds L[ti + kPG x][tj + kPG y] and
+// the same entries of X (x, y < kPE) in registers for the whole factorisation, and the column
+// loop is unrolled so the pivot's register slot (j / kPG) is a compile-time index.  Per column
+// ONE barrier: the threads holding column j of L / row j of X put their kPE values into an LDS
+// snapshot (double-buffered, so the next column's writes never race this column's reads),
+// every thread reads the snapshot entries its rows and columns need, and updates its entries
 // in registers (right-looking potf2 on the lower triangle, the same elimination applied to the
 // identity).  Round 2's form kept L and X in LDS and re-read / re-wrote them every column: ~80
 // LDS operations per thread per column, 76 us per 64 x 64 block.
-__global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda, int k0, int b,
+__global__ __launch_bounds__(kPG * kPG) void potrf_block_kernel(double* A, int64_t lda, int k0, int b,
                                                           double* Linv, int* info) {
   __shared__ double s_col[2][kPotrfB];  // column j of L (unscaled), per step parity
   __shared__ double s_xr[2][kPotrfB];   // row j of X (unscaled)
   const int t = threadIdx.x;
-  const int ti = t >> 4, tj = t & 15;
+  const int ti = t / kPG, tj = t % kPG;
   double* blk = A + (int64_t)k0 * lda + k0;
-  double L[4][4], X[4][4];
+  double L[kPE][kPE], X[kPE][kPE];
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int x = 0; x < kPE; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const int i = ti + 16 * x, k = tj + 16 * y;
+    for (int y = 0; y < kPE; ++y) {
+      const int i = ti + kPG * x, k = tj + kPG * y;
       L[x][y] = (i < b && k <= i) ? blk[(int64_t)i * lda + k] : 0.0;
       X[x][y] = (i == k && i < b) ? 1.0 : 0.0;
     }
@@ -643,14 +648,14 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda
 #pragma clang loop unroll(full)
   for (int j = 0; j < kPotrfB; ++j) {
     if (j < b && !bad) {  // block-uniform
-      const int q = j >> 4, c = j & 15, buf = j & 1;
+      const int q = j / kPG, c = j % kPG, buf = j & 1;
       if (tj == c) {
 #pragma unroll
-        for (int x = 0; x < 4; ++x) s_col[buf][ti + 16 * x] = L[x][q];
+        for (int x = 0; x < kPE; ++x) s_col[buf][ti + kPG * x] = L[x][q];
       }
       if (ti == c) {
 #pragma unroll
-        for (int y = 0; y < 4; ++y) s_xr[buf][tj + 16 * y] = X[q][y];
+        for (int y = 0; y < kPE; ++y) s_xr[buf][tj + kPG * y] = X[q][y];
       }
       __syncthreads();
       const double d = s_col[buf][j];
@@ -668,18 +673,18 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda
         // take zero.  Entries above the diagonal (k > i) take updates too: they are never read
         // (a column snapshot's rows above its pivot are masked here) and are zeroed on output.
         // X needs no column mask: row j of X is zero past column j.
-        double ci[4], ck[4], xr[4];
+        double ci[kPE], ck[kPE], xr[kPE];
 #pragma unroll
-        for (int x = 0; x < 4; ++x) ci[x] = ti + 16 * x > j ? s_col[buf][ti + 16 * x] * rd : 0.0;
+        for (int x = 0; x < kPE; ++x) ci[x] = ti + kPG * x > j ? s_col[buf][ti + kPG * x] * rd : 0.0;
 #pragma unroll
-        for (int y = 0; y < 4; ++y) {
-          ck[y] = tj + 16 * y > j ? s_col[buf][tj + 16 * y] : 0.0;
-          xr[y] = s_xr[buf][tj + 16 * y];
+        for (int y = 0; y < kPE; ++y) {
+          ck[y] = tj + kPG * y > j ? s_col[buf][tj + kPG * y] : 0.0;
+          xr[y] = s_xr[buf][tj + kPG * y];
         }
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
+        for (int x = 0; x < kPE; ++x) {
 #pragma unroll
-          for (int y = 0; y < 4; ++y) {
+          for (int y = 0; y < kPE; ++y) {
             L[x][y] = fma(-ci[x], ck[y], L[x][y]);
             X[x][y] = fma(-ci[x], xr[y], X[x][y]);
           }
@@ -687,23 +692,23 @@ __global__ __launch_bounds__(256) void potrf_block_kernel(double* A, int64_t lda
         // finish column j of L and row j of X (the snapshot the other threads read is unscaled)
         if (tj == c) {
 #pragma unroll
-          for (int x = 0; x < 4; ++x) {
-            const int i = ti + 16 * x;
+          for (int x = 0; x < kPE; ++x) {
+            const int i = ti + kPG * x;
             L[x][q] = i > j ? L[x][q] * rs : (i == j ? sq : L[x][q]);
           }
         }
         if (ti == c) {
 #pragma unroll
-          for (int y = 0; y < 4; ++y) X[q][y] = tj + 16 * y <= j ? X[q][y] * rs : X[q][y];
+          for (int y = 0; y < kPE; ++y) X[q][y] = tj + kPG * y <= j ? X[q][y] * rs : X[q][y];
         }
       }
     }
   }
 #pragma unroll
-  for (int x = 0; x < 4; ++x)
+  for (int x = 0; x < kPE; ++x)
 #pragma unroll
-    for (int y = 0; y < 4; ++y) {
-      const int i = ti + 16 * x, k = tj + 16 * y;
+    for (int y = 0; y < kPE; ++y) {
+      const int i = ti + kPG * x, k = tj + kPG * y;
       if (i < b && k < b) {
         blk[(int64_t)i * lda + k] = k <= i ? L[x][y] : 0.0;
         Linv[(int64_t)i * b + k] = bad ? 0.0 : X[x][y];
@@ -718,7 +723,7 @@ int potrf_block_size() { return kPotrfB; }
 int launch_potrf_block(double* A, int64_t lda, int k0, int b, double* Linv, int* info,
                        hipStream_t stream) {
   if (b < 1 || b > kPotrfB) return 1;
-  potrf_block_kernel<<<1, 256, 0, stream>>>(A, lda, k0, b, Linv, info);
+  potrf_block_kernel<<<1, kPG * kPG, 0, stream>>>(A, lda, k0, b, Linv, info);
   return hipGetLastError() == hipSuccess ? 0 : 2;
 }
 
