@@ -254,8 +254,9 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     const uint64_t active = __ballot(valid);
     const uint32_t d = (k[j] >> shift) & 0xffu;
     const uint64_t peers = match_digit(d, active);
-    r[j] = wc[w][d] + static_cast<uint32_t>(__popcll(peers & below));
-    if (valid && (__ffsll(static_cast<long long>(peers)) - 1) == lane)
+    const uint64_t pb = peers & below;
+    r[j] = wc[w][d] + static_cast<uint32_t>(__popcll(pb));
+    if (valid && pb == 0ull)  // the lowest lane of the digit's peers advances its counter
       wc[w][d] += static_cast<uint32_t>(__popcll(peers));
   }
   __syncthreads();
