@@ -62,7 +62,9 @@ float* f32_out(const optional<Tensor>& t, const Tensor& ref, int64_t numel, cons
 // Allocate (warm up) before any HIP-graph capture that uses it.
 unsigned long long* fold_workspace(const Tensor& like, hipStream_t stream) {
   static std::mutex mu;
-  static std::unordered_map<uint64_t, Tensor> cache;
+  // process-lifetime (never destroyed): no device free from a static destructor at exit, after
+  // the HIP runtime or an attached profiler has already shut down
+  static auto& cache = *new std::unordered_map<uint64_t, Tensor>();
   const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
                        reinterpret_cast<uint64_t>(stream);
   std::lock_guard<std::mutex> lock(mu);
@@ -80,7 +82,9 @@ unsigned long long* fold_workspace(const Tensor& like, hipStream_t stream) {
 void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot,
                        int64_t* capacity = nullptr) {
   static std::mutex mu;
-  static std::unordered_map<uint64_t, Tensor> cache;
+  // process-lifetime (never destroyed): no device free from a static destructor at exit, after
+  // the HIP runtime or an attached profiler has already shut down
+  static auto& cache = *new std::unordered_map<uint64_t, Tensor>();
   const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
                        (static_cast<uint64_t>(slot) << 48) ^ reinterpret_cast<uint64_t>(stream);
   std::lock_guard<std::mutex> lock(mu);
@@ -99,7 +103,9 @@ void* zeroed_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, in
 // slot), grown on demand.
 void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, int slot) {
   static std::mutex mu;
-  static std::unordered_map<uint64_t, Tensor> cache;
+  // process-lifetime (never destroyed): no device free from a static destructor at exit, after
+  // the HIP runtime or an attached profiler has already shut down
+  static auto& cache = *new std::unordered_map<uint64_t, Tensor>();
   const uint64_t key = (static_cast<uint64_t>(like.device().index()) << 56) ^
                        (static_cast<uint64_t>(slot) << 48) ^ reinterpret_cast<uint64_t>(stream);
   std::lock_guard<std::mutex> lock(mu);
