@@ -269,6 +269,12 @@ def main() -> None:
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
+        # the sync engine's own RCCL communicators go first, while every peer is still alive
+        from torcheval_amd.parallel import rccl_direct
+
+        if not on_cpu:
+            torch.cuda.synchronize()
+        rccl_direct.destroy_all()
         dist.destroy_process_group()
 
 

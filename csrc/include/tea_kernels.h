@@ -486,4 +486,6 @@ int launch_snapshot_flags(const void* src, void* dst, int64_t bytes, const int* 
                           hipStream_t stream);
 // summed [ws][words][2] slots -> int32 [words], max over ranks
 int launch_merge_flag_slots(const float* slots, int* out, int words, int ws, hipStream_t stream);
+// test support (csrc/kernels/testing.hip): one lane spins until *flag != 0 or max_ms elapse
+int launch_spin_on_flag(const int* flag, int64_t max_ms, hipStream_t stream);
 }  // namespace tea

@@ -218,6 +218,8 @@ def test_binned_metrics_gpu_vs_cpu():
     y = torch.randint(0, 6, (3000,), generator=g)
     torch.testing.assert_close(multiclass_binned_auroc(X.to(DEV), y.to(DEV), num_classes=6)[0].cpu(),
                                multiclass_binned_auroc(X, y, num_classes=6)[0])
+    torch.testing.assert_close(multiclass_binned_auroc(X.to(DEV), y.to(DEV), num_classes=6, one_vs_rest=True)[0].cpu(),
+                               multiclass_binned_auroc(X, y, num_classes=6, one_vs_rest=True)[0])
     torch.testing.assert_close(multiclass_binned_auprc(X.to(DEV), y.to(DEV))[0].cpu(), multiclass_binned_auprc(X, y)[0])
     Y = torch.randint(0, 2, (3000, 6), generator=g)
     torch.testing.assert_close(multilabel_binned_auprc(X.to(DEV), Y.to(DEV))[0].cpu(), multilabel_binned_auprc(X, Y)[0])

@@ -151,4 +151,158 @@ def test_async_sync_on_side_stream_snapshots_at_call(pg, monkeypatch):
                 assert torch.equal(a, b)
         else:
             assert torch.equal(got, w)
-    assert not torch.equal(acc.compute(), want["acc"]) or True  # live metric moved on
+    # the live metrics moved on (20 more batches) while the synced copies kept the call's state
+    assert float(acc.num_total) == 23 * 4096
+    assert float(synced["acc"].num_total) == 3 * 4096
+    assert float(cm.confusion_matrix.sum()) == 23 * 4096
+    assert float(synced["cm"].confusion_matrix.sum()) == 3 * 4096
+
+
+def test_graphed_update_survives_a_sync(pg):
+    """a sync must not rebind the states a captured HIP graph writes."""
+    from torcheval_amd.metrics import MulticlassAccuracy, MulticlassConfusionMatrix
+    from torcheval_amd.metrics.toolkit import get_synced_metric, sync_and_compute
+    from torcheval_amd.utils.graphs import GraphedUpdate
+
+    g = torch.Generator(device=DEV).manual_seed(3)
+    xs = [torch.randn(1024, 50, device=DEV, generator=g) for _ in range(5)]
+    ys = [torch.randint(0, 50, (1024,), device=DEV, generator=g) for _ in range(5)]
+    for m in (MulticlassAccuracy(device=DEV), MulticlassConfusionMatrix(50, device=DEV)):
+        step = GraphedUpdate(m, xs[0], ys[0])
+        for i in range(3):
+            step(xs[i], ys[i])
+        with collectives_at_world_size_1():
+            synced = get_synced_metric(m)
+            v = sync_and_compute(m)
+        torch.testing.assert_close(v, synced.compute())
+        for i in range(3, 5):
+            step(xs[i], ys[i])  # must land in the live metric
+        ref = type(m)(device=DEV) if isinstance(m, MulticlassAccuracy) else MulticlassConfusionMatrix(50, device=DEV)
+        for i in range(5):
+            ref.update(xs[i], ys[i])
+        assert torch.equal(m.compute(), ref.compute())
+        m.reset()  # in place: the graph keeps writing the same buffer
+        step(xs[0], ys[0])
+        ref.reset()
+        ref.update(xs[0], ys[0])
+        assert torch.equal(m.compute(), ref.compute())
+        m.load_state_dict(ref.state_dict())  # rebinds: the next replay must refuse
+        with pytest.raises(RuntimeError, match="rebound after graph capture"):
+            step(xs[1], ys[1])
+
+
+def test_direct_plan_covers_flags_bool_and_wide_types(pg):
+    """The out-of-place grouped plan: confusion matrix (large f32 group + int32 flag), bool /
+    f64 / i64 states; the synced copies view a fresh buffer, the live buffer is untouched."""
+    from torcheval_amd.metrics.toolkit import get_synced_metric
+    from torcheval_amd.parallel import state_buffer as sbm
+    from torcheval_amd.metrics.metric import Metric
+
+    class Mixed(Metric[torch.Tensor]):
+        def __init__(self):
+            super().__init__(device=DEV)
+            self._add_state("f", torch.zeros(5, dtype=torch.float64, device=DEV), merge="sum")
+            self._add_state("i", torch.zeros(3, dtype=torch.int64, device=DEV), merge="max")
+            self._add_state("b", torch.zeros(7, dtype=torch.bool, device=DEV), merge="sum")
+            self._add_state("h", torch.zeros(9, dtype=torch.bfloat16, device=DEV), merge="min")
+
+        def update(self, x):
+            self.f += x[:5].double()
+            self.i.copy_(torch.maximum(self.i, x[:3].long()))
+            self.b |= x[:7] > 0
+            self.h.copy_(torch.minimum(self.h, x[:9].bfloat16()))
+            return self
+
+        def compute(self):
+            return self.f
+
+        def merge_state(self, metrics):
+            return self
+
+    _, cm, _ = _metrics()
+    mx = Mixed().update(torch.arange(-4.0, 12.0, device=DEV))
+    with collectives_at_world_size_1():
+        for m in (cm, mx):
+            synced = get_synced_metric(m)
+            plan = sbm._plan_for(sbm.buffer_of(m), dist.group.WORLD, 1, m)
+            assert plan.rplan is not None
+            for name in m._state_merge_kinds():
+                a, b = getattr(synced, name), getattr(m, name)
+                assert torch.equal(a, b) and a.data_ptr() != b.data_ptr(), name
+    assert synced.b.dtype == torch.bool
+    assert torch.equal(get_synced_metric_flag(cm), torch.zeros(3, dtype=torch.int32, device=DEV))
+
+
+def get_synced_metric_flag(cm):
+    from torcheval_amd.metrics.toolkit import get_synced_metric
+
+    with collectives_at_world_size_1():
+        return get_synced_metric(cm)._err
+
+
+def test_sync_timeout_raises_then_recovers(pg):
+    """A collective held behind a spinning kernel: ``timeout=`` raises TimeoutError near the
+    deadline (direct path kept), the communicator is aborted in the background, and the next
+    sync builds a fresh one and succeeds."""
+    import time
+    from datetime import timedelta
+
+    from torcheval_amd.metrics.toolkit import sync_and_compute
+
+    _, cm, _ = _metrics()
+    with collectives_at_world_size_1():
+        want = sync_and_compute(cm)  # builds the communicator and the plan
+        torch.cuda.synchronize()
+        h_old = rccl_direct.comm_for(dist.group.WORLD, 1, DEV)
+        native().test_host_flag_set(0)
+        native().test_spin_on_host_flag(0, 20000)  # holds the stream for at most 20 s
+        t0 = time.perf_counter()
+        try:
+            with pytest.raises(TimeoutError, match="did not complete"):
+                sync_and_compute(cm, timeout=timedelta(milliseconds=500))
+            elapsed = time.perf_counter() - t0
+        finally:
+            native().test_host_flag_set(1)
+        torch.cuda.synchronize()
+        assert 0.4 < elapsed < 5.0, elapsed
+        assert rccl_direct.state(h_old) in (1, 2)
+        got = sync_and_compute(cm, timeout=timedelta(seconds=60))
+        h_new = rccl_direct.comm_for(dist.group.WORLD, 1, DEV)
+    assert h_new != h_old and rccl_direct.state(h_new) == 0
+    assert rccl_direct.state(h_old) == 2  # aborted
+    assert torch.equal(got, want)
+
+
+def test_watchdog_deadline_without_timeout_argument(pg, monkeypatch):
+    """No ``timeout=``: the sync returns at once (stream-ordered) and the watchdog enforces the
+    communicator's deadline (the process group's timeout by default) in the background.  With
+    TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING=0 the process survives; the next sync rebuilds."""
+    import time
+
+    from torcheval_amd.metrics.toolkit import get_synced_metric, sync_and_compute
+
+    monkeypatch.setenv("TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING", "0")
+    acc, _, _ = _metrics()
+    with collectives_at_world_size_1():
+        want = sync_and_compute(acc)
+        torch.cuda.synchronize()
+        h = rccl_direct.comm_for(dist.group.WORLD, 1, DEV)
+        assert rccl_direct.group_timeout(dist.group.WORLD, DEV).total_seconds() > 60  # the PG's own
+        native().rccl_set_timeout(h, 300)
+        native().test_host_flag_set(0)
+        native().test_spin_on_host_flag(0, 20000)
+        try:
+            fut = get_synced_metric(acc)  # enqueued behind the spinning kernel; no host wait
+            deadline = time.perf_counter() + 10
+            while rccl_direct.state(h) == 0 and time.perf_counter() < deadline:
+                time.sleep(0.05)
+            st = rccl_direct.state(h)
+        finally:
+            native().test_host_flag_set(1)
+        torch.cuda.synchronize()
+        del fut
+        assert st in (1, 2), st
+        assert "did not complete" in native().rccl_comm_reason(h)
+        got = sync_and_compute(acc)  # rebuilds the communicator
+        assert rccl_direct.comm_for(dist.group.WORLD, 1, DEV) != h
+    assert torch.equal(got, want)

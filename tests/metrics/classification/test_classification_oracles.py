@@ -323,7 +323,8 @@ class TestBinned(MetricClassTester):
         xm, ym = _mc_data(15)
         xm = (xm * 10).round() / 10
         thr_m = torch.linspace(0, 1, 11)
-        aucs, _ = multiclass_binned_auroc(xm.reshape(-1, C), ym.flatten(), num_classes=C, threshold=thr_m, average=None)
+        aucs, _ = multiclass_binned_auroc(xm.reshape(-1, C), ym.flatten(), num_classes=C, threshold=thr_m, average=None,
+                                       one_vs_rest=True)
         exact_m = multiclass_auroc(xm.reshape(-1, C), ym.flatten(), num_classes=C, average=None)
         torch.testing.assert_close(aucs.double(), exact_m.double(), atol=1e-5, rtol=1e-5)
 

@@ -47,6 +47,25 @@ def test_reset_is_one_copy_and_keeps_views():
     assert float(m.compute()) == 3.0
 
 
+def test_compute_then_reset_keeps_the_returned_value():
+    """``v = m.compute(); m.reset()`` must leave ``v`` alone even though the reset
+    restores the state buffer in place (reference metric.py:120-147 rebinds instead)."""
+    from torcheval_amd.metrics import Max, Min
+
+    s = Sum().update(torch.tensor([1.0, 2.0]))
+    mx = Max().update(torch.tensor([1.0, 5.0]))
+    mn = Min().update(torch.tensor([1.0, -5.0]))
+    cm = MulticlassConfusionMatrix(3).update(torch.eye(3), torch.arange(3))
+    for m in (s, mx, mn, cm):
+        assert buffer_of(m) is not None  # what the first sync builds
+    got = [m.compute() for m in (s, mx, mn, cm)] + [cm.normalized(None)]
+    for m in (s, mx, mn, cm):
+        m.reset()
+    assert float(got[0]) == 3.0 and float(got[1]) == 5.0 and float(got[2]) == -5.0
+    assert torch.equal(got[3], torch.eye(3)) and torch.equal(got[4], torch.eye(3))
+    assert float(cm.compute().sum()) == 0.0
+
+
 def test_rebinding_rebuilds_the_buffer():
     m = Mean()
     m.update(torch.tensor([1.0, 3.0]))

@@ -23,7 +23,7 @@ class Max(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:
-        return self.max
+        return self.max.clone()  # reset() restores states in place
 
     @torch.inference_mode()
     def merge_state(self, metrics: Iterable["Max"]) -> "Max":

@@ -34,7 +34,8 @@ class Sum(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:
-        return self.weighted_sum
+        # a copy: reset() restores the state buffer in place, so the state itself would be zeroed
+        return self.weighted_sum.clone()
 
     @torch.inference_mode()
     def merge_state(self, metrics: Iterable["Sum"]) -> "Sum":

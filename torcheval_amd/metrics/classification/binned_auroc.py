@@ -47,7 +47,8 @@ class BinaryBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[torch.T
 
 
 class MulticlassBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[torch.Tensor, torch.Tensor]]):
-    """(one-vs-rest binned AUROC, thresholds).  Functional: ``multiclass_binned_auroc``."""
+    """(binned AUROC, thresholds).  Functional: ``multiclass_binned_auroc``: the reference's
+    per-sample rows by default, per-class one-vs-rest with ``one_vs_rest=True``."""
 
     def __init__(
         self,
@@ -55,6 +56,7 @@ class MulticlassBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[tor
         num_classes: int,
         threshold: Union[int, List[float], torch.Tensor] = 200,
         average: Optional[str] = "macro",
+        one_vs_rest: bool = False,
         device: Optional[torch.device] = None,
     ) -> None:
         super().__init__(device=device)
@@ -63,10 +65,12 @@ class MulticlassBinnedAUROC(_ThresholdFollowsDevice, SampleStoreMetric[Tuple[tor
         self.num_classes = num_classes
         self.threshold = threshold
         self.average = average
+        self.one_vs_rest = one_vs_rest
 
     def _check(self, input, target) -> None:
         _multiclass_binned_auroc_update_input_check(input, target, self.num_classes)
 
     @torch.inference_mode()
     def compute(self) -> Tuple[torch.Tensor, torch.Tensor]:
-        return _multiclass_binned_auroc_compute(*self._cat(), self.num_classes, self.threshold, self.average)
+        return _multiclass_binned_auroc_compute(*self._cat(), self.num_classes, self.threshold, self.average,
+                                                getattr(self, "one_vs_rest", False))

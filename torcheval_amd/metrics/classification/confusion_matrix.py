@@ -88,14 +88,17 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
     @torch.inference_mode()
     def compute(self: TMulticlassConfusionMatrix) -> torch.Tensor:
         self._check_device_errors()
-        return _confusion_matrix_compute(self.confusion_matrix, normalize=self.normalize)
+        out = _confusion_matrix_compute(self.confusion_matrix, normalize=self.normalize)
+        # never hand out the state itself: reset() restores the state buffer in place
+        return out.clone() if out is self.confusion_matrix else out
 
     @torch.inference_mode()
     def normalized(self: TMulticlassConfusionMatrix, normalize: Optional[str] = None) -> torch.Tensor:
         """The confusion matrix normalised with ``normalize`` (ignores the constructor's)."""
         _confusion_matrix_param_check(self.num_classes, normalize)
         self._check_device_errors()
-        return _confusion_matrix_compute(self.confusion_matrix, normalize)
+        out = _confusion_matrix_compute(self.confusion_matrix, normalize)
+        return out.clone() if out is self.confusion_matrix else out
 
     @torch.inference_mode()
     def merge_state(

@@ -1,5 +1,8 @@
 """Binned AUROC, functional API (parity: functional/classification/binned_auroc.py:17-256).
 
+``multiclass_binned_auroc`` reproduces the reference's per-sample rows by default and offers
+per-class one-vs-rest as ``one_vs_rest=True`` (docs/parity.md).
+
 The reference materialises a [T, tasks, N] boolean prediction tensor (binned_auroc.py:
 111-138); here the per-threshold TP/FP counts come from the K4 histogram kernel and the
 trapezoid runs over the T+1 curve points.
@@ -92,12 +95,61 @@ def multiclass_binned_auroc(
     num_classes: int,
     threshold: Union[int, List[float], torch.Tensor] = DEFAULT_NUM_THRESHOLD,
     average: Optional[str] = "macro",
+    one_vs_rest: bool = False,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """One-vs-rest binned AUROC.  Class: ``MulticlassBinnedAUROC``."""
+    """Binned AUROC for multiclass scores.  Class: ``MulticlassBinnedAUROC``.
+
+    By default this returns exactly what the reference returns (binned_auroc.py:188-215): the
+    one-hot product is summed over the CLASS dim, so each row of the curve is one SAMPLE (its
+    true-class score as the single positive, its other classes as negatives), and ``average=None``
+    gives one value per sample.  The reference's own example: ``tensor(0.4000)`` and the
+    5-vector ``[0.5, 0.25, 0.25, 0.0, 1.0]`` for 5 samples x 3 classes.
+
+    ``one_vs_rest=True`` opts into per-class one-vs-rest binned AUROC (one value per class;
+    at thresholds that cover every score it equals the exact ``multiclass_auroc``), computed
+    from the K4 histogram kernel.
+    """
     threshold = _create_threshold_tensor(threshold, target.device)
     _multiclass_binned_auroc_param_check(num_classes, threshold, average)
     _multiclass_binned_auroc_update_input_check(input, target, num_classes)
-    return _multiclass_binned_auroc_compute(input, target, num_classes, threshold, average)
+    return _multiclass_binned_auroc_compute(input, target, num_classes, threshold, average, one_vs_rest)
+
+
+def _per_sample_binned_auroc(input: torch.Tensor, target: torch.Tensor, num_classes: int,
+                             threshold: torch.Tensor) -> torch.Tensor:
+    """float32 [N]: the reference's per-sample rows, without its [T, N, C] boolean tensor.
+
+    Each score's bin b = #{t : score >= thr_t} (one searchsorted); per sample, the count of
+    classes at or above thr_t is the suffix sum of a [T + 1] histogram of its bins; the true
+    class contributes tp_t = [t < b_true] and the rest fp_t.  The trapezoid runs over the
+    descending-threshold curve with a leading 0, as ``rot90`` + ``pad`` build it there."""
+    if target.numel() and (int(target.min()) < 0 or int(target.max()) >= num_classes):
+        raise RuntimeError("Class values must be smaller than num_classes.")  # F.one_hot's check
+    n, T = input.shape[0], threshold.numel()
+    dev = input.device
+    dt = torch.promote_types(input.dtype, threshold.dtype)
+    thr = threshold.to(device=dev, dtype=dt).contiguous()
+    out = torch.empty(n, dtype=torch.float32, device=dev)
+    ar = torch.arange(T, device=dev)
+    step = max(1, (1 << 24) // max(T + 1, num_classes))  # bounds the [rows, T + 1] temporaries
+    for s0 in range(0, n, step):
+        x = input[s0 : s0 + step].to(dt)
+        rows = x.shape[0]
+        b = torch.searchsorted(thr, x.contiguous(), right=True)
+        b = torch.where(torch.isnan(x), torch.zeros_like(b), b)  # NaN >= thr is false
+        hist = torch.zeros(rows, T + 1, dtype=torch.int64, device=dev).scatter_add_(1, b, torch.ones_like(b))
+        ge = hist.flip(1).cumsum(1).flip(1)[:, 1:]  # [rows, T]: classes with score >= thr_t
+        b_true = b.gather(1, target[s0 : s0 + step].long().view(-1, 1))
+        tp = (ar.view(1, -1) < b_true).to(torch.int64)
+        fp = ge - tp
+        zero = torch.zeros(rows, 1, dtype=torch.int64, device=dev)
+        tpd = torch.cat([zero, tp.flip(1)], 1).to(torch.float64)
+        fpd = torch.cat([zero, fp.flip(1)], 1).to(torch.float64)
+        area = ((fpd[:, 1:] - fpd[:, :-1]) * (tpd[:, 1:] + tpd[:, :-1])).sum(1) / 2  # exact
+        factor = (tp[:, 0] * fp[:, 0]).to(torch.float32)
+        res = area.to(torch.float32) / torch.where(factor == 0, torch.ones_like(factor), factor)
+        out[s0 : s0 + rows] = torch.where(factor == 0, torch.full_like(res, 0.5), res)
+    return out
 
 
 def _multiclass_binned_auroc_compute(
@@ -106,9 +158,13 @@ def _multiclass_binned_auroc_compute(
     num_classes: int,
     threshold: torch.Tensor,
     average: Optional[str] = "macro",
+    one_vs_rest: bool = False,
 ) -> Tuple[torch.Tensor, torch.Tensor]:
-    tp, fp, _ = binned_counts(input, target, threshold, 1)
-    auroc = _binned_trapz(tp, fp).to(torch.float32)
+    if one_vs_rest:
+        tp, fp, _ = binned_counts(input, target, threshold, 1)
+        auroc = _binned_trapz(tp, fp).to(torch.float32)
+    else:
+        auroc = _per_sample_binned_auroc(input, target, num_classes, threshold)
     if isinstance(average, str) and average == "macro":
         return auroc.mean(), threshold
     return auroc, threshold

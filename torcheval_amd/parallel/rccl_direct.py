@@ -5,8 +5,22 @@ objects, stream-sync events, watchdog bookkeeping: ``profiles/rccl_primitive_lat
 which is most of a small-state ``sync_and_compute``.  For its hot path the sync engine
 (``parallel/state_buffer.py``) keeps one RCCL communicator per process group of its own:
 rank 0 draws an ``ncclUniqueId``, the group broadcasts it once through torch.distributed, and
-``ncclAllGather`` / ``ncclAllReduce`` are then enqueued straight onto the caller's current HIP
-stream (ordered after the update kernels, no cross-stream events).
+each metric's sync is then ONE grouped RCCL call (a registered *plan*: every state run of the
+metric's contiguous buffer all-reduced out of place into a result buffer) enqueued straight
+onto the caller's current HIP stream.
+
+Failure semantics match c10d's (reference ``toolkit.py:388`` runs under the process group's
+timeout):
+
+* every collective records a completion event that a native watchdog thread polls, with
+  ``ncclCommGetAsyncError``; the deadline defaults to the process group's own timeout;
+* a collective still pending at its deadline, or an async RCCL error, aborts the communicator
+  (``ncclCommAbort``) and - like c10d's default async error handling - tears the process down
+  with a message (``TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING=0``: keep the process; the next
+  sync raises and rebuilds the communicator);
+* a sync given an explicit ``timeout=`` waits for its own completion on the host and raises
+  ``TimeoutError`` at the deadline; the communicator is aborted in the background and the next
+  sync on the group builds a fresh one.
 
 Bootstrapping is collective: every rank of the group reaches ``comm_for`` at the same sync
 (the engine's plans are built at the same call on every rank).  ``TORCHEVAL_AMD_DIRECT_RCCL=0``
@@ -16,13 +30,18 @@ collectives on other streams with metric syncs in a rank-dependent order).
 
 import atexit
 import os
-from typing import Dict, Optional
+from datetime import timedelta
+from typing import Dict, List, Optional, Sequence
 
 import torch
 import torch.distributed as dist
 
 _COMMS: Dict[int, tuple] = {}  # id(group) -> (group, world size, handle)
+# bumped whenever a communicator is dropped: cached sync plans holding an older handle rebuild
+GENERATION = [0]
+_ABORTING: List[int] = []  # failed handles whose background abort a new communicator waits for
 _OPS = {"sum": 0, "max": 1, "min": 2}
+_DEFAULT_TIMEOUT = timedelta(minutes=10)  # c10d's NCCL default when the group reports none
 
 
 def enabled() -> bool:
@@ -33,15 +52,42 @@ def enabled() -> bool:
     return native_loaded() and bool(native().rccl_available())
 
 
+def group_timeout(group, device: torch.device) -> timedelta:
+    """The process group's own collective timeout (the direct path's default deadline)."""
+    try:
+        t = group._get_backend(device).options._timeout
+        if isinstance(t, timedelta) and t.total_seconds() > 0:
+            return t
+    except Exception:  # noqa: BLE001 - backends without options (fake / custom groups)
+        pass
+    t = getattr(dist.distributed_c10d, "default_pg_nccl_timeout", None)
+    return t if isinstance(t, timedelta) else _DEFAULT_TIMEOUT
+
+
+def _ms(t: timedelta) -> int:
+    return max(1, int(t.total_seconds() * 1000))
+
+
 def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
-    """The direct communicator of ``group`` (created on first use, collectively), or None."""
+    """The direct communicator of ``group`` (created on first use, collectively), or None.
+
+    A communicator that failed (deadline or async error) is replaced by a fresh one here, after
+    its background abort has finished."""
     if device.type != "cuda" or not enabled():
         return None
-    hit = _COMMS.get(id(group))
-    if hit is not None and hit[0] is group and hit[1] == ws:
-        return hit[2]
     from torcheval_amd.ops import native
 
+    hit = _COMMS.get(id(group))
+    if hit is not None and hit[0] is group and hit[1] == ws:
+        h = hit[2]
+        if h is None or native().rccl_comm_state(h) == 0:
+            return h
+        native().rccl_wait_aborted(h, 60_000)
+        del _COMMS[id(group)]
+        GENERATION[0] += 1
+
+    while _ABORTING:  # never bootstrap next to a communicator that is still being torn down
+        native().rccl_wait_aborted(_ABORTING.pop(), 60_000)
     rank = dist.get_rank(group)
     uid = torch.zeros(128, dtype=torch.uint8)
     if rank == 0:
@@ -52,7 +98,8 @@ def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
         dist.broadcast(dev_uid, src=src, group=group)
         uid = dev_uid.cpu()
     try:
-        handle: Optional[int] = int(native().rccl_comm_init(uid, ws, rank, device.index if device.index is not None else 0))
+        handle: Optional[int] = int(native().rccl_comm_init(
+            uid, ws, rank, device.index if device.index is not None else 0, _ms(group_timeout(group, device))))
     except RuntimeError:
         handle = None
     if ws > 1:
@@ -66,6 +113,64 @@ def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
             handle = None
     _COMMS[id(group)] = (group, ws, handle)
     return handle
+
+
+def forget(handle: int) -> None:
+    """Drop a failed communicator from the cache (the next ``comm_for`` rebuilds)."""
+    for k, (_, _, h) in list(_COMMS.items()):
+        if h == handle:
+            del _COMMS[k]
+    _ABORTING.append(handle)
+    GENERATION[0] += 1
+
+
+def state(handle: int) -> int:
+    """0 ok, 1 failed (abort pending), 2 aborted, 3 destroyed."""
+    from torcheval_amd.ops import native
+
+    return int(native().rccl_comm_state(handle))
+
+
+def wait(handle: int, timeout: timedelta) -> None:
+    """Block until the newest collective of ``handle`` completes; ``TimeoutError`` at the deadline
+    (the communicator is then aborted in the background and replaced at the next sync)."""
+    from torcheval_amd.ops import native
+
+    if not native().rccl_wait(handle, _ms(timeout)):
+        reason = native().rccl_comm_reason(handle)
+        forget(handle)
+        raise TimeoutError(f"metric-state sync did not complete within {timeout} ({reason})")
+
+
+def plan_create(ops: Sequence[Sequence[int]]) -> int:
+    """Register a sync plan: ``[kind, src_off, dst_off, count, dtype_code, op_code]`` per operand
+    (kind 0 all-reduce of ``count`` elements, 1 all-gather of ``count`` bytes; byte offsets)."""
+    from torcheval_amd.ops import native
+
+    return int(native().rccl_plan_create([list(map(int, o)) for o in ops]))
+
+
+def plan_run(handle: int, plan: int, src: torch.Tensor, dst: torch.Tensor, ws: int, grouped: bool = False) -> None:
+    from torcheval_amd.ops import native
+
+    try:
+        native().rccl_plan_run(handle, plan, src, dst, ws, grouped)
+    except RuntimeError:
+        if state(handle) != 0:  # failed earlier (watchdog): rebuild at the next sync
+            forget(handle)
+        raise
+
+
+def group_start() -> None:
+    from torcheval_amd.ops import native
+
+    native().rccl_group_start()
+
+
+def group_end(track: int = -1, device: Optional[torch.device] = None) -> None:
+    from torcheval_amd.ops import native
+
+    native().rccl_group_end(track, device.index if device is not None and device.index is not None else 0)
 
 
 def all_gather(handle: int, src: torch.Tensor, out: torch.Tensor) -> None:
@@ -82,19 +187,23 @@ def all_reduce(handle: int, t: torch.Tensor, op: str, out: Optional[torch.Tensor
 
 
 def destroy_all() -> None:
-    """Destroy every direct communicator (also registered with atexit)."""
+    """Destroy every direct communicator (after its work drains) and stop the watchdog.
+    Call it before ``dist.destroy_process_group()``; also registered with atexit."""
     from torcheval_amd.ops import native, native_loaded
 
     if not native_loaded():
         return
-    for _, _, handle in list(_COMMS.values()):
-        if handle is None:
-            continue
+    handles: List[int] = [h for _, _, h in _COMMS.values() if h is not None]
+    _COMMS.clear()
+    for handle in handles:
         try:
             native().rccl_comm_destroy(handle)
         except RuntimeError:
             pass
-    _COMMS.clear()
+    try:
+        native().rccl_shutdown()
+    except RuntimeError:
+        pass
 
 
 atexit.register(destroy_all)

@@ -312,7 +312,7 @@ class _Plan:
     the send view, the receive size, the segment table and where each state lands."""
 
     __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large", "fused",
-                 "rank", "flag_src", "comm", "single")
+                 "rank", "flag_src", "comm", "single", "gen", "rplan", "dassign")
 
     def __init__(self, sb: StateBuffer, group, ws: int, metric) -> None:
         from torch.distributed.distributed_c10d import _get_default_group
@@ -359,12 +359,35 @@ class _Plan:
         if (self.comm is not None and not sb.flag_words and len(gath) == 1 and gath[0].off == sb.gather_off
                 and gath[0].op == "sum" and gath[0].dtype != torch.bool):
             self.single = (gath[0].dtype, gath[0].nbytes)
+        self.gen = rccl_direct.GENERATION[0]
+        # the direct plan: every group (and the error flag, max-merged as int32) all-reduced OUT OF
+        # PLACE from the live buffer into a result buffer of the same layout, as ONE RCCL group
+        # (csrc/runtime/rccl_direct.cpp) - no snapshot copy, no gather + seg_reduce pass.  int16
+        # has no RCCL type: such metrics keep the gather path.
+        self.rplan = None
+        self.dassign = None
+        if self.comm is not None and all(g.dtype != torch.int16 for g in sb.groups):
+            ops = []
+            for g in sb.groups:
+                op = g.op if g.dtype != torch.bool else ("min" if g.op == "min" else "max")  # or / and
+                ops.append((0, g.off, g.off, g.nbytes // _esize(g.dtype), _DT_CODE[g.dtype], _OP_CODE[op]))
+            if sb.flag_words:
+                ops.append((0, sb.flag_off, sb.flag_off, sb.flag_words, _DT_CODE[torch.int32], _OP_CODE["max"]))
+            self.rplan = rccl_direct.plan_create(ops)
+            self.dassign = []
+            for g in sb.groups:
+                es = _esize(g.dtype)
+                for name, shape, boff, n in g.members:
+                    prop = isinstance(getattr(cls, name, None), property)
+                    self.dassign.append((name, g.dtype, (g.off + boff) // es, n, shape if shape else None, prop))
+            if sb.flag_words:
+                self.dassign.append(("_err", torch.int32, sb.flag_off // 4, sb.flag_words, (sb.flag_words,), False))
 
 
 def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
     key = (id(group), ws)
     plan = sb.plans.get(key)
-    if plan is None or plan.group is not group:
+    if plan is None or plan.group is not group or (plan.comm is not None and plan.gen != rccl_direct.GENERATION[0]):
         plan = sb.plans[key] = _Plan(sb, group, ws, metric)
     return plan
 
@@ -387,7 +410,40 @@ def _direct(plan: _Plan) -> Optional[int]:
     return plan.comm if collectives.current_sync_timeout() is None else None
 
 
+def _merged_copy(m, dst: torch.Tensor, dassign):
+    """A shallow copy of ``m`` whose states view the synced buffer ``dst`` (same layout)."""
+    r = object.__new__(type(m))  # a shallow copy (copy.copy costs ~4x this)
+    d = r.__dict__
+    getstate = getattr(type(m), "__getstate__", None)
+    d.update(m.__dict__ if getstate is None else getstate(m))
+    d["_tea_sb"] = None
+    typed = {}
+    for name, dtype, eo, n, shape, prop in dassign:
+        t = typed.get(dtype)
+        if t is None:
+            t = typed[dtype] = dst.view(dtype)
+        v = t[eo] if shape is None else t[eo : eo + n].view(shape)
+        if prop:
+            setattr(r, name, v)
+        else:
+            d[name] = v
+    return r
+
+
+def _sync_one_direct(m, sb: StateBuffer, plan: _Plan):
+    """ONE grouped RCCL call from the live buffer into a fresh result buffer, stream-ordered
+    after the updates; with a ``timeout=``, the host waits for it (``TimeoutError``)."""
+    dst = torch.empty(sb.buf.numel(), dtype=torch.uint8, device=sb.device)
+    rccl_direct.plan_run(plan.comm, plan.rplan, sb.buf, dst, plan.ws)
+    t = collectives.current_sync_timeout()
+    if t is not None:
+        rccl_direct.wait(plan.comm, t)
+    return _merged_copy(m, dst, plan.dassign)
+
+
 def _sync_one(m, sb: StateBuffer, plan: _Plan):
+    if plan.rplan is not None:
+        return _sync_one_direct(m, sb, plan)
     ws = plan.ws
     snap = None
     merged_err = None
@@ -487,7 +543,7 @@ class _FastIssue:
     """A fast sync between issue and finish: the snapshots, the receive buffer and (async) the
     event the side stream records after its collectives."""
 
-    __slots__ = ("metrics", "sbs", "reduced", "gathered", "ws", "row_bytes", "done", "dev", "keep")
+    __slots__ = ("metrics", "sbs", "reduced", "gathered", "ws", "row_bytes", "done", "dev", "keep", "direct")
 
 
 def _fast_issue(metrics, group, ws: int, side: bool) -> Optional[_FastIssue]:
@@ -513,6 +569,10 @@ def _fast_issue(metrics, group, ws: int, side: bool) -> Optional[_FastIssue]:
         comm = rccl_direct.comm_for(group if group is not None else _get_default_group(), ws, dev)
     if side and comm is None:
         return None
+    if comm is not None:
+        plans = [_plan_for(sb, group, ws, m) for sb, m in zip(sbs, metrics.values())]
+        if all(p.rplan is not None for p in plans):
+            return _fast_issue_direct(metrics, sbs, plans, comm, ws, dev, side)
 
     # snapshots (the live buffers keep changing under later updates on the async path)
     reduced: List[Optional[torch.Tensor]] = [sb.buf[: sb.reduce_end].clone() if sb.reduce_end else None for sb in sbs]
@@ -546,6 +606,7 @@ def _fast_issue(metrics, group, ws: int, side: bool) -> Optional[_FastIssue]:
     issue.metrics, issue.sbs, issue.reduced, issue.ws, issue.row_bytes, issue.dev = metrics, sbs, reduced, ws, row_bytes, dev
     issue.keep = send  # referenced until finish: the side stream reads it
     issue.done = None
+    issue.direct = None
     if side:
         ready = torch.cuda.Event()
         ready.record()
@@ -553,6 +614,11 @@ def _fast_issue(metrics, group, ws: int, side: bool) -> Optional[_FastIssue]:
         stream.wait_event(ready)
         with torch.cuda.stream(stream):
             issue.gathered = collectives_now()
+        # allocated on the compute stream, used by RCCL on the side stream: a dropped future must
+        # not let the caching allocator hand these blocks out while the collectives still run
+        for t in [x for x in reduced if x is not None] + [send, gathered]:
+            if t is not None:
+                t.record_stream(stream)
         issue.done = torch.cuda.Event()
         issue.done.record(stream)
     else:
@@ -560,10 +626,53 @@ def _fast_issue(metrics, group, ws: int, side: bool) -> Optional[_FastIssue]:
     return issue
 
 
+def _fast_issue_direct(metrics, sbs, plans, comm: int, ws: int, dev: torch.device, side: bool) -> _FastIssue:
+    """Every metric's plan in ONE RCCL group, out of place into per-metric result buffers.  The
+    async form snapshots each buffer (one copy; later updates keep writing the live ones) and
+    runs the group on the engine's side stream."""
+    dsts = [torch.empty(sb.buf.numel(), dtype=torch.uint8, device=dev) for sb in sbs]
+    issue = _FastIssue()
+    issue.metrics, issue.sbs, issue.ws, issue.dev = metrics, sbs, ws, dev
+    issue.reduced, issue.gathered, issue.row_bytes, issue.keep = None, None, 0, None
+    issue.direct = (dsts, plans)
+    issue.done = None
+
+    def run(srcs):
+        rccl_direct.group_start()
+        try:
+            for p, src, dst in zip(plans, srcs, dsts):
+                rccl_direct.plan_run(comm, p.rplan, src, dst, ws, grouped=True)
+        finally:
+            rccl_direct.group_end(comm, dev)
+
+    if side:
+        srcs = [sb.buf.clone() for sb in sbs]
+        ready = torch.cuda.Event()
+        ready.record()
+        stream = _side_stream(dev)
+        stream.wait_event(ready)
+        with torch.cuda.stream(stream):
+            run(srcs)
+        for t in srcs + dsts:
+            t.record_stream(stream)
+        issue.keep = srcs
+        issue.done = torch.cuda.Event()
+        issue.done.record(stream)
+    else:
+        run([sb.buf for sb in sbs])
+        t = collectives.current_sync_timeout()
+        if t is not None:
+            rccl_direct.wait(comm, t)
+    return issue
+
+
 def _fast_finish(issue: _FastIssue) -> Dict[str, "object"]:
     """The merged metrics of an issued fast sync (shallow copies viewing the merged buffers)."""
     if issue.done is not None:
         torch.cuda.current_stream(issue.dev).wait_event(issue.done)
+    if issue.direct is not None:
+        dsts, plans = issue.direct
+        return {key: _merged_copy(m, dst, p.dassign) for (key, m), dst, p in zip(issue.metrics.items(), dsts, plans)}
     metrics, sbs, ws = issue.metrics, issue.sbs, issue.ws
     merged_small: Optional[torch.Tensor] = None
     if issue.gathered is not None:

@@ -10,6 +10,11 @@ Requirements (checked): the update must write its states in place (the native ke
 an update that rebinds a state attribute, e.g. ``self.x = self.x + y``, would replay against
 stale tensors and is rejected), must not synchronise with the host, and every replay must
 use inputs of the captured shapes / dtypes.
+
+The metric's contiguous state buffer (``parallel/state_buffer.py``) is built right before capture,
+so a later ``sync_and_compute`` / ``reset`` finds it valid and never rebinds the states the
+graph writes.  Anything else that rebinds a state after capture (``load_state_dict``,
+``to()``) is caught at the next replay, which raises instead of writing into freed memory.
 """
 
 from typing import Any, Dict, List, Tuple
@@ -58,6 +63,12 @@ class GraphedUpdate:
             for _ in range(warmup):  # workspaces / lazy buffers are created outside capture
                 metric.update(*self._static)
         torch.cuda.current_stream().wait_stream(stream)
+        # the states (and error flags the warm-up created) move into their final contiguous
+        # buffer now, not at the first sync, which would rebind what the graph writes
+        from torcheval_amd.parallel.state_buffer import buffer_of
+
+        buffer_of(metric)
+        stream.wait_stream(torch.cuda.current_stream())
         ptrs = _state_ptrs(metric)
         self.graph = torch.cuda.CUDAGraph()
         try:
@@ -81,6 +92,8 @@ class GraphedUpdate:
                 else:
                     setattr(metric, name, v)
         torch.cuda.current_stream().wait_stream(stream)
+        self._names = tuple(n for n, p in ptrs.items() if isinstance(p, int))
+        self._ptrs = tuple(ptrs[n] for n in self._names)
 
     @property
     def static_inputs(self) -> Tuple[torch.Tensor, ...]:
@@ -96,6 +109,12 @@ class GraphedUpdate:
                 )
             if src.data_ptr() != dst.data_ptr():
                 dst.copy_(src, non_blocking=True)
+        m = self.metric
+        if tuple(getattr(m, n).data_ptr() for n in self._names) != self._ptrs:
+            raise RuntimeError(
+                f"{type(m).__name__}: a state was rebound after graph capture (load_state_dict / to()); "
+                "re-create the GraphedUpdate"
+            )
         self.graph.replay()
         mark = getattr(self.metric, "_mark_updated", None)
         if mark is not None:  # metrics with deferred folds (K1 micro's pending cells)
