@@ -33,6 +33,8 @@ def _t(fn, n=300) -> float:
 
 def main() -> None:
     from torcheval_amd.metrics import MulticlassAccuracy, MulticlassConfusionMatrix
+    from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
+    from torcheval_amd.parallel import rccl_direct
     from torcheval_amd.metrics.toolkit import get_synced_metric, sync_and_compute
     from torcheval_amd.parallel import state_buffer as sbm
     from torcheval_amd.parallel.collectives import collectives_at_world_size_1
@@ -44,21 +46,33 @@ def main() -> None:
     y = torch.randint(0, 1000, (8192,), device=dev)
     out = {}
     with collectives_at_world_size_1():
-        for name, m in (("acc", MulticlassAccuracy(device=dev)), ("cm", MulticlassConfusionMatrix(1000, device=dev))):
-            m.update(x, y)
+        fid = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=2048, device=dev)
+        fid.update_activations(torch.randn(1000, 2048, device=dev), True)
+        fid.update_activations(torch.randn(1000, 2048, device=dev), False)
+        for name, m in (("acc", MulticlassAccuracy(device=dev)), ("cm", MulticlassConfusionMatrix(1000, device=dev)),
+                        ("fid", fid)):
+            if name != "fid":
+                m.update(x, y)
             sync_and_compute(m)
             sb = sbm.buffer_of(m)
             plan = sbm._plan_for(sb, dist.group.WORLD, 1, m)
             res = {
-                "sync_and_compute": _t(lambda: sync_and_compute(m)),
                 "get_synced_metric": _t(lambda: get_synced_metric(m)),
-                "local_compute": _t(lambda: m.compute()),
                 "buffer_valid": _t(lambda: sb.valid(m)),
                 "sync_one": _t(lambda: sbm._sync_one(m, sb, plan)),
             }
-            if plan.src is not None:
+            if name != "fid":  # FID's compute is the D=2048 eigen-solve (profiled separately)
+                res["sync_and_compute"] = _t(lambda: sync_and_compute(m))
+                res["local_compute"] = _t(lambda: m.compute())
+            if plan.rplan is not None:  # the direct plan's phases
+                dst = torch.empty(sb.buf.numel(), dtype=torch.uint8, device=dev)
+                res["result_alloc"] = _t(lambda: torch.empty(sb.buf.numel(), dtype=torch.uint8, device=dev))
+                res["plan_run"] = _t(lambda: rccl_direct.plan_run(plan.comm, plan.rplan, sb.buf, dst, 1))
+                res["merged_copy"] = _t(lambda: sbm._merged_copy(m, dst, plan.dassign))
+                res["device_copy_same_bytes"] = _t(lambda: dst.copy_(sb.buf))
+            if plan.src is not None and plan.rplan is None:
                 res["gather_only"] = _t(lambda: sbm._gather(plan, plan.src))
-            if plan.large:
+            if plan.large and plan.rplan is None:
                 res["snapshot_clone"] = _t(lambda: sb.buf[: sb.reduce_end].clone())
                 snap = sb.buf[: sb.reduce_end].clone()
                 off, nb, dtype, op = plan.large[0]

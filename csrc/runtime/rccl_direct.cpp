@@ -107,6 +107,7 @@ struct Comm {
   int64_t timeout_ms = 600000;
   std::atomic<int> state{kOk};
   bool observed = false;  // a blocking waiter reported the failure itself (no teardown)
+  bool teardown = false;  // decided when the failure is detected (env read then, not at abort)
   std::string reason;
 };
 
@@ -156,6 +157,7 @@ void mark_failed_locked(int64_t handle, const std::string& why, bool observed) {
   if (!c.state.compare_exchange_strong(expect, kFailed)) return;
   c.reason = why;
   c.observed = observed;
+  c.teardown = !observed && teardown_on_failure();
   g_abort_queue.push_back(handle);
   g_cv.notify_all();
 }
@@ -176,7 +178,7 @@ void abort_comm(int64_t handle) {
     std::lock_guard<std::mutex> lock(g_mu);
     Comm& c = *g_comms[handle];
     c.state.store(kAborted);
-    teardown = !c.observed && teardown_on_failure();
+    teardown = c.teardown;
     why = c.reason;
     // the aborted collectives' events complete once the stream drains; drop them unqueried
     for (auto it = g_pending.begin(); it != g_pending.end();) {

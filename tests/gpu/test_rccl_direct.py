@@ -303,6 +303,11 @@ def test_watchdog_deadline_without_timeout_argument(pg, monkeypatch):
         del fut
         assert st in (1, 2), st
         assert "did not complete" in native().rccl_comm_reason(h)
-        got = sync_and_compute(acc)  # rebuilds the communicator
+        # the failure was not observed by a waiter: the next use raises (its result would have
+        # been garbage), and the sync after that runs on a fresh communicator
+        with pytest.raises(RuntimeError, match="unusable"):
+            sync_and_compute(acc)
+        assert native().rccl_wait_aborted(h, 30000)
+        got = sync_and_compute(acc)
         assert rccl_direct.comm_for(dist.group.WORLD, 1, DEV) != h
     assert torch.equal(got, want)

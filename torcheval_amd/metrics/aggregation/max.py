@@ -23,7 +23,7 @@ class Max(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:
-        return self.max.clone()  # reset() restores states in place
+        return self.max if self._tea_sb is None else self.max.clone()  # buffer reset is in place
 
     @torch.inference_mode()
     def merge_state(self, metrics: Iterable["Max"]) -> "Max":

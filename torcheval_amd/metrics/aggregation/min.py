@@ -23,7 +23,7 @@ class Min(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:
-        return self.min.clone()  # reset() restores states in place
+        return self.min if self._tea_sb is None else self.min.clone()  # buffer reset is in place
 
     @torch.inference_mode()
     def merge_state(self, metrics: Iterable["Min"]) -> "Min":

@@ -34,8 +34,8 @@ class Sum(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:
-        # a copy: reset() restores the state buffer in place, so the state itself would be zeroed
-        return self.weighted_sum.clone()
+        # a copy once the state lives in a state buffer: reset() then restores it in place
+        return self.weighted_sum if self._tea_sb is None else self.weighted_sum.clone()
 
     @torch.inference_mode()
     def merge_state(self, metrics: Iterable["Sum"]) -> "Sum":

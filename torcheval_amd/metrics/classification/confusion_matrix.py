@@ -89,8 +89,8 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
     def compute(self: TMulticlassConfusionMatrix) -> torch.Tensor:
         self._check_device_errors()
         out = _confusion_matrix_compute(self.confusion_matrix, normalize=self.normalize)
-        # never hand out the state itself: reset() restores the state buffer in place
-        return out.clone() if out is self.confusion_matrix else out
+        # never hand out a state that lives in a state buffer: reset() restores it in place
+        return out.clone() if out is self.confusion_matrix and self._tea_sb is not None else out
 
     @torch.inference_mode()
     def normalized(self: TMulticlassConfusionMatrix, normalize: Optional[str] = None) -> torch.Tensor:
@@ -98,7 +98,7 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
         _confusion_matrix_param_check(self.num_classes, normalize)
         self._check_device_errors()
         out = _confusion_matrix_compute(self.confusion_matrix, normalize)
-        return out.clone() if out is self.confusion_matrix else out
+        return out.clone() if out is self.confusion_matrix and self._tea_sb is not None else out
 
     @torch.inference_mode()
     def merge_state(

@@ -41,8 +41,11 @@ _REDUCE_OPS = {
 
 # ---------------------------------------------------------------------------- all-reduce
 
-# Per-call deadline for the metric-sync collectives; None = the process
-# group's own timeout.  Set through ``sync_timeout`` / the toolkit's ``timeout=`` argument.
+# Per-call deadline for the metric-sync collectives, set through
+# ``sync_timeout`` / the toolkit's ``timeout=`` argument: the sync then waits on the host and
+# raises TimeoutError at the deadline, on the direct RCCL path (parallel/rccl_direct.py) as on
+# torch.distributed's.  None = no host wait: torch.distributed's watchdog, or the direct path's
+# own watchdog thread, enforces the process group's timeout in the background.
 _SYNC_TIMEOUT: "contextvars.ContextVar[Optional[timedelta]]" = contextvars.ContextVar(
     "torcheval_amd_sync_timeout", default=None
 )
