@@ -23,6 +23,7 @@
 //  * "narrow" kernel (C <= 32): one thread per row, LDS-privatised class histograms.
 //  * invalid targets / predictions never fault: they are skipped and flagged in ``err``
 //    (bit 0: target out of range, bit 1: predicted label out of range).
+#include <algorithm>
 #include <cstdlib>
 
 #include "tea_common.h"
@@ -428,10 +429,12 @@ __global__ __launch_bounds__(kBlock) void cls_micro_kernel(ClsCountsArgs a) {
   block_micro(a, correct_acc, rows_acc);
 }
 
-// The north-star launch: pending-cell epilogue and a 48-byte kernel-argument block (one
-// scalar cache line) instead of the ~200-byte ClsCountsArgs.  Each wave's first instructions
-// wait on its kernel arguments; with the wide struct the first wave of every CU fetched four
-// lines of it (profiles/k1_floor_r4.txt: 6.50 us against a 5.97 us pure-read floor).
+// The north-star launch: pending-cell epilogue and a compact kernel-argument block.  Each
+// wave's first instructions wait on its kernel arguments, and with ClsCountsArgs (~200 B) and
+// in-kernel lane-mask arithmetic the generated code issued the kernarg loads in two dependent
+// rounds and ~60 scalar instructions before the first row load.  Here everything the row
+// loads need sits in the first 64 B (one s_load_dwordx16), and the ballot lane masks of the
+// tie check (a function of C only) are computed on the host (profiles/k1_floor_r4*.txt).
 struct MicroPendArgs {
   const void* input;
   const void* target;
@@ -439,16 +442,68 @@ struct MicroPendArgs {
   float* total;
   int64_t n;
   int64_t row_stride;
+  int32_t c;
+  int32_t pad;
+  uint64_t lanes[kChunkLoads];  // per 16-B load of the chunk: lanes whose columns are < C
 };
 
 template <int KIND, typename TGT>
-__global__ __launch_bounds__(kBlock) void cls_micro_pend_kernel(MicroPendArgs a, int C) {
-  uint32_t correct_acc = 0, rows_acc = 0;
-  micro_rows<KIND, TGT>(a.input, static_cast<const TGT*>(a.target), a.n, C, a.row_stride, correct_acc, rows_acc);
+__device__ __forceinline__ bool micro_row(const MicroPendArgs& a, const char* __restrict__ rp, int64_t t, int lane) {
+  constexpr int VEC = KIND == 0 ? 4 : 8;
+  constexpr int NV = kChunkLoads * VEC;
+  constexpr int STEP = kWave * VEC;
+  typedef typename RowVals<NV>::type vec_t;
+  const int C = a.c;
+  float f[kChunkLoads][VEC];
+#pragma unroll
+  for (int u = 0; u < kChunkLoads; ++u) {
+    const int col = u * STEP + lane * VEC;
+    load_vec<KIND, VEC>(rp, col < C ? col : 0, f[u]);
+  }
+  vec_t v;
+#pragma unroll
+  for (int u = 0; u < kChunkLoads; ++u)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) v[u * VEC + e] = f[u][e];
+  float m = fmaximum(v[0], v[1]);
+#pragma unroll
+  for (int e = 2; e < NV; ++e) m = fmaximum(m, v[e]);
+  const float wm = wave_max_dpp(m);
+  if (__builtin_expect(wm != wm, 0)) return row_argmax_exact<KIND>(rp, C, lane) == t;  // NaN row
+  if (!(t >= 0 && t < C)) return false;
+  const int tu = static_cast<int>(t);
+  const float sel = v[(tu / STEP) * VEC + (tu % VEC)];  // uniform index: one indexed move
+  const float xt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sel), (tu % STEP) / VEC));
+  if (xt != wm) return false;
+  // the target holds the max: correct iff it is the only column that does
+  int cnt = 0;
+#pragma unroll
+  for (int u = 0; u < kChunkLoads; ++u)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) cnt += __builtin_popcountll(__ballot(v[u * VEC + e] == wm) & a.lanes[u]);
+  return cnt == 1 || row_argmax_exact<KIND>(rp, C, lane) == t;
+}
+
+template <int KIND, typename TGT>
+__global__ __launch_bounds__(kBlock) void cls_micro_pend_kernel(MicroPendArgs a) {
+  constexpr int ELSIZE = KIND == 0 ? 4 : 2;
+  const int lane = lane_id();
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  // the wave's first row is loaded unconditionally (clamped to the last row), so nothing
+  // branches on `n` before the loads and every kernel argument arrives in one scalar round trip
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id();
+  const int64_t r0 = row0 < a.n ? row0 : a.n - 1;  // the launcher guarantees n >= 1
+  const bool c0 = micro_row<KIND, TGT>(a, static_cast<const char*>(a.input) + r0 * a.row_stride * ELSIZE,
+                                       static_cast<const TGT*>(a.target)[r0], lane);
+  uint32_t correct_acc = (row0 < a.n && c0) ? 1u : 0u;
+  for (int64_t row = row0 + nwaves; row < a.n; row += nwaves) {
+    const char* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELSIZE;
+    correct_acc += micro_row<KIND, TGT>(a, rp, static_cast<const TGT*>(a.target)[row], lane);
+  }
   // deferred fold: one no-return atomic per wave into one of 64 pending cells, no LDS, no
   // block barrier, no returning atomic on the kernel's tail (the fold's ~0.6 us + the block
   // reduction's ~0.45 us in the A/B harness); the metric folds the cells at compute / sync
-  if (lane_id() == 0 && correct_acc)
+  if (lane == 0 && correct_acc)
     atomicAdd(a.pend + ((blockIdx.x * kWavesPerBlock + wave_id()) % kPendCells) * kPendStride,
               static_cast<unsigned long long>(correct_acc));
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.total) atomicAdd(a.total, static_cast<float>(a.n));
@@ -604,13 +659,16 @@ void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
   const bool micro_only = micro_on && pred_free && VEC > 1 && a.k == 1 && a.cls_correct == nullptr &&
                           a.cls_label == nullptr && a.err == nullptr && a.err_max == nullptr && !a.check_target;
   if (micro_only && a.pend && (a.tg_dt == DType::i64 || a.tg_dt == DType::i32)) {
-    const MicroPendArgs m{a.input, a.target, a.pend, a.micro_total, a.n, a.row_stride};
+    MicroPendArgs m{a.input, a.target, a.pend, a.micro_total, a.n, a.row_stride, static_cast<int32_t>(a.c), 0, {}};
+    constexpr int kStep = kWave * VEC;
+    for (int u = 0; u < kChunkLoads; ++u) {
+      const int64_t valid = std::min<int64_t>(std::max<int64_t>((a.c - u * kStep + VEC - 1) / VEC, 0), kWave);
+      m.lanes[u] = valid >= kWave ? ~0ull : ((1ull << valid) - 1);
+    }
     if (a.tg_dt == DType::i64)
-      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t>), dim3(grid), dim3(kBlock), 0, s, m,
-                         static_cast<int>(a.c));
+      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t>), dim3(grid), dim3(kBlock), 0, s, m);
     else
-      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t>), dim3(grid), dim3(kBlock), 0, s, m,
-                         static_cast<int>(a.c));
+      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t>), dim3(grid), dim3(kBlock), 0, s, m);
     return;
   }
   if (micro_only && a.tg_dt == DType::i64) {

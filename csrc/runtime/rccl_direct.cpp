@@ -117,12 +117,14 @@ struct Pending {
   Clock::time_point deadline;
 };
 
-std::mutex g_mu;
-std::condition_variable g_cv;
-std::vector<std::unique_ptr<Comm>> g_comms;  // handle = index (slots are never reused)
-std::deque<Pending> g_pending;
-std::vector<hipEvent_t> g_event_pool;
-std::vector<int64_t> g_abort_queue;
+// Process-lifetime state, never destroyed: a watchdog still running when static destructors
+// start (a program that skipped Python's atexit) must not find its mutex or queues gone.
+std::mutex& g_mu = *new std::mutex;
+std::condition_variable& g_cv = *new std::condition_variable;
+std::vector<std::unique_ptr<Comm>>& g_comms = *new std::vector<std::unique_ptr<Comm>>;  // handle = index
+std::deque<Pending>& g_pending = *new std::deque<Pending>;
+std::vector<hipEvent_t>& g_event_pool = *new std::vector<hipEvent_t>;
+std::vector<int64_t>& g_abort_queue = *new std::vector<int64_t>;
 std::thread* g_watchdog = nullptr;  // leaked on purpose: joined by rccl_shutdown, never destroyed at exit
 bool g_stop = false;
 
@@ -514,7 +516,7 @@ struct Plan {
   std::vector<PlanOp> ops;
   int64_t src_end = 0, dst_end_per_rank = 0;
 };
-std::vector<Plan> g_plans;  // under g_mu; plans are immutable once created
+std::deque<Plan>& g_plans = *new std::deque<Plan>;  // under g_mu; immutable, stable addresses
 
 // codes of torcheval_amd.parallel.state_buffer._DT_CODE
 bool nccl_dtype(int64_t code, ncclDataType_t* dt, int64_t* es) {
