@@ -5,7 +5,8 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/gpu/test_k1_micro.py tests/gpu/test_k1_classification.py tests/gpu/test_accuracy_gpu.py > gpurun_out/r4e_tests.log 2>&1
+  tests/gpu/test_k1_micro.py tests/gpu/test_k1_classification.py tests/gpu/test_accuracy_gpu.py \
+  tests/gpu/test_rccl_direct.py tests/gpu/test_sync_multirank_kernels.py > gpurun_out/r4e_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/r4e_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 120 ./csrc/bench/k1_floor.bin 8 400 > gpurun_out/k1_floor_r4c.txt 2>&1
 rc=$?; cat gpurun_out/k1_floor_r4c.txt; [ $rc -ne 0 ] && exit $rc

@@ -512,9 +512,17 @@ struct PlanOp {
   ncclRedOp_t op;
   int64_t esize;
 };
+// A state view of the result buffer (the synced metric's states): dtype, element offset into
+// the buffer viewed as that dtype, shape (empty = 0-dim).
+struct ViewSpec {
+  at::ScalarType dtype;
+  int64_t elem_off;
+  std::vector<int64_t> shape;
+};
 struct Plan {
   std::vector<PlanOp> ops;
   int64_t src_end = 0, dst_end_per_rank = 0;
+  std::vector<ViewSpec> views;
 };
 std::deque<Plan>& g_plans = *new std::deque<Plan>;  // under g_mu; immutable, stable addresses
 
@@ -613,6 +621,62 @@ void rccl_plan_run(int64_t handle, int64_t plan, const at::Tensor& src, const at
   if (!grouped) track(handle, s);
 }
 
+at::ScalarType scalar_of_code(int64_t code) {
+  switch (code) {
+    case 0: return at::kFloat;
+    case 1: return at::kHalf;
+    case 2: return at::kBFloat16;
+    case 3: return at::kDouble;
+    case 4: return at::kLong;
+    case 5: return at::kInt;
+    case 6: return at::kByte;
+    case 7: return at::kBool;
+    case 8: return at::kChar;
+    case 9: return at::kShort;
+    default: TORCH_CHECK(false, "rccl_plan_set_views: bad dtype code ", code);
+  }
+  return at::kByte;
+}
+
+// views: [dtype_code, elem_off, *shape] per state, in the order the caller assigns them
+void rccl_plan_set_views(int64_t plan, const std::vector<std::vector<int64_t>>& views) {
+  std::vector<ViewSpec> vs;
+  for (const auto& v : views) {
+    TORCH_CHECK(v.size() >= 2 && v[1] >= 0, "rccl_plan_set_views: each view is [dtype, elem_off, *shape]");
+    vs.push_back({scalar_of_code(v[0]), v[1], std::vector<int64_t>(v.begin() + 2, v.end())});
+  }
+  std::lock_guard<std::mutex> lock(g_mu);
+  TORCH_CHECK(plan >= 0 && plan < static_cast<int64_t>(g_plans.size()), "rccl_plan_set_views: invalid plan ", plan);
+  g_plans[plan].views = std::move(vs);
+}
+
+// The whole direct sync of one metric in one call: a fresh result buffer like `src`, the
+// plan's grouped collectives (live buffer -> result, on the current stream), and the synced
+// states as views of the result buffer (plan order).  Returns [result, *views].
+std::vector<at::Tensor> rccl_plan_sync(int64_t handle, int64_t plan, const at::Tensor& src, int64_t nranks) {
+  at::Tensor dst = at::empty_like(src);
+  rccl_plan_run(handle, plan, src, dst, nranks, false);
+  const Plan* p;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    p = &g_plans[plan];
+  }
+  std::vector<at::Tensor> out;
+  out.reserve(p->views.size() + 1);
+  out.push_back(dst);
+  at::Tensor typed[32];  // one typed view of the result buffer per dtype (ScalarType < 32)
+  for (const auto& v : p->views) {
+    const int key = static_cast<int>(v.dtype);
+    TORCH_CHECK(key >= 0 && key < 32, "rccl_plan_sync: dtype out of range");
+    if (!typed[key].defined()) typed[key] = dst.view(v.dtype);
+    const at::Tensor& t = typed[key];
+    std::vector<int64_t> strides(v.shape.size(), 1);
+    for (int64_t d = static_cast<int64_t>(v.shape.size()) - 2; d >= 0; --d) strides[d] = strides[d + 1] * v.shape[d + 1];
+    out.push_back(t.as_strided(v.shape, strides, v.elem_off));
+  }
+  return out;
+}
+
 // ------------------------------------------------------------------ test support
 // A pinned, device-visible host flag and a one-lane kernel that spins on it (bounded by
 // max_ms of wall clock): lets a test hold a stream ahead of a collective to exercise the
@@ -671,6 +735,11 @@ void tea_register_rccl(pybind11::module_& m) {
   m.def("rccl_plan_run", &rccl_plan_run, "run a sync plan as one RCCL group (src -> dst, out of place)",
         py::arg("handle"), py::arg("plan"), py::arg("src"), py::arg("dst"), py::arg("nranks"),
         py::arg("grouped") = false);
+  m.def("rccl_plan_set_views", &rccl_plan_set_views, "register a plan's state views: [[dtype, elem_off, *shape]]",
+        py::arg("plan"), py::arg("views"));
+  m.def("rccl_plan_sync", &rccl_plan_sync,
+        "fresh result buffer + the plan's grouped collectives + the synced state views -> [result, *views]",
+        py::arg("handle"), py::arg("plan"), py::arg("src"), py::arg("nranks"));
   m.def("rccl_group_start", &rccl_group_start, "ncclGroupStart");
   m.def("rccl_group_end", &rccl_group_end, "ncclGroupEnd (+ completion event of track_handle on device's stream)",
         py::arg("track_handle") = -1, py::arg("device") = 0);

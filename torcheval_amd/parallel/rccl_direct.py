@@ -150,6 +150,25 @@ def plan_create(ops: Sequence[Sequence[int]]) -> int:
     return int(native().rccl_plan_create([list(map(int, o)) for o in ops]))
 
 
+def plan_set_views(plan: int, views: Sequence[Sequence[int]]) -> None:
+    """Register the synced-state views of a plan: ``[dtype_code, elem_off, *shape]`` each."""
+    from torcheval_amd.ops import native
+
+    native().rccl_plan_set_views(plan, [list(map(int, v)) for v in views])
+
+
+def plan_sync(handle: int, plan: int, src: torch.Tensor, ws: int) -> List[torch.Tensor]:
+    """Fresh result buffer + the plan's grouped collectives + the state views: [result, *views]."""
+    from torcheval_amd.ops import native
+
+    try:
+        return native().rccl_plan_sync(handle, plan, src, ws)
+    except RuntimeError:
+        if state(handle) != 0:  # failed earlier (watchdog): rebuild at the next sync
+            forget(handle)
+        raise
+
+
 def plan_run(handle: int, plan: int, src: torch.Tensor, dst: torch.Tensor, ws: int, grouped: bool = False) -> None:
     from torcheval_amd.ops import native
 

@@ -108,7 +108,8 @@ class StateBuffer:
     """The contiguous state buffer of one metric plus its cached sync plans."""
 
     __slots__ = ("buf", "device", "groups", "reduce_end", "gather_off", "gather_bytes", "flag_off",
-                 "flag_words", "names", "ptrs", "err_obj", "default_img", "nbytes", "_seg_cache", "plans")
+                 "flag_words", "names", "ptrs", "err_obj", "default_img", "nbytes", "_seg_cache", "plans",
+                 "_plain", "_props")
 
     # ---------------------------------------------------------------- construction
     @classmethod
@@ -171,6 +172,13 @@ class StateBuffer:
             metric._err = slot
         self.err_obj = getattr(metric, "_err", None) if words else None
         self.ptrs = tuple(getattr(metric, n).data_ptr() for n in self.names)
+        # the validity check: plain attributes by object identity straight from the instance
+        # dict (no data_ptr calls), properties (e.g. states with a deferred fold) through getattr
+        cls = type(metric)
+        self._plain = tuple((n, metric.__dict__.get(n)) for n in self.names
+                            if not isinstance(getattr(cls, n, None), property) and n in metric.__dict__)
+        plain = {n for n, _ in self._plain}
+        self._props = tuple((n, p) for n, p in zip(self.names, self.ptrs) if n not in plain)
         self._seg_cache = None
         self.plans = {}
         metric._tea_sb = self
@@ -217,12 +225,19 @@ class StateBuffer:
     def valid(self, metric) -> bool:
         if self.buf is None:
             return False
-        if self.flag_words and getattr(metric, "_err", None) is not self.err_obj:
+        d = metric.__dict__
+        if self.flag_words and d.get("_err", getattr(metric, "_err", None)) is not self.err_obj:
             return False
+        for n, obj in self._plain:
+            if d.get(n) is not obj:
+                return False
         try:
-            return tuple(getattr(metric, n).data_ptr() for n in self.names) == self.ptrs
+            for n, p in self._props:
+                if getattr(metric, n).data_ptr() != p:
+                    return False
         except AttributeError:
             return False
+        return True
 
     def segments(self, base: int = 0) -> Tuple[List[int], List[int], List[int], List[int]]:
         """(byte offsets relative to the gather region + base, counts, dtype codes, op codes)."""
@@ -312,7 +327,7 @@ class _Plan:
     the send view, the receive size, the segment table and where each state lands."""
 
     __slots__ = ("group", "pg", "ws", "nccl", "src", "row_bytes", "segs", "assign", "flag", "large", "fused",
-                 "rank", "flag_src", "comm", "single", "gen", "rplan", "dassign")
+                 "rank", "flag_src", "comm", "single", "gen", "rplan", "dassign", "dnames")
 
     def __init__(self, sb: StateBuffer, group, ws: int, metric) -> None:
         from torch.distributed.distributed_c10d import _get_default_group
@@ -382,6 +397,11 @@ class _Plan:
                     self.dassign.append((name, g.dtype, (g.off + boff) // es, n, shape if shape else None, prop))
             if sb.flag_words:
                 self.dassign.append(("_err", torch.int32, sb.flag_off // 4, sb.flag_words, (sb.flag_words,), False))
+            # the synced states are built as views of the result buffer inside the same native
+            # call (rccl_plan_sync): one pybind round trip instead of a Python view per state
+            rccl_direct.plan_set_views(self.rplan, [
+                [_DT_CODE[dt], eo, *(shape if shape is not None else ())] for _, dt, eo, _, shape, _ in self.dassign])
+            self.dnames = [(name, prop) for name, _, _, _, _, prop in self.dassign]
 
 
 def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
@@ -432,13 +452,23 @@ def _merged_copy(m, dst: torch.Tensor, dassign):
 
 def _sync_one_direct(m, sb: StateBuffer, plan: _Plan):
     """ONE grouped RCCL call from the live buffer into a fresh result buffer, stream-ordered
-    after the updates; with a ``timeout=``, the host waits for it (``TimeoutError``)."""
-    dst = torch.empty(sb.buf.numel(), dtype=torch.uint8, device=sb.device)
-    rccl_direct.plan_run(plan.comm, plan.rplan, sb.buf, dst, plan.ws)
+    after the updates, and the synced states as views of it - one native call; with a
+    ``timeout=``, the host waits for it (``TimeoutError``)."""
+    views = rccl_direct.plan_sync(plan.comm, plan.rplan, sb.buf, plan.ws)
     t = collectives.current_sync_timeout()
     if t is not None:
         rccl_direct.wait(plan.comm, t)
-    return _merged_copy(m, dst, plan.dassign)
+    r = object.__new__(type(m))  # a shallow copy (copy.copy costs ~4x this)
+    d = r.__dict__
+    getstate = getattr(type(m), "__getstate__", None)
+    d.update(m.__dict__ if getstate is None else getstate(m))
+    d["_tea_sb"] = None
+    for (name, prop), v in zip(plan.dnames, views[1:]):
+        if prop:
+            setattr(r, name, v)
+        else:
+            d[name] = v
+    return r
 
 
 def _sync_one(m, sb: StateBuffer, plan: _Plan):
