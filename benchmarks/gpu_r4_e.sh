@@ -14,6 +14,8 @@ timeout -k 10 200 python benchmarks/sync_breakdown.py > gpurun_out/sync_breakdow
 rc=$?; cat gpurun_out/sync_breakdown_r4.json; [ $rc -ne 0 ] && { tail -20 gpurun_out/sb.err; exit $rc; }
 timeout -k 10 300 python benchmarks/rccl_sync_floor.py > gpurun_out/sync_floor_r4.json 2> gpurun_out/sync_floor_r4.err
 rc=$?; cat gpurun_out/sync_floor_r4.json; [ $rc -ne 0 ] && exit $rc
+timeout -k 10 200 python benchmarks/latency_anatomy.py > gpurun_out/latency_anatomy_r4.json 2> gpurun_out/la.err
+rc=$?; echo "latency anatomy: $(cat gpurun_out/latency_anatomy_r4.json)"; [ $rc -ne 0 ] && { tail -5 gpurun_out/la.err; exit $rc; }
 timeout -k 10 200 python benchmarks/bench_fixed_cost.py > gpurun_out/fc.json 2> gpurun_out/fc.err
 rc=$?; echo "fixed cost: $(cat gpurun_out/fc.json)"; [ $rc -ne 0 ] && exit $rc
 for i in 1 2; do

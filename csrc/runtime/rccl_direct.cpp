@@ -653,12 +653,22 @@ void rccl_plan_set_views(int64_t plan, const std::vector<std::vector<int64_t>>& 
 // The whole direct sync of one metric in one call: a fresh result buffer like `src`, the
 // plan's grouped collectives (live buffer -> result, on the current stream), and the synced
 // states as views of the result buffer (plan order).  Returns [result, *views].
+std::vector<at::Tensor> plan_views(int64_t plan, const at::Tensor& dst);
+
 std::vector<at::Tensor> rccl_plan_sync(int64_t handle, int64_t plan, const at::Tensor& src, int64_t nranks) {
   at::Tensor dst = at::empty_like(src);
   rccl_plan_run(handle, plan, src, dst, nranks, false);
+  return plan_views(plan, dst);
+}
+
+// [dst, *views]: the plan's state views of a result buffer (no collectives; CPU-testable)
+std::vector<at::Tensor> plan_views(int64_t plan, const at::Tensor& dst) {
+  TORCH_CHECK(dst.scalar_type() == at::kByte && dst.is_contiguous() && dst.dim() == 1,
+              "rccl_plan_views: a contiguous 1-D uint8 buffer expected");
   const Plan* p;
   {
     std::lock_guard<std::mutex> lock(g_mu);
+    TORCH_CHECK(plan >= 0 && plan < static_cast<int64_t>(g_plans.size()), "rccl_plan_views: invalid plan ", plan);
     p = &g_plans[plan];
   }
   std::vector<at::Tensor> out;
@@ -671,7 +681,12 @@ std::vector<at::Tensor> rccl_plan_sync(int64_t handle, int64_t plan, const at::T
     if (!typed[key].defined()) typed[key] = dst.view(v.dtype);
     const at::Tensor& t = typed[key];
     std::vector<int64_t> strides(v.shape.size(), 1);
-    for (int64_t d = static_cast<int64_t>(v.shape.size()) - 2; d >= 0; --d) strides[d] = strides[d + 1] * v.shape[d + 1];
+    int64_t numel = 1;
+    for (int64_t d = static_cast<int64_t>(v.shape.size()) - 1; d >= 0; --d) {
+      strides[d] = numel;
+      numel *= v.shape[d];
+    }
+    TORCH_CHECK(v.elem_off + numel <= t.numel(), "rccl_plan_views: view outside the buffer");
     out.push_back(t.as_strided(v.shape, strides, v.elem_off));
   }
   return out;
@@ -740,6 +755,8 @@ void tea_register_rccl(pybind11::module_& m) {
   m.def("rccl_plan_sync", &rccl_plan_sync,
         "fresh result buffer + the plan's grouped collectives + the synced state views -> [result, *views]",
         py::arg("handle"), py::arg("plan"), py::arg("src"), py::arg("nranks"));
+  m.def("rccl_plan_views", &plan_views, "[buffer, *the plan's state views of it] (no collectives)",
+        py::arg("plan"), py::arg("dst"));
   m.def("rccl_group_start", &rccl_group_start, "ncclGroupStart");
   m.def("rccl_group_end", &rccl_group_end, "ncclGroupEnd (+ completion event of track_handle on device's stream)",
         py::arg("track_handle") = -1, py::arg("device") = 0);

@@ -381,27 +381,44 @@ class _Plan:
         # has no RCCL type: such metrics keep the gather path.
         self.rplan = None
         self.dassign = None
-        if self.comm is not None and all(g.dtype != torch.int16 for g in sb.groups):
-            ops = []
-            for g in sb.groups:
-                op = g.op if g.dtype != torch.bool else ("min" if g.op == "min" else "max")  # or / and
-                ops.append((0, g.off, g.off, g.nbytes // _esize(g.dtype), _DT_CODE[g.dtype], _OP_CODE[op]))
-            if sb.flag_words:
-                ops.append((0, sb.flag_off, sb.flag_off, sb.flag_words, _DT_CODE[torch.int32], _OP_CODE["max"]))
+        spec = direct_plan_spec(sb, cls) if self.comm is not None else None
+        if spec is not None:
+            ops, self.dassign = spec
             self.rplan = rccl_direct.plan_create(ops)
-            self.dassign = []
-            for g in sb.groups:
-                es = _esize(g.dtype)
-                for name, shape, boff, n in g.members:
-                    prop = isinstance(getattr(cls, name, None), property)
-                    self.dassign.append((name, g.dtype, (g.off + boff) // es, n, shape if shape else None, prop))
-            if sb.flag_words:
-                self.dassign.append(("_err", torch.int32, sb.flag_off // 4, sb.flag_words, (sb.flag_words,), False))
             # the synced states are built as views of the result buffer inside the same native
             # call (rccl_plan_sync): one pybind round trip instead of a Python view per state
-            rccl_direct.plan_set_views(self.rplan, [
-                [_DT_CODE[dt], eo, *(shape if shape is not None else ())] for _, dt, eo, _, shape, _ in self.dassign])
+            rccl_direct.plan_set_views(self.rplan, view_specs(self.dassign))
             self.dnames = [(name, prop) for name, _, _, _, _, prop in self.dassign]
+
+
+def direct_plan_spec(sb: StateBuffer, cls) -> Optional[Tuple[list, list]]:
+    """The direct-RCCL plan of a buffer layout: (collective ops, state assignments), or None
+    when a group has no RCCL type (int16).  Ops are ``(kind 0, src_off, dst_off, count, dtype
+    code, op code)``: every group and the error flag (int32 max) all-reduced from the live
+    buffer into the same offsets of a result buffer.  Assignments are ``(name, dtype, element
+    offset, numel, shape or None, is_property)``."""
+    if any(g.dtype == torch.int16 for g in sb.groups):
+        return None
+    ops = []
+    for g in sb.groups:
+        op = g.op if g.dtype != torch.bool else ("min" if g.op == "min" else "max")  # or / and
+        ops.append((0, g.off, g.off, g.nbytes // _esize(g.dtype), _DT_CODE[g.dtype], _OP_CODE[op]))
+    if sb.flag_words:
+        ops.append((0, sb.flag_off, sb.flag_off, sb.flag_words, _DT_CODE[torch.int32], _OP_CODE["max"]))
+    assign = []
+    for g in sb.groups:
+        es = _esize(g.dtype)
+        for name, shape, boff, n in g.members:
+            prop = isinstance(getattr(cls, name, None), property)
+            assign.append((name, g.dtype, (g.off + boff) // es, n, shape if shape else None, prop))
+    if sb.flag_words:
+        assign.append(("_err", torch.int32, sb.flag_off // 4, sb.flag_words, (sb.flag_words,), False))
+    return ops, assign
+
+
+def view_specs(assign) -> List[List[int]]:
+    """``[dtype code, element offset, *shape]`` per assignment (rccl_plan_set_views)."""
+    return [[_DT_CODE[dt], eo, *(shape if shape is not None else ())] for _, dt, eo, _, shape, _ in assign]
 
 
 def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
