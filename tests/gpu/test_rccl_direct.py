@@ -126,18 +126,22 @@ def test_collection_sync_matches_local(pg, monkeypatch, direct):
             assert torch.equal(g_, w)
 
 
-def test_async_sync_on_side_stream_snapshots_at_call(pg, monkeypatch):
+@pytest.mark.parametrize("side_stream", ["1", "0"])
+def test_async_sync_on_side_stream_snapshots_at_call(pg, monkeypatch, side_stream):
+    """Async sync: the opt-in side-stream direct path and the default general engine (one
+    communicator: torch.distributed's async collectives) both snapshot at the call."""
     from torcheval_amd.metrics.toolkit import get_synced_metric_async
     from torcheval_amd.parallel.state_buffer import FastPendingSync
 
     monkeypatch.setenv("TORCHEVAL_AMD_DIRECT_RCCL", "1")
+    monkeypatch.setenv("TORCHEVAL_AMD_ASYNC_DIRECT_RCCL", side_stream)
     acc, cm, bap = _metrics()
     coll = {"acc": acc, "cm": cm, "bap": bap}
     want = {k: m.compute() for k, m in coll.items()}
     g = torch.Generator(device=DEV).manual_seed(7)
     with collectives_at_world_size_1():
         fut = get_synced_metric_async(coll)
-        assert isinstance(fut._pending, FastPendingSync)
+        assert isinstance(fut._pending, FastPendingSync) == (side_stream == "1")
         for _ in range(20):  # the live metrics keep changing while the collectives run
             x = torch.randn(4096, 100, device=DEV, generator=g)
             y = torch.randint(0, 100, (4096,), device=DEV, generator=g)

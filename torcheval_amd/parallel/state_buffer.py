@@ -28,6 +28,7 @@ pickled metric, then ``merge_state`` on every rank).
 """
 
 import copy
+import os
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
@@ -774,7 +775,15 @@ class FastPendingSync:
 
 def start_fast_sync(metrics, group, ws: int) -> Optional[FastPendingSync]:
     """Async form of :func:`fast_sync`: snapshot now, collectives on the engine's side HIP
-    stream (direct RCCL), merge at ``finish()``.  None when not eligible."""
+    stream (direct RCCL), merge at ``finish()``.  None when not eligible.
+
+    Opt-in (``TORCHEVAL_AMD_ASYNC_DIRECT_RCCL=1``): the engine's own communicator then runs on a
+    second stream concurrently with whatever the process group runs (e.g. DDP's all-reduces),
+    and two communicators in flight at once can deadlock if ranks issue them in different
+    orders.  By default the async sync uses the general engine on torch.distributed's own
+    async collectives (still overlapped with ``update()``, one communicator)."""
+    if os.environ.get("TORCHEVAL_AMD_ASYNC_DIRECT_RCCL", "0") != "1":
+        return None
     issue = _fast_issue(metrics, group, ws, side=True)
     return None if issue is None else FastPendingSync(issue)
 
