@@ -137,7 +137,11 @@ def test_async_sync_on_side_stream_snapshots_at_call(pg, monkeypatch, side_strea
     monkeypatch.setenv("TORCHEVAL_AMD_ASYNC_DIRECT_RCCL", side_stream)
     acc, cm, bap = _metrics()
     coll = {"acc": acc, "cm": cm, "bap": bap}
-    want = {k: m.compute() for k, m in coll.items()}
+
+    def snap(v):  # compute() may hand out the live state (the reference's aliasing)
+        return tuple(x.clone() for x in v) if isinstance(v, tuple) else v.clone()
+
+    want = {k: snap(m.compute()) for k, m in coll.items()}
     g = torch.Generator(device=DEV).manual_seed(7)
     with collectives_at_world_size_1():
         fut = get_synced_metric_async(coll)

@@ -21,7 +21,7 @@ from torcheval_amd.metrics.metric import Metric, TComputeReturn
 from datetime import timedelta
 
 from torcheval_amd.parallel.collectives import skip_collectives, sync_timeout
-from torcheval_amd.parallel.distributed import PGWrapper
+from torcheval_amd.parallel.distributed import PGWrapper, cached_world_size
 from torcheval_amd.parallel.state_buffer import start_fast_sync
 from torcheval_amd.parallel.state_sync import (
     PendingSync,
@@ -101,7 +101,7 @@ def get_synced_metric_async(
     The result reflects the states at the time of this call (same on every rank).
     """
     single = isinstance(metric, Metric)
-    world_size = PGWrapper(process_group).get_world_size()
+    world_size = cached_world_size(process_group)
     _validate_rank_and_world_size(world_size)
     if skip_collectives(world_size):
         return SyncFuture(None, clone_metric(metric) if single else {k: clone_metric(m) for k, m in metric.items()}, single)
@@ -168,7 +168,7 @@ def get_synced_metric(
     ``process_group``.  With world size 1 the input metric itself is returned (reference
     toolkit.py:242-246 behaviour, with its warning).
     """
-    world_size = PGWrapper(process_group).get_world_size()
+    world_size = cached_world_size(process_group)
     _validate_rank_and_world_size(world_size)
     if skip_collectives(world_size):
         return metric
@@ -186,7 +186,7 @@ def get_synced_metric_collection(
     timeout: Optional[timedelta] = None,
 ) -> Union[Dict[str, Metric], MutableMapping[str, Metric]]:
     """Return a dict of metrics whose states are synced across the ranks (one batched exchange)."""
-    world_size = PGWrapper(process_group).get_world_size()
+    world_size = cached_world_size(process_group)
     _validate_rank_and_world_size(world_size)
     if skip_collectives(world_size):
         return metric_collection

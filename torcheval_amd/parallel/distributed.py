@@ -55,6 +55,23 @@ def get_world_size(pg: Optional[dist.ProcessGroup] = None) -> int:
     return PGWrapper(pg).get_world_size()
 
 
+_WS_CACHE: dict = {}  # id(group) -> (group, world size); a group's size never changes
+
+
+def cached_world_size(pg: Optional[dist.ProcessGroup] = None) -> int:
+    """``PGWrapper(pg).get_world_size()`` with the per-group size cached (the sync hot path:
+    torch's lookup walks the group registry on every call, ~3 us)."""
+    if not dist.is_available() or not dist.is_initialized():
+        return 1
+    g = pg if pg is not None else dist.group.WORLD
+    hit = _WS_CACHE.get(id(g))
+    if hit is not None and hit[0] is g:
+        return hit[1]
+    ws = dist.get_world_size(g)
+    _WS_CACHE[id(g)] = (g, ws)  # holds the group: its id cannot be reused while cached
+    return ws
+
+
 def get_rank(pg: Optional[dist.ProcessGroup] = None) -> int:
     return PGWrapper(pg).get_rank()
 
