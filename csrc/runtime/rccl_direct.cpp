@@ -115,6 +115,7 @@ struct Pending {
   hipEvent_t ev;
   int64_t handle;
   Clock::time_point deadline;
+  uint64_t seq;  // unique per tracked collective (events are pooled and reused)
 };
 
 // Process-lifetime state, never destroyed: a watchdog still running when static destructors
@@ -125,6 +126,7 @@ std::vector<std::unique_ptr<Comm>>& g_comms = *new std::vector<std::unique_ptr<C
 std::deque<Pending>& g_pending = *new std::deque<Pending>;
 std::vector<hipEvent_t>& g_event_pool = *new std::vector<hipEvent_t>;
 std::vector<int64_t>& g_abort_queue = *new std::vector<int64_t>;
+uint64_t g_seq = 0;  // under g_mu
 std::thread* g_watchdog = nullptr;  // leaked on purpose: joined by rccl_shutdown, never destroyed at exit
 bool g_stop = false;
 
@@ -268,7 +270,7 @@ void track(int64_t handle, hipStream_t stream) {
   TORCH_CHECK(hipEventRecord(ev, stream) == hipSuccess, "rccl_direct: hipEventRecord failed");
   std::lock_guard<std::mutex> lock(g_mu);
   Comm& c = comm_ref(handle);
-  g_pending.push_back({ev, handle, Clock::now() + std::chrono::milliseconds(c.timeout_ms)});
+  g_pending.push_back({ev, handle, Clock::now() + std::chrono::milliseconds(c.timeout_ms), ++g_seq});
   if (!g_watchdog) {
     g_stop = false;
     g_watchdog = new std::thread(watchdog_loop);
@@ -413,27 +415,27 @@ void rccl_comm_destroy(int64_t handle) {
 // timeout_ms.  false = deadline passed: the communicator is marked failed (observed, so no
 // teardown) and aborted in the background.
 bool rccl_wait(int64_t handle, int64_t timeout_ms) {
-  hipEvent_t ev = nullptr;
+  uint64_t seq = 0;
   {
     std::lock_guard<std::mutex> lock(g_mu);
     Comm& c = comm_ref(handle);
     TORCH_CHECK(c.state.load() == kOk, "rccl_direct: communicator ", handle, " is unusable (", c.reason, ")");
     for (auto it = g_pending.rbegin(); it != g_pending.rend(); ++it)
       if (it->handle == handle) {
-        ev = it->ev;
+        seq = it->seq;
         break;
       }
   }
-  if (!ev) return true;  // nothing in flight (the watchdog already retired it)
+  if (!seq) return true;  // nothing in flight (the watchdog already retired it)
   const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
   for (;;) {
     {
       std::lock_guard<std::mutex> lock(g_mu);
-      // still ours? (the watchdog may have retired it into the pool)
-      bool live = false;
+      // still pending? (the watchdog retires completed entries; their events are reused)
+      hipEvent_t ev = nullptr;
       for (const auto& p : g_pending)
-        if (p.ev == ev) live = true;
-      if (!live) return g_comms[handle]->state.load() == kOk;
+        if (p.seq == seq) ev = p.ev;
+      if (!ev) return g_comms[handle]->state.load() == kOk;
       const hipError_t q = hipEventQuery(ev);
       if (q == hipSuccess) return true;
       if (q != hipErrorNotReady || Clock::now() > deadline) {
