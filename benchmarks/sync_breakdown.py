@@ -70,6 +70,14 @@ def main() -> None:
                 res["plan_run"] = _t(lambda: rccl_direct.plan_run(plan.comm, plan.rplan, sb.buf, dst, 1))
                 res["merged_copy"] = _t(lambda: sbm._merged_copy(m, dst, plan.dassign))
                 res["device_copy_same_bytes"] = _t(lambda: dst.copy_(sb.buf))
+                os.environ["TORCHEVAL_AMD_RCCL_WATCHDOG"] = "0"  # A/B: no completion event
+                res["plan_run_no_watchdog"] = _t(lambda: rccl_direct.plan_run(plan.comm, plan.rplan, sb.buf, dst, 1))
+                res["get_synced_metric_no_watchdog"] = _t(lambda: get_synced_metric(m))
+                del os.environ["TORCHEVAL_AMD_RCCL_WATCHDOG"]
+                t8 = torch.zeros(2, device=dev)
+                res["raw_all_reduce_8B"] = _t(lambda: rccl_direct.all_reduce(plan.comm, t8, "sum"))
+                ev = torch.cuda.Event()
+                res["torch_event_record"] = _t(lambda: ev.record())
             if plan.src is not None and plan.rplan is None:
                 res["gather_only"] = _t(lambda: sbm._gather(plan, plan.src))
             if plan.large and plan.rplan is None:

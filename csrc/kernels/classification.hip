@@ -433,8 +433,8 @@ __global__ __launch_bounds__(kBlock) void cls_micro_kernel(ClsCountsArgs a) {
 // wave's first instructions wait on its kernel arguments, and with ClsCountsArgs (~200 B) and
 // in-kernel lane-mask arithmetic the generated code issued the kernarg loads in two dependent
 // rounds and ~60 scalar instructions before the first row load.  Here everything the row
-// loads need sits in the first 64 B (one s_load_dwordx16), and the ballot lane masks of the
-// tie check (a function of C only) are computed on the host (profiles/k1_floor_r4*.txt).
+// loads need sits in one 56-byte block (one scalar round trip) and the row test needs no lane
+// masks (profiles/k1_floor_r4*.txt).
 struct MicroPendArgs {
   const void* input;
   const void* target;
@@ -444,7 +444,6 @@ struct MicroPendArgs {
   int64_t row_stride;
   int32_t c;
   int32_t pad;
-  uint64_t lanes[kChunkLoads];  // per 16-B load of the chunk: lanes whose columns are < C
 };
 
 template <int KIND, typename TGT>
@@ -465,23 +464,26 @@ __device__ __forceinline__ bool micro_row(const MicroPendArgs& a, const char* __
   for (int u = 0; u < kChunkLoads; ++u)
 #pragma unroll
     for (int e = 0; e < VEC; ++e) v[u * VEC + e] = f[u][e];
+  // compare-only: no wave-wide max.  A column beats the target under torch.argmax's order if
+  // it is larger, or equal at a lower index (NaN rows take the exact path).  Lanes past C hold
+  // clamped copies of columns 0..VEC-1: real values of the row, so they cannot create a larger
+  // value, and their nominal column (>= C > t) keeps them out of the tie test.
   float m = fmaximum(v[0], v[1]);
 #pragma unroll
   for (int e = 2; e < NV; ++e) m = fmaximum(m, v[e]);
-  const float wm = wave_max_dpp(m);
-  if (__builtin_expect(wm != wm, 0)) return row_argmax_exact<KIND>(rp, C, lane) == t;  // NaN row
+  if (__builtin_expect(__ballot(m != m) != 0, 0)) return row_argmax_exact<KIND>(rp, C, lane) == t;  // NaN
   if (!(t >= 0 && t < C)) return false;
   const int tu = static_cast<int>(t);
   const float sel = v[(tu / STEP) * VEC + (tu % VEC)];  // uniform index: one indexed move
   const float xt = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(sel), (tu % STEP) / VEC));
-  if (xt != wm) return false;
-  // the target holds the max: correct iff it is the only column that does
-  int cnt = 0;
+  if (__ballot(m > xt) != 0) return false;  // a larger column somewhere: the common incorrect row
+  // the target holds the row max: correct iff no column before it ties it (first index wins)
+  bool tie = false;
 #pragma unroll
   for (int u = 0; u < kChunkLoads; ++u)
 #pragma unroll
-    for (int e = 0; e < VEC; ++e) cnt += __builtin_popcountll(__ballot(v[u * VEC + e] == wm) & a.lanes[u]);
-  return cnt == 1 || row_argmax_exact<KIND>(rp, C, lane) == t;
+    for (int e = 0; e < VEC; ++e) tie |= (v[u * VEC + e] == xt) & (u * STEP + lane * VEC + e < tu);  // no branches
+  return __ballot(tie) == 0;
 }
 
 template <int KIND, typename TGT>
@@ -659,12 +661,7 @@ void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
   const bool micro_only = micro_on && pred_free && VEC > 1 && a.k == 1 && a.cls_correct == nullptr &&
                           a.cls_label == nullptr && a.err == nullptr && a.err_max == nullptr && !a.check_target;
   if (micro_only && a.pend && (a.tg_dt == DType::i64 || a.tg_dt == DType::i32)) {
-    MicroPendArgs m{a.input, a.target, a.pend, a.micro_total, a.n, a.row_stride, static_cast<int32_t>(a.c), 0, {}};
-    constexpr int kStep = kWave * VEC;
-    for (int u = 0; u < kChunkLoads; ++u) {
-      const int64_t valid = std::min<int64_t>(std::max<int64_t>((a.c - u * kStep + VEC - 1) / VEC, 0), kWave);
-      m.lanes[u] = valid >= kWave ? ~0ull : ((1ull << valid) - 1);
-    }
+    const MicroPendArgs m{a.input, a.target, a.pend, a.micro_total, a.n, a.row_stride, static_cast<int32_t>(a.c), 0};
     if (a.tg_dt == DType::i64)
       hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t>), dim3(grid), dim3(kBlock), 0, s, m);
     else

@@ -109,6 +109,13 @@ struct Comm {
   bool observed = false;  // a blocking waiter reported the failure itself (no teardown)
   bool teardown = false;  // decided when the failure is detected (env read then, not at abort)
   std::string reason;
+  // completion tracking (under g_mu): one probe event in flight per communicator.  Collectives
+  // enqueued while a probe is pending are counted; when the probe retires, the watchdog records
+  // a follow-up probe behind them on their stream (hipEventRecord costs ~5 us of host time, so
+  // a burst of syncs pays it once, not per sync)
+  int probes = 0;
+  uint64_t untracked = 0;
+  hipStream_t last_stream = nullptr;
 };
 
 struct Pending {
@@ -182,6 +189,8 @@ void abort_comm(int64_t handle) {
     std::lock_guard<std::mutex> lock(g_mu);
     Comm& c = *g_comms[handle];
     c.state.store(kAborted);
+    c.probes = 0;
+    c.untracked = 0;
     teardown = c.teardown;
     why = c.reason;
     // the aborted collectives' events complete once the stream drains; drop them unqueried
@@ -207,8 +216,55 @@ void abort_comm(int64_t handle) {
   }
 }
 
+bool watchdog_enabled();
+void watchdog_loop();
+
+// a probe event from the pool (or a new one); caller does NOT hold g_mu
+hipEvent_t take_event() {
+  hipEvent_t ev = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    if (!g_event_pool.empty()) {
+      ev = g_event_pool.back();
+      g_event_pool.pop_back();
+    }
+  }
+  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
+  return ev;
+}
+
+// record a probe for `handle` on `stream` and queue it (caller does NOT hold g_mu and has
+// already counted it in c.probes); false when the record failed (count undone)
+bool record_probe(int64_t handle, hipStream_t stream) {
+  hipEvent_t ev = take_event();
+  const bool ok = ev && hipEventRecord(ev, stream) == hipSuccess;
+  std::lock_guard<std::mutex> lock(g_mu);
+  Comm& c = *g_comms[handle];
+  if (!ok) {
+    --c.probes;
+    if (ev) g_event_pool.push_back(ev);
+    return false;
+  }
+  g_pending.push_back({ev, handle, Clock::now() + std::chrono::milliseconds(c.timeout_ms), ++g_seq});
+  if (!g_watchdog) {
+    g_stop = false;
+    g_watchdog = new std::thread(watchdog_loop);
+  }
+  g_cv.notify_all();
+  return true;
+}
+
 void watchdog_loop() {
   auto last_async_poll = Clock::now();
+  struct Probe {
+    uint64_t seq;
+    hipEvent_t ev;
+    int64_t handle;
+    Clock::time_point deadline;
+    hipError_t q;
+  };
+  std::vector<Probe> batch;
+  std::vector<std::pair<int64_t, hipStream_t>> follow_ups;
   std::unique_lock<std::mutex> lk(g_mu);
   while (!g_stop) {
     if (!g_abort_queue.empty()) {
@@ -223,24 +279,65 @@ void watchdog_loop() {
       g_cv.wait_for(lk, std::chrono::milliseconds(200));
       continue;
     }
+    // query a snapshot of the oldest probes WITHOUT the lock (hipEventQuery takes the runtime's
+    // own locks; holding g_mu here stalled every sync's enqueue behind the scan)
+    batch.clear();
+    for (const auto& p : g_pending) {
+      batch.push_back({p.seq, p.ev, p.handle, p.deadline, hipSuccess});
+      if (batch.size() >= 64) break;
+    }
+    lk.unlock();
+    for (auto& b : batch) b.q = hipEventQuery(b.ev);
     const auto now = Clock::now();
-    for (auto it = g_pending.begin(); it != g_pending.end();) {
-      const hipError_t q = hipEventQuery(it->ev);
-      if (q == hipSuccess) {
+    lk.lock();
+    follow_ups.clear();
+    for (const auto& b : batch) {
+      auto it = g_pending.begin();
+      while (it != g_pending.end() && it->seq != b.seq) ++it;
+      if (it == g_pending.end()) continue;  // retired meanwhile (destroy / abort)
+      Comm& c = *g_comms[b.handle];
+      if (b.q == hipSuccess) {
         g_event_pool.push_back(it->ev);
-        it = g_pending.erase(it);
+        g_pending.erase(it);
+        --c.probes;
+        if (c.state.load() == kOk && c.probes == 0 && c.untracked > 0 && c.last_stream) {
+          // collectives enqueued behind the retired probe: probe them now
+          c.untracked = 0;
+          ++c.probes;
+          follow_ups.emplace_back(b.handle, c.last_stream);
+        }
         continue;
       }
-      Comm& c = *g_comms[it->handle];
       if (c.state.load() == kOk) {
-        if (q != hipErrorNotReady) {
-          mark_failed_locked(it->handle, std::string("completion query failed: ") + hipGetErrorString(q), false);
-        } else if (now > it->deadline) {
-          mark_failed_locked(it->handle,
+        if (b.q != hipErrorNotReady) {
+          mark_failed_locked(b.handle, std::string("completion query failed: ") + hipGetErrorString(b.q), false);
+        } else if (now > b.deadline) {
+          mark_failed_locked(b.handle,
                              "a collective did not complete within " + std::to_string(c.timeout_ms) + " ms", false);
         }
       }
-      ++it;
+    }
+    if (!follow_ups.empty()) {
+      lk.unlock();
+      for (const auto& fu : follow_ups) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        int dev = 0;
+        {
+          std::lock_guard<std::mutex> lock(g_mu);
+          dev = g_comms[fu.first]->device;
+        }
+        (void)hipSetDevice(dev);
+        // never insert into a stream that is being captured into a graph
+        const bool capturing = hipStreamIsCapturing(fu.second, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+        const bool ok = !capturing && record_probe(fu.first, fu.second);  // a failed record undoes its count
+        if (!ok) {
+          std::lock_guard<std::mutex> lock(g_mu);
+          Comm& c = *g_comms[fu.first];
+          if (capturing) --c.probes;
+          ++c.untracked;  // probed at the next sync of this communicator
+        }
+      }
+      lk.lock();
     }
     if (now - last_async_poll > std::chrono::milliseconds(10)) {
       last_async_poll = now;
@@ -256,26 +353,29 @@ void watchdog_loop() {
   }
 }
 
-// record a completion event for `handle` on `stream` (caller does NOT hold g_mu)
-void track(int64_t handle, hipStream_t stream) {
-  hipEvent_t ev = nullptr;
+// TORCHEVAL_AMD_RCCL_WATCHDOG=0: no completion events (no deadlines; A/B of the tracking cost)
+bool watchdog_enabled() {
+  const char* e = std::getenv("TORCHEVAL_AMD_RCCL_WATCHDOG");
+  return !(e && std::strcmp(e, "0") == 0);
+}
+
+// completion tracking of a collective just enqueued for `handle` on `stream` (caller does NOT
+// hold g_mu): a probe event when none is in flight, else counted for the watchdog's follow-up
+// probe.  `force`: always record (a host waiter needs this collective's own completion).
+void track(int64_t handle, hipStream_t stream, bool force = false) {
+  if (!watchdog_enabled() && !force) return;
   {
     std::lock_guard<std::mutex> lock(g_mu);
-    if (!g_event_pool.empty()) {
-      ev = g_event_pool.back();
-      g_event_pool.pop_back();
+    Comm& c = comm_ref(handle);
+    c.last_stream = stream;
+    if (c.probes > 0 && !force) {
+      ++c.untracked;
+      return;
     }
+    ++c.probes;
+    if (force) c.untracked = 0;  // the forced probe covers everything before it on the stream
   }
-  if (!ev) TORCH_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess, "rccl_direct: event");
-  TORCH_CHECK(hipEventRecord(ev, stream) == hipSuccess, "rccl_direct: hipEventRecord failed");
-  std::lock_guard<std::mutex> lock(g_mu);
-  Comm& c = comm_ref(handle);
-  g_pending.push_back({ev, handle, Clock::now() + std::chrono::milliseconds(c.timeout_ms), ++g_seq});
-  if (!g_watchdog) {
-    g_stop = false;
-    g_watchdog = new std::thread(watchdog_loop);
-  }
-  g_cv.notify_all();
+  TORCH_CHECK(record_probe(handle, stream), "rccl_direct: hipEventRecord failed");
 }
 
 ncclDataType_t dtype_of(const at::Tensor& t) {
@@ -367,6 +467,14 @@ bool rccl_wait_aborted(int64_t handle, int64_t timeout_ms) {
 void rccl_comm_destroy(int64_t handle) {
   ncclComm_t comm;
   int device;
+  hipStream_t s_untracked = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    if (handle >= 0 && handle < static_cast<int64_t>(g_comms.size()) && g_comms[handle] &&
+        g_comms[handle]->state.load() == kOk && g_comms[handle]->untracked > 0)
+      s_untracked = g_comms[handle]->last_stream;
+  }
+  if (s_untracked) track(handle, s_untracked, true);  // drain-check every collective, tracked or not
   {
     std::lock_guard<std::mutex> lock(g_mu);
     if (handle < 0 || handle >= static_cast<int64_t>(g_comms.size()) || !g_comms[handle]) return;
@@ -416,10 +524,16 @@ void rccl_comm_destroy(int64_t handle) {
 // teardown) and aborted in the background.
 bool rccl_wait(int64_t handle, int64_t timeout_ms) {
   uint64_t seq = 0;
+  hipStream_t s_untracked = nullptr;
   {
     std::lock_guard<std::mutex> lock(g_mu);
     Comm& c = comm_ref(handle);
     TORCH_CHECK(c.state.load() == kOk, "rccl_direct: communicator ", handle, " is unusable (", c.reason, ")");
+    if (c.untracked > 0) s_untracked = c.last_stream;
+  }
+  if (s_untracked) track(handle, s_untracked, true);  // the newest collective gets its own probe
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
     for (auto it = g_pending.rbegin(); it != g_pending.rend(); ++it)
       if (it->handle == handle) {
         seq = it->seq;
@@ -608,7 +722,10 @@ void rccl_plan_run(int64_t handle, int64_t plan, const at::Tensor& src, const at
   const ncclComm_t comm = usable_comm(handle);
   const uint8_t* sp = src.data_ptr<uint8_t>();
   uint8_t* dp = dst.data_ptr<uint8_t>();
-  check(api().group_start(), "ncclGroupStart");
+  // a one-operand plan (e.g. MulticlassAccuracy's counters) needs no group: its ncclGroupEnd
+  // launch bookkeeping is pure host cost
+  const bool group = p->ops.size() > 1;
+  if (group) check(api().group_start(), "ncclGroupStart");
   ncclResult_t rc = ncclSuccess;
   for (const auto& q : p->ops) {
     rc = q.kind == 0 ? api().all_reduce(sp + q.src_off, dp + q.dst_off, static_cast<size_t>(q.count), q.dt, q.op,
@@ -617,7 +734,7 @@ void rccl_plan_run(int64_t handle, int64_t plan, const at::Tensor& src, const at
                                         comm, s);
     if (rc != ncclSuccess) break;
   }
-  const ncclResult_t rc_end = api().group_end();
+  const ncclResult_t rc_end = group ? api().group_end() : ncclSuccess;
   check(rc, "sync plan collective");
   check(rc_end, "ncclGroupEnd");
   if (!grouped) track(handle, s);
