@@ -586,8 +586,16 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   unsigned long long* slots = a.slots;
   unsigned* ctl = a.ctl;
   void* args[] = {&A, &n, &R, &ld, &d, &e, &slots, &ctl};
-  if (hipLaunchCooperativeKernel(kern, dim3(G), dim3(kThreads), args, 0, stream) != hipSuccess)
-    return 3;
+  // TORCHEVAL_AMD_SYMEIG_COOP=0: a plain launch of the same grid (A/B of the cooperative
+  // launch's process-exit behaviour under rocprofv3; G <= #CUs workgroups are co-resident in
+  // practice and the bounded hand-off spins abort to the library fallback if they are not)
+  static const bool coop = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_COOP");
+    return !(e && e[0] == '0');
+  }();
+  const hipError_t lrc = coop ? hipLaunchCooperativeKernel(kern, dim3(G), dim3(kThreads), args, 0, stream)
+                              : hipLaunchKernel(kern, dim3(G), dim3(kThreads), args, 0, stream);
+  if (lrc != hipSuccess) return 3;
   sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
   if (n >= 1536)
     tridiag_eigvals_kernel<16><<<(n + kWaves * 4 - 1) / (kWaves * 4), kThreads, 0, stream>>>(d, e, n, a.grid, a.lam);
