@@ -113,6 +113,47 @@ def test_k7_strided_rows_and_class():
     assert float(m.compute()) == pytest.approx(ref, rel=2e-5)
 
 
+@pytest.mark.parametrize("vocab", [4096, 4112, 8192, 12288, 12304])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_k7_long_row_chunk_edges(vocab, dtype):
+    """Long rows stream in 1024-value wave-wide chunks: rows of exactly 4, 8 and 12 chunks and of
+    4 and 12 chunks plus a 16-value tail, with the max in the last chunk of one row."""
+    g = torch.Generator().manual_seed(vocab + 7)
+    x = (torch.randn(3, 11, vocab, generator=g) * 4).to(dtype)
+    x[0, 0, vocab - 1] = 40.0  # the max sits in the last chunk of one row
+    t = torch.randint(0, vocab, (3, 11), generator=g)
+    t[0, 0] = vocab - 1
+    got = float(perplexity(x.to(DEV), t.to(DEV)))
+    assert got == pytest.approx(_ppl_ref(x, t), rel=2e-5)
+    ign = int(t[1, 3])
+    got_i = float(perplexity(x.to(DEV), t.to(DEV), ignore_index=ign))
+    assert got_i == pytest.approx(_ppl_ref(x, t, ign), rel=2e-5)
+
+
+def test_k7_many_long_rows_strided_and_deterministic():
+    from torcheval_amd.config import flags
+
+    g = torch.Generator().manual_seed(11)
+    big = torch.randn(2, 4100, 4096 + 32, generator=g)  # grid-stride: more rows than waves in the grid
+    x = big[..., :4096]  # row stride != vocab
+    t = torch.randint(0, 4096, (2, 4100), generator=g)
+    ref = _ppl_ref(x, t)
+    xd, td = x.to(DEV), t.to(DEV)
+    got = float(perplexity(xd, td))
+    assert got == pytest.approx(ref, rel=2e-5)
+    with flags(deterministic=True):
+        a = perplexity(xd, td)
+        b = perplexity(xd, td)
+    assert float(a) == pytest.approx(ref, rel=2e-5)
+    assert torch.equal(a, b)
+
+
+def test_k7_long_row_invalid_target_raises():
+    x = torch.randn(2, 2, 4096, device=DEV)
+    with pytest.raises(ValueError, match="vocab_size minus one"):
+        perplexity(x, torch.tensor([[1, 4096], [0, 3]], device=DEV))
+
+
 def test_k7_invalid_target_raises():
     with pytest.raises(ValueError, match="vocab_size minus one"):
         perplexity(torch.rand(3, 2, 3, device=DEV), torch.tensor([[4, 2], [1, 0], [0, 0]], device=DEV))
