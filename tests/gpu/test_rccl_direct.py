@@ -60,6 +60,7 @@ def test_primitives(pg):
     torch.ops.torcheval_amd.rccl_all_gather(h, src, out)
     torch.ops.torcheval_amd.rccl_all_reduce(h, t, 0)
     torch.cuda.synchronize()
+    assert rccl_direct._self_check(h, 1, 0, torch.device(DEV))  # the ws > 1 bootstrap check's calls
 
 
 def test_accuracy_plan_uses_one_all_reduce(pg):

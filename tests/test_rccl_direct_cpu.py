@@ -159,3 +159,34 @@ def test_int16_layouts_keep_the_gather_path():
             return self
 
     assert sbm.direct_plan_spec(sbm.buffer_of(Short()), Short) is None
+
+
+class _FakeRccl:
+    """Stands in for the native all-reduce / all-gather of a ws-rank group as seen from one rank."""
+
+    def __init__(self, ws, others, shift=0):
+        self.ws, self.others, self.shift = ws, others, shift
+
+    def rccl_all_reduce(self, handle, send, op, out):
+        out.copy_(send + self.others)
+
+    def rccl_all_gather(self, handle, src, dst):
+        dst.copy_(torch.roll(torch.arange(1, self.ws + 1, dtype=torch.int32), self.shift))
+
+
+@pytest.mark.parametrize("ws,rank", [(2, 0), (4, 3), (8, 5)])
+def test_direct_comm_bootstrap_self_check(monkeypatch, ws, rank):
+    import torcheval_amd.ops as ops
+    from torcheval_amd.parallel import rccl_direct
+
+    # what the other ranks contribute: sum over r != rank of [r + 1, ws - r]
+    others = torch.tensor([sum(r + 1 for r in range(ws) if r != rank), sum(ws - r for r in range(ws) if r != rank)],
+                          dtype=torch.int32)
+    monkeypatch.setattr(ops, "native", lambda: _FakeRccl(ws, others))
+    assert rccl_direct._self_check(1, ws, rank, torch.device("cpu"))
+    monkeypatch.setattr(ops, "native", lambda: _FakeRccl(ws, others, shift=1))  # rank order mismatch
+    with pytest.warns(UserWarning, match="bootstrap check"):
+        assert not rccl_direct._self_check(1, ws, rank, torch.device("cpu"))
+    monkeypatch.setattr(ops, "native", lambda: _FakeRccl(ws, others + 1))  # wrong reduction
+    with pytest.warns(UserWarning, match="bootstrap check"):
+        assert not rccl_direct._self_check(1, ws, rank, torch.device("cpu"))

@@ -102,6 +102,9 @@ def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
             uid, ws, rank, device.index if device.index is not None else 0, _ms(group_timeout(group, device))))
     except RuntimeError:
         handle = None
+    if ws > 1 and handle is not None and not _self_check(handle, ws, rank, device):
+        native().rccl_comm_destroy(handle)
+        handle = None
     if ws > 1:
         # every rank must take the same path: one failed init sends the whole group back to
         # torch.distributed (a rank-dependent choice would pair a direct collective with a
@@ -113,6 +116,31 @@ def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
             handle = None
     _COMMS[id(group)] = (group, ws, handle)
     return handle
+
+
+def _self_check(handle: int, ws: int, rank: int, device: torch.device) -> bool:
+    """One-time bootstrap check of a new multi-rank communicator: an out-of-place all-reduce
+    and an all-gather whose results every rank can predict.  A communicator that does not
+    reproduce them (a rank bound to the wrong device, a mismatched rank order) is dropped and
+    the group stays on torch.distributed - the caller's MIN vote makes that choice collective."""
+    from torcheval_amd.ops import native
+
+    try:
+        send = torch.tensor([rank + 1, ws - rank], dtype=torch.int32, device=device)
+        red = torch.empty_like(send)
+        native().rccl_all_reduce(handle, send, _OPS["sum"], red)
+        gat = torch.empty(ws, dtype=torch.int32, device=device)
+        native().rccl_all_gather(handle, send[:1], gat)
+        want = ws * (ws + 1) // 2
+        ok = red.tolist() == [want, want] and gat.tolist() == list(range(1, ws + 1))
+    except RuntimeError:
+        return False
+    if not ok:
+        import warnings
+
+        warnings.warn(f"torcheval_amd: the direct RCCL communicator failed its bootstrap check on rank {rank} "
+                      "(all-reduce / all-gather results differ); syncs use torch.distributed", stacklevel=3)
+    return ok
 
 
 def forget(handle: int) -> None:
