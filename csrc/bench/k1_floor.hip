@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -240,5 +241,37 @@ int main(int argc, char** argv) {
     printf("{\"variant\": \"%s\", \"pool\": %d, \"us_per_launch\": %.3f, \"TBps\": %.2f}\n", names[v], POOL, best[v],
            v != 2 ? bytes / (best[v] * 1e-6) / 1e12 : 0.0);
   printf("{\"prod_over_floor\": %.4f}\n", best[0] / best[1]);
+
+  // Host side: the host cost of one production launch with no Python in
+  // front of it, and bench.py's timed region (synchronize, t0, 20 updates, the micro_finish
+  // fold, synchronize, t1) driven from C++: what the region costs with a zero-overhead caller.
+  float* acc_out;
+  CK(hipMalloc(&acc_out, 4));
+  std::vector<double> enq, region1, region20;
+  for (int rep = 0; rep < 41; ++rep) {
+    CK(hipDeviceSynchronize());
+    auto t0 = std::chrono::steady_clock::now();
+    for (int i = 0; i < 20; ++i) prod(i);
+    auto t1 = std::chrono::steady_clock::now();
+    enq.push_back(std::chrono::duration<double, std::micro>(t1 - t0).count() / 20);
+    CK(hipDeviceSynchronize());
+    for (int n : {1, 20}) {
+      for (int i = 0; i < 5; ++i) prod(i);  // bench.py's warmup right before the region
+      CK(hipDeviceSynchronize());
+      auto r0 = std::chrono::steady_clock::now();
+      for (int i = 0; i < n; ++i) prod(i);
+      launch_micro_finish(pend, correct, total, acc_out, 0);
+      CK(hipDeviceSynchronize());
+      auto r1 = std::chrono::steady_clock::now();
+      (n == 1 ? region1 : region20).push_back(std::chrono::duration<double, std::micro>(r1 - r0).count());
+    }
+  }
+  auto med = [](std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  printf("{\"host_us_per_launch\": %.3f, \"region_1_us\": %.2f, \"region_20_us\": %.2f, "
+         "\"updates_per_s_at_20\": %.0f}\n",
+         med(enq), med(region1), med(region20), 20.0 / med(region20) * 1e6);
   return 0;
 }
