@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <tuple>
 #include <vector>
 
 #include "tea_runtime.h"
@@ -309,9 +310,96 @@ void cpu_binned_counts(const at::Tensor& scores, const at::Tensor& target, const
   }
 }
 
+// ---- tie-aware binary AUROC / AUPRC rows (host twin of the K3 sort-scan, _curve.py) ----
+
+// row r of a [rows, n] tensor (any strides) widened to double
+void row_as_double(const at::Tensor& t, int64_t r, std::vector<double>& out) {
+  const int64_t n = t.size(1), s0 = t.stride(0), s1 = t.stride(1);
+  out.resize(n);
+  switch (t.scalar_type()) {
+#define TEA_ROW(ST, CT)                                                          \
+  case ST: {                                                                     \
+    const CT* p = t.data_ptr<CT>() + r * s0;                                     \
+    for (int64_t i = 0; i < n; ++i) out[i] = static_cast<double>(p[i * s1]);   \
+    break;                                                                       \
+  }
+    TEA_ROW(at::kFloat, float)
+    TEA_ROW(at::kDouble, double)
+    TEA_ROW(at::kLong, int64_t)
+    TEA_ROW(at::kInt, int32_t)
+    TEA_ROW(at::kByte, uint8_t)
+    TEA_ROW(at::kBool, bool)
+#undef TEA_ROW
+    default: TORCH_CHECK(false, "cpu_binary_auc: unsupported dtype ", t.scalar_type());
+  }
+}
+
+template <typename S>
+void auc_row(const S* x, int64_t n, int64_t sx, const std::vector<double>& t, const std::vector<double>* w,
+             std::vector<int64_t>& idx, double& roc_out, double& pr_out) {
+  idx.resize(n);
+  for (int64_t i = 0; i < n; ++i) idx[i] = i;
+  // torch.sort(descending=True) order: NaN above everything; ties in any order (only the
+  // tie-group ends are used)
+  std::sort(idx.begin(), idx.end(), [&](int64_t i, int64_t j) {
+    const S a = x[i * sx], b = x[j * sx];
+    if (std::isnan(static_cast<double>(a))) return !std::isnan(static_cast<double>(b));
+    if (std::isnan(static_cast<double>(b))) return false;
+    return a > b;
+  });
+  double tp = 0.0, fp = 0.0, tp0 = 0.0, fp0 = 0.0, roc = 0.0, pr = 0.0;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = idx[k];
+    const double wi = w ? (*w)[i] : 1.0;
+    tp += wi * t[i];
+    fp += wi * (1.0 - t[i]);
+    // a group ends where the next sorted score differs (NaN != NaN: every NaN ends its own)
+    if (k + 1 < n && x[idx[k + 1] * sx] == x[i * sx]) continue;
+    roc += (fp - fp0) * (tp + tp0);
+    const double den = tp + fp;
+    pr += (tp - tp0) * (den > 0 ? tp / den : 0.0);
+    tp0 = tp;
+    fp0 = fp;
+  }
+  roc /= 2;
+  roc_out = tp * fp == 0.0 ? 0.5 : roc / (tp * fp);
+  pr_out = tp == 0.0 ? 0.0 : pr / tp;
+}
+
+// x [rows, n] float32 / float64 scores, t [rows, n] targets, w optional [rows, n] weights ->
+// (roc, pr) float64 [rows]: AUROC (0.5 when a row has no positives or no negatives) and AUPRC
+// (0 without positives) with the reference's tie semantics
+std::tuple<at::Tensor, at::Tensor> cpu_binary_auc(const at::Tensor& x, const at::Tensor& t,
+                                                  const c10::optional<at::Tensor>& w) {
+  TORCH_CHECK(!x.is_cuda() && !t.is_cuda() && (!w.has_value() || !w->is_cuda()), "cpu_binary_auc: CPU tensors");
+  TORCH_CHECK(x.dim() == 2 && t.sizes() == x.sizes() && (!w.has_value() || w->sizes() == x.sizes()),
+              "cpu_binary_auc: x, t (and w) [rows, n]");
+  const int64_t rows = x.size(0), n = x.size(1);
+  const auto f64 = at::TensorOptions().dtype(at::kDouble);
+  at::Tensor roc = at::empty({rows}, f64), pr = at::empty({rows}, f64);
+  double* pr_ = pr.data_ptr<double>();
+  double* roc_ = roc.data_ptr<double>();
+  std::vector<double> tv, wv;
+  std::vector<int64_t> idx;
+  for (int64_t r = 0; r < rows; ++r) {
+    row_as_double(t, r, tv);
+    if (w.has_value()) row_as_double(*w, r, wv);
+    const std::vector<double>* wp = w.has_value() ? &wv : nullptr;
+    if (x.scalar_type() == at::kFloat)
+      auc_row(x.data_ptr<float>() + r * x.stride(0), n, x.stride(1), tv, wp, idx, roc_[r], pr_[r]);
+    else if (x.scalar_type() == at::kDouble)
+      auc_row(x.data_ptr<double>() + r * x.stride(0), n, x.stride(1), tv, wp, idx, roc_[r], pr_[r]);
+    else
+      TORCH_CHECK(false, "cpu_binary_auc: float32 / float64 scores");
+  }
+  return {roc, pr};
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
+  m.def("cpu_binary_auc", &cpu_binary_auc, "host twin of the K3 AUROC / AUPRC rows for small CPU batches",
+        pybind11::arg("x"), pybind11::arg("t"), pybind11::arg("w") = pybind11::none());
   m.def("cpu_binned_counts", &cpu_binned_counts, "host twin of binned_counts for small CPU batches");
   m.def("cpu_labels_valid", &cpu_labels_valid, "all targets / label predictions in [0, num_classes)");
   m.def("cpu_cls_counts", &cpu_cls_counts, "host twin of cls_counts for small CPU batches");

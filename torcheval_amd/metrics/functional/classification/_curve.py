@@ -14,7 +14,7 @@ from typing import List, Optional, Tuple
 import torch
 import torch.nn.functional as F
 
-from torcheval_amd.ops import native_loaded, use_native
+from torcheval_amd.ops import compiling, native_loaded, use_native
 
 
 def _group_ends(s: torch.Tensor) -> torch.Tensor:
@@ -96,6 +96,13 @@ def binary_areas(
         from torcheval_amd.ops.sortscan import binary_auc
 
         return binary_auc(x, t, w, roc=roc, pr=pr)
+    if _cpu_auc_ok(x, t, w):
+        # small CPU batches: one C++ pass per row (sort + tie-group scan) instead of ~15 ATen
+        # dispatches per row
+        from torcheval_amd.ops import native
+
+        r_, p_ = native().cpu_binary_auc(x, t, w)
+        return (r_ if roc else None, p_ if pr else None)
     rocs, prs = [], []
     s, a, b = _sorted_ab(x.to(torch.float64) if x.dtype in (torch.float16, torch.bfloat16) else x, t, w)
     for r in range(s.shape[0]):
@@ -106,6 +113,23 @@ def binary_areas(
         prs.append(ap)
     dev = x.device
     return (torch.stack(rocs).to(dev) if roc else None, torch.stack(prs).to(dev) if pr else None)
+
+
+_CPU_AUC_MAX = 1 << 16
+_CPU_AUC_TARGETS = (torch.bool, torch.uint8, torch.int32, torch.int64, torch.float32, torch.float64)
+
+
+def _cpu_auc_ok(x: torch.Tensor, t: torch.Tensor, w: Optional[torch.Tensor]) -> bool:
+    return (
+        not x.is_cuda
+        and x.device.type == "cpu"
+        and x.numel() <= _CPU_AUC_MAX
+        and x.dtype in (torch.float32, torch.float64)
+        and t.dtype in _CPU_AUC_TARGETS
+        and (w is None or w.dtype in (torch.float32, torch.float64))
+        and not compiling()
+        and native_loaded()
+    )
 
 
 def multiclass_areas(
