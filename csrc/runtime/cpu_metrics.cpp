@@ -395,9 +395,58 @@ std::tuple<at::Tensor, at::Tensor> cpu_binary_auc(const at::Tensor& x, const at:
   return {roc, pr};
 }
 
+// ---- binary accuracy (host twin of binary_counts' accuracy contract) ----
+
+template <typename S>
+int64_t count_binary_correct(const S* x, int64_t n, int64_t sx, const at::Tensor& target, S thr) {
+  std::vector<double> tv;
+  row_as_double(target.unsqueeze(0), 0, tv);
+  int64_t correct = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    // torch.where(input < threshold, 0, 1) with the threshold in the input's dtype (NaN -> 1)
+    const double pred = x[i * sx] < thr ? 0.0 : 1.0;
+    correct += (pred == tv[i]);
+  }
+  return correct;
+}
+
+int64_t count_binary(const at::Tensor& input, const at::Tensor& target, double threshold) {
+  TORCH_CHECK(!input.is_cuda() && !target.is_cuda() && input.dim() == 1 && target.dim() == 1 &&
+                  input.size(0) == target.size(0), "cpu_binary_accuracy: CPU [N] input and target");
+  const int64_t n = input.size(0);
+  if (input.scalar_type() == at::kFloat)
+    return count_binary_correct(input.data_ptr<float>(), n, input.stride(0), target, static_cast<float>(threshold));
+  TORCH_CHECK(input.scalar_type() == at::kDouble, "cpu_binary_accuracy: float32 / float64 input");
+  return count_binary_correct(input.data_ptr<double>(), n, input.stride(0), target, threshold);
+}
+
+// functional: 0-d float32 accuracy (NaN for an empty batch, like 0 / 0)
+at::Tensor cpu_binary_accuracy(const at::Tensor& input, const at::Tensor& target, double threshold) {
+  const int64_t c = count_binary(input, target, threshold);
+  at::Tensor out = at::empty({}, at::TensorOptions().dtype(at::kFloat));
+  out.data_ptr<float>()[0] = static_cast<float>(c) / static_cast<float>(target.size(0));
+  return out;
+}
+
+// class update: 0-d float32 states += (correct, N)
+void cpu_binary_accuracy_update(const at::Tensor& input, const at::Tensor& target, double threshold,
+                                at::Tensor& correct, at::Tensor& total) {
+  TORCH_CHECK(correct.dim() == 0 && total.dim() == 0 && correct.scalar_type() == at::kFloat &&
+                  total.scalar_type() == at::kFloat && !correct.is_cuda() && !total.is_cuda(),
+              "cpu_binary_accuracy_update: 0-d float32 CPU states");
+  const int64_t c = count_binary(input, target, threshold);
+  correct.data_ptr<float>()[0] += static_cast<float>(c);
+  total.data_ptr<float>()[0] += static_cast<float>(target.size(0));
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
+  m.def("cpu_binary_accuracy", &cpu_binary_accuracy, "host fast path of binary_accuracy for small CPU batches",
+        pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("threshold"));
+  m.def("cpu_binary_accuracy_update", &cpu_binary_accuracy_update,
+        "host fast path of BinaryAccuracy.update: counts added into the 0-d float32 states", pybind11::arg("input"),
+        pybind11::arg("target"), pybind11::arg("threshold"), pybind11::arg("correct"), pybind11::arg("total"));
   m.def("cpu_binary_auc", &cpu_binary_auc, "host twin of the K3 AUROC / AUPRC rows for small CPU batches",
         pybind11::arg("x"), pybind11::arg("t"), pybind11::arg("w") = pybind11::none());
   m.def("cpu_binned_counts", &cpu_binned_counts, "host twin of binned_counts for small CPU batches");

@@ -91,7 +91,8 @@ def inference_update(fn: Callable) -> Callable:
 
     @functools.wraps(fn)
     def wrapper(*args, **kwargs):
-        if torch.compiler.is_compiling():
+        # already inside (a subclass update calling super().update): no second ~2 us context
+        if torch.is_inference_mode_enabled() or torch.compiler.is_compiling():
             return fn(*args, **kwargs)
         with torch.inference_mode():
             return fn(*args, **kwargs)
