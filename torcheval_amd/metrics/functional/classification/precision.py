@@ -55,11 +55,12 @@ def _precision_update(
         input = torch.argmax(input, dim=1)
     if average == "micro":
         return (input == target).sum(), (input != target).sum(), torch.tensor(0.0)
-    hit = input == target
-    ones = torch.ones_like(target)
-    num_label = target.new_zeros(num_classes).scatter_add_(0, target, ones)
-    num_tp = target.new_zeros(num_classes).scatter_add_(0, target[hit], ones[hit])
-    num_fp = target.new_zeros(num_classes).scatter_add_(0, input[~hit], ones[~hit])
+    # hit / miss as 0/1 scatter weights (no boolean-mask indexing: static shapes, traceable by
+    # torch.compile, same counts)
+    hit = (input == target).to(target.dtype)
+    num_label = target.new_zeros(num_classes).scatter_add_(0, target, torch.ones_like(target))
+    num_tp = target.new_zeros(num_classes).scatter_add_(0, target, hit)
+    num_fp = target.new_zeros(num_classes).scatter_add_(0, input, 1 - hit)
     return num_tp, num_fp, num_label
 
 

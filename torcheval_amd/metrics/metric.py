@@ -91,8 +91,9 @@ def inference_update(fn: Callable) -> Callable:
 
     @functools.wraps(fn)
     def wrapper(*args, **kwargs):
-        # already inside (a subclass update calling super().update): no second ~2 us context
-        if torch.is_inference_mode_enabled() or torch.compiler.is_compiling():
+        # compiling first (dynamo cannot trace is_inference_mode_enabled); already inside (a
+        # subclass update calling super().update): no second ~2 us context
+        if torch.compiler.is_compiling() or torch.is_inference_mode_enabled():
             return fn(*args, **kwargs)
         with torch.inference_mode():
             return fn(*args, **kwargs)

@@ -109,12 +109,17 @@ def update_states(
         wt, ws = w, 1.0
     else:
         wt, ws = None, float(1.0 if w is None else w)
-    native().row_sums(x, t, wt, ws, [o for o, _, _ in outs], [s * 8 + op for _, s, op in outs], rows)
+    update(x, t, wt, ws, [o for o, _, _ in outs], [s * 8 + op for _, s, op in outs], rows)
 
 
 def update(x: torch.Tensor, t: Optional[torch.Tensor], w: Optional[torch.Tensor], w_scalar: float,
            outs: list, codes: list, rows: int = 1) -> None:
-    """Lean form for the per-batch metric updates: outputs and packed codes (stat * 8 + op)."""
+    """Lean form for the per-batch metric updates: outputs and packed codes (stat * 8 + op).
+    Eager calls take the pybind entry (less host time); under torch.compile the dispatcher op
+    (CPU host twin / GPU kernel, with a Meta kernel) keeps the update in the graph."""
+    if _ops.compiling():
+        torch.ops.torcheval_amd.row_sums(x, t, w, w_scalar, outs, codes, rows)
+        return
     native().row_sums(x, t, w, w_scalar, outs, codes, rows)
 
 
