@@ -137,6 +137,25 @@ __global__ __launch_bounds__(256) void read_nt_kernel(const float* __restrict__ 
 
 __global__ void empty_kernel() {}
 
+// the read floor with TPB-thread workgroups (TPB / 64 rows each): same 8192 waves, fewer and
+// larger workgroups - is workgroup dispatch part of the per-launch cost?
+template <int TPB>
+__global__ __launch_bounds__(TPB) void read_floor_wg_kernel(const float* __restrict__ x, const int64_t* __restrict__ y,
+                                                            float* __restrict__ sink) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * (TPB / 64) + (threadIdx.x >> 6);
+  const float* rp = x + row * C;
+  float m = -__builtin_huge_valf();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int col = u * FSTEP + lane * 4;
+    const float4 q = *reinterpret_cast<const float4*>(rp + (col < C ? col : 0));
+    m = fmaxf(m, fmaxf(fmaxf(q.x, q.y), fmaxf(q.z, q.w)));
+  }
+  const int64_t t = y[row];
+  if (m == 12345.678f && t == 7) sink[row] = m;
+}
+
 template <typename F>
 float time_it(F launch, int iters, hipEvent_t e0, hipEvent_t e1) {
   for (int i = 0; i < 20; ++i) launch(i);
@@ -221,9 +240,19 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(read_floor_bigargs_kernel, dim3(N / 4), dim3(256), 0, 0, a);
   };
 
+  auto read512 = [&](int i) {
+    hipLaunchKernelGGL(read_floor_wg_kernel<512>, dim3(N / 8), dim3(512), 0, 0, xs[i % POOL], ys[i % POOL], sink);
+  };
+  auto read1024 = [&](int i) {
+    hipLaunchKernelGGL(read_floor_wg_kernel<1024>, dim3(N / 16), dim3(1024), 0, 0, xs[i % POOL], ys[i % POOL], sink);
+  };
+  auto empty1024 = [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(N / 16), dim3(1024), 0, 0); };
+  auto empty1 = [&](int) { hipLaunchKernelGGL(empty_kernel, dim3(1), dim3(64), 0, 0); };
+
   // interleave the variants over 3 rounds and keep each one's best median-of-round
-  constexpr int NV = 7;
-  float best[NV] = {1e9f, 1e9f, 1e9f, 1e9f, 1e9f, 1e9f, 1e9f};
+  constexpr int NV = 11;
+  float best[NV];
+  for (float& b : best) b = 1e9f;
   for (int r = 0; r < 3; ++r) {
     best[0] = std::min(best[0], time_it(prod, iters, e0, e1));
     best[1] = std::min(best[1], time_it(read, iters, e0, e1));
@@ -232,14 +261,19 @@ int main(int argc, char** argv) {
     best[4] = std::min(best[4], time_it(readatomic, iters, e0, e1));
     best[5] = std::min(best[5], time_it(readreduce, iters, e0, e1));
     best[6] = std::min(best[6], time_it(readnt, iters, e0, e1));
+    best[7] = std::min(best[7], time_it(read512, iters, e0, e1));
+    best[8] = std::min(best[8], time_it(read1024, iters, e0, e1));
+    best[9] = std::min(best[9], time_it(empty1024, iters, e0, e1));
+    best[10] = std::min(best[10], time_it(empty1, iters, e0, e1));
   }
   const double bytes = static_cast<double>(N) * C * 4 + N * 8;
   const char* names[NV] = {"prod (launch_cls_counts micro)", "read floor (same geometry)", "empty (2048 x 256)",
                            "read floor behind ClsCountsArgs", "read floor + one atomic", "read floor + DPP max + target compare",
-                           "read floor, non-temporal loads"};
+                           "read floor, non-temporal loads", "read floor, 512-thread workgroups",
+                           "read floor, 1024-thread workgroups", "empty (512 x 1024)", "empty (1 x 64)"};
   for (int v = 0; v < NV; ++v)
     printf("{\"variant\": \"%s\", \"pool\": %d, \"us_per_launch\": %.3f, \"TBps\": %.2f}\n", names[v], POOL, best[v],
-           v != 2 ? bytes / (best[v] * 1e-6) / 1e12 : 0.0);
+           (v != 2 && v < 9) ? bytes / (best[v] * 1e-6) / 1e12 : 0.0);
   printf("{\"prod_over_floor\": %.4f}\n", best[0] / best[1]);
 
   // Host side: the host cost of one production launch with no Python in
