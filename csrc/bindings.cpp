@@ -1350,6 +1350,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   tea_register_runtime(m);
   tea_register_cpu_metrics(m);
   tea_register_rccl(m);
+  tea_register_hostread(m);
 }
 
 // ---------------------------------------------------------------- torch dispatcher registration

@@ -487,5 +487,9 @@ int launch_snapshot_flags(const void* src, void* dst, int64_t bytes, const int* 
 // summed [ws][words][2] slots -> int32 [words], max over ranks
 int launch_merge_flag_slots(const float* slots, int* out, int words, int ws, hipStream_t stream);
 // test support (csrc/kernels/testing.hip): one lane spins until *flag != 0 or max_ms elapse
+// low-latency host read (hostread.hip): words <= kHostReadWords int32 from src into a pinned,
+// device-mapped host slot [seq, words...], published by a system-scope release store of seq
+constexpr int kHostReadWords = 14;
+int launch_publish_words(const int32_t* src, int words, int32_t* slot_dev, int32_t seq, hipStream_t stream);
 int launch_spin_on_flag(const int* flag, int64_t max_ms, hipStream_t stream);
 }  // namespace tea

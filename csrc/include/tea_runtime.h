@@ -8,3 +8,4 @@
 void tea_register_runtime(pybind11::module_& m);
 void tea_register_cpu_metrics(pybind11::module_& m);
 void tea_register_rccl(pybind11::module_& m);  // csrc/runtime/rccl_direct.cpp
+void tea_register_hostread(pybind11::module_& m);  // csrc/runtime/hostread.cpp

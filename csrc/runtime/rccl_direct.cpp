@@ -115,7 +115,8 @@ struct Comm {
   // a burst of syncs pays it once, not per sync)
   int probes = 0;
   uint64_t untracked = 0;
-  hipStream_t last_stream = nullptr;
+  hipStream_t last_stream = nullptr;  // nullptr is a real stream here: the device's null stream
+  bool has_last = false;              // a collective was ever enqueued (last_stream is valid)
 };
 
 struct Pending {
@@ -234,8 +235,8 @@ hipEvent_t take_event() {
 }
 
 // record a probe for `handle` on `stream` and queue it (caller does NOT hold g_mu and has
-// already counted it in c.probes); false when the record failed (count undone)
-bool record_probe(int64_t handle, hipStream_t stream) {
+// already counted it in c.probes); its sequence number, or 0 when the record failed (count undone)
+uint64_t record_probe(int64_t handle, hipStream_t stream) {
   hipEvent_t ev = take_event();
   const bool ok = ev && hipEventRecord(ev, stream) == hipSuccess;
   std::lock_guard<std::mutex> lock(g_mu);
@@ -243,15 +244,16 @@ bool record_probe(int64_t handle, hipStream_t stream) {
   if (!ok) {
     --c.probes;
     if (ev) g_event_pool.push_back(ev);
-    return false;
+    return 0;
   }
-  g_pending.push_back({ev, handle, Clock::now() + std::chrono::milliseconds(c.timeout_ms), ++g_seq});
+  const uint64_t seq = ++g_seq;
+  g_pending.push_back({ev, handle, Clock::now() + std::chrono::milliseconds(c.timeout_ms), seq});
   if (!g_watchdog) {
     g_stop = false;
     g_watchdog = new std::thread(watchdog_loop);
   }
   g_cv.notify_all();
-  return true;
+  return seq;
 }
 
 void watchdog_loop() {
@@ -300,7 +302,7 @@ void watchdog_loop() {
         g_event_pool.push_back(it->ev);
         g_pending.erase(it);
         --c.probes;
-        if (c.state.load() == kOk && c.probes == 0 && c.untracked > 0 && c.last_stream) {
+        if (c.state.load() == kOk && c.probes == 0 && c.untracked > 0 && c.has_last) {
           // collectives enqueued behind the retired probe: probe them now
           c.untracked = 0;
           ++c.probes;
@@ -329,7 +331,7 @@ void watchdog_loop() {
         (void)hipSetDevice(dev);
         // never insert into a stream that is being captured into a graph
         const bool capturing = hipStreamIsCapturing(fu.second, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
-        const bool ok = !capturing && record_probe(fu.first, fu.second);  // a failed record undoes its count
+        const bool ok = !capturing && record_probe(fu.first, fu.second) != 0;  // a failed record undoes its count
         if (!ok) {
           std::lock_guard<std::mutex> lock(g_mu);
           Comm& c = *g_comms[fu.first];
@@ -361,21 +363,26 @@ bool watchdog_enabled() {
 
 // completion tracking of a collective just enqueued for `handle` on `stream` (caller does NOT
 // hold g_mu): a probe event when none is in flight, else counted for the watchdog's follow-up
-// probe.  `force`: always record (a host waiter needs this collective's own completion).
-void track(int64_t handle, hipStream_t stream, bool force = false) {
-  if (!watchdog_enabled() && !force) return;
+// probe.  `force`: always record (a host waiter needs a probe behind everything it enqueued:
+// the watchdog's follow-up for counted collectives may not be recorded yet).  Returns the
+// recorded probe's sequence number (0 = none recorded).
+uint64_t track(int64_t handle, hipStream_t stream, bool force = false) {
+  if (!watchdog_enabled() && !force) return 0;
   {
     std::lock_guard<std::mutex> lock(g_mu);
     Comm& c = comm_ref(handle);
     c.last_stream = stream;
+    c.has_last = true;
     if (c.probes > 0 && !force) {
       ++c.untracked;
-      return;
+      return 0;
     }
     ++c.probes;
     if (force) c.untracked = 0;  // the forced probe covers everything before it on the stream
   }
-  TORCH_CHECK(record_probe(handle, stream), "rccl_direct: hipEventRecord failed");
+  const uint64_t seq = record_probe(handle, stream);
+  TORCH_CHECK(seq != 0, "rccl_direct: hipEventRecord failed");
+  return seq;
 }
 
 ncclDataType_t dtype_of(const at::Tensor& t) {
@@ -467,14 +474,19 @@ bool rccl_wait_aborted(int64_t handle, int64_t timeout_ms) {
 void rccl_comm_destroy(int64_t handle) {
   ncclComm_t comm;
   int device;
-  hipStream_t s_untracked = nullptr;
+  hipStream_t s_last = nullptr;
+  bool has_last = false;
   {
     std::lock_guard<std::mutex> lock(g_mu);
     if (handle >= 0 && handle < static_cast<int64_t>(g_comms.size()) && g_comms[handle] &&
-        g_comms[handle]->state.load() == kOk && g_comms[handle]->untracked > 0)
-      s_untracked = g_comms[handle]->last_stream;
+        g_comms[handle]->state.load() == kOk) {
+      s_last = g_comms[handle]->last_stream;
+      has_last = g_comms[handle]->has_last;
+    }
   }
-  if (s_untracked) track(handle, s_untracked, true);  // drain-check every collective, tracked or not
+  // a probe behind every collective enqueued so far, tracked or counted (a watchdog follow-up
+  // for counted ones may not be recorded yet, so never rely on it here)
+  if (has_last) track(handle, s_last, true);
   {
     std::lock_guard<std::mutex> lock(g_mu);
     if (handle < 0 || handle >= static_cast<int64_t>(g_comms.size()) || !g_comms[handle]) return;
@@ -523,24 +535,20 @@ void rccl_comm_destroy(int64_t handle) {
 // timeout_ms.  false = deadline passed: the communicator is marked failed (observed, so no
 // teardown) and aborted in the background.
 bool rccl_wait(int64_t handle, int64_t timeout_ms) {
-  uint64_t seq = 0;
-  hipStream_t s_untracked = nullptr;
+  hipStream_t s_last = nullptr;
+  bool has_last = false;
   {
     std::lock_guard<std::mutex> lock(g_mu);
     Comm& c = comm_ref(handle);
     TORCH_CHECK(c.state.load() == kOk, "rccl_direct: communicator ", handle, " is unusable (", c.reason, ")");
-    if (c.untracked > 0) s_untracked = c.last_stream;
+    s_last = c.last_stream;
+    has_last = c.has_last;
   }
-  if (s_untracked) track(handle, s_untracked, true);  // the newest collective gets its own probe
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    for (auto it = g_pending.rbegin(); it != g_pending.rend(); ++it)
-      if (it->handle == handle) {
-        seq = it->seq;
-        break;
-      }
-  }
-  if (!seq) return true;  // nothing in flight (the watchdog already retired it)
+  if (!has_last) return true;  // nothing was ever enqueued
+  // our own probe behind the newest collective: "the newest pending entry" is not enough - a
+  // counted collective's follow-up probe may still be on its way from the watchdog (that race
+  // let a held collective pass as complete)
+  const uint64_t seq = track(handle, s_last, true);
   const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
   for (;;) {
     {

@@ -266,12 +266,24 @@ def test_sync_timeout_raises_then_recovers(pg):
         native().test_host_flag_set(0)
         native().test_spin_on_host_flag(0, 20000)  # holds the stream for at most 20 s
         t0 = time.perf_counter()
+        raised = None
         try:
-            with pytest.raises(TimeoutError, match="did not complete"):
+            try:
                 sync_and_compute(cm, timeout=timedelta(milliseconds=500))
+            except TimeoutError as e:
+                raised = e
             elapsed = time.perf_counter() - t0
         finally:
             native().test_host_flag_set(1)
+        if raised is None:
+            from torcheval_amd.parallel.state_buffer import plan_summary
+
+            sb = cm.__dict__.get("_tea_sb")
+            plans = [(k, p.comm, p.rplan, p.gen) for k, p in sb.plans.items()] if sb is not None else None
+            pytest.fail(f"no TimeoutError after {elapsed:.3f} s; comm {h_old} state {rccl_direct.state(h_old)}; "
+                        f"plan {plan_summary(cm)}; plans {plans} gen {rccl_direct.GENERATION[0]}; "
+                        f"comm now {rccl_direct.comm_for(dist.group.WORLD, 1, DEV)}")
+        assert "did not complete" in str(raised)
         torch.cuda.synchronize()
         assert 0.4 < elapsed < 5.0, elapsed
         assert rccl_direct.state(h_old) in (1, 2)

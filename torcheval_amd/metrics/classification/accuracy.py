@@ -34,6 +34,7 @@ from torcheval_amd.metrics.functional.classification.accuracy import (
 from torcheval_amd.metrics.metric import Metric, inference_update
 import torcheval_amd.ops as _ops
 from torcheval_amd.ops import compiling, native, native_loaded, use_native
+from torcheval_amd.ops.hostread import read_int
 
 # K1 micro-accuracy entry of the loaded extension (None when unbuilt); metrics built while
 # ``torcheval_amd.ops.DISABLE_HIP`` is set do not use it (checked per metric, at construction)
@@ -73,8 +74,8 @@ def _micro_op_ok(input: torch.Tensor, target: torch.Tensor, state: torch.Tensor,
 
 def _raise_on_device_error(err: Optional[torch.Tensor]) -> None:
     """Surface a device-side validation failure recorded by a K1 kernel."""
-    if err is not None and int(err.item()) != 0:
-        code = int(err.item())
+    code = read_int(err) if err is not None else 0
+    if code != 0:
         err.zero_()
         raise RuntimeError(
             "index out of bounds: a target (or predicted) class index was outside "

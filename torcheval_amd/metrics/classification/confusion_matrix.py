@@ -19,6 +19,7 @@ from torcheval_amd.metrics.functional.classification.confusion_matrix import (
 )
 from torcheval_amd.metrics.metric import Metric, inference_update
 from torcheval_amd.ops.classification import cls_counts, native_cls
+from torcheval_amd.ops.hostread import read_ints
 
 TMulticlassConfusionMatrix = TypeVar("TMulticlassConfusionMatrix")
 TBinaryConfusionMatrix = TypeVar("TBinaryConfusionMatrix")
@@ -77,7 +78,7 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
     def _check_device_errors(self) -> None:
         if self._err is None:
             return
-        code, max_t, max_p = self._err.tolist()
+        code, max_t, max_p = read_ints(self._err)
         if code != 0:
             self._err.zero_()
             # same message as the reference's update-time check (its torch.max of the batch is

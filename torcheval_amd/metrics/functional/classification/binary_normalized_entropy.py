@@ -16,6 +16,7 @@ from torcheval_amd.metrics.functional.tensor_utils import _require_samples
 import torch.nn.functional as F
 
 from torcheval_amd.ops import use_native
+from torcheval_amd.ops.hostread import read_int, read_ints
 
 
 @torch.inference_mode()
@@ -89,7 +90,7 @@ def _baseline_update(num_positive: torch.Tensor, num_examples: torch.Tensor) -> 
 
 
 def _raise_range(flag: torch.Tensor, input: torch.Tensor) -> None:
-    if int(flag.item()) != 0:
+    if read_int(flag) != 0:
         _ne_range_check(input, False)
 
 
@@ -124,12 +125,14 @@ def _ne_device_error(err: torch.Tensor, from_logits: bool, dtype: torch.dtype) -
     the reference's message.  The range is over every update since the last check, which is
     the failing batch's own range when one update was bad (the reference raises at that
     update)."""
-    vals = err.cpu()
-    if int(vals[0]) == 0:
+    vals = read_ints(err)
+    if vals[0] == 0:
         return
     err.zero_()
     mask = (1 << 64) - 1
-    kmax, kmin = (k & mask for k in vals[2:6].view(torch.int64).tolist())
+    # words 2-5: two little-endian u64 keys (max, complemented min)
+    kmax = (vals[2] & 0xFFFFFFFF) | ((vals[3] & 0xFFFFFFFF) << 32)
+    kmin = (vals[4] & 0xFFFFFFFF) | ((vals[5] & 0xFFFFFFFF) << 32)
 
     def decode(key: int) -> float:
         u = key & ~(1 << 63) if key >> 63 else ~key & mask

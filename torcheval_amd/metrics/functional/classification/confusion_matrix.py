@@ -13,6 +13,7 @@ import torch
 import torch.nn.functional as F
 
 from torcheval_amd.ops.classification import binary_counts, cls_counts, native_binary, native_cls
+from torcheval_amd.ops.hostread import read_int
 
 
 @torch.inference_mode()
@@ -128,7 +129,7 @@ def _confusion_matrix_update(
 
 
 def _raise_confusion_err(err: torch.Tensor, input, target, num_classes: int) -> None:
-    code = int(err.item())
+    code = read_int(err)
     if code & 2:
         raise ValueError(
             "Got `input` prediction class which is too large for the number of classes, "

@@ -7,6 +7,7 @@ import torch.nn.functional as F
 
 from torcheval_amd.metrics.functional.tensor_utils import _require_samples
 from torcheval_amd.ops import use_native
+from torcheval_amd.ops.hostread import read_int
 
 __all__ = ["perplexity"]
 
@@ -39,7 +40,7 @@ def _perplexity_update(
         from torcheval_amd.config import config
 
         native().perplexity_sums(logits, tgt, ignore_index, out, flag, config.deterministic)
-        if err is None and int(flag.item()) != 0:
+        if err is None and read_int(flag) != 0:
             _perplexity_label_check(input, target, ignore_index)
         return out[0], out[1]
     _perplexity_label_check(input, target, ignore_index)

@@ -8,6 +8,7 @@ from torcheval_amd.metrics.metric import inference_update
 
 from torcheval_amd.metrics.functional.text import _perplexity_compute, _perplexity_update
 from torcheval_amd.metrics.text._sum_states import _SumStates
+from torcheval_amd.ops.hostread import read_int
 
 __all__ = ["Perplexity"]
 
@@ -35,7 +36,7 @@ class Perplexity(_SumStates):
         return self
 
     def _check_device_errors(self) -> None:
-        if self._err is not None and int(self._err.item()) != 0:
+        if self._err is not None and read_int(self._err) != 0:
             self._err.zero_()
             raise ValueError(
                 "Class labels in `target` tensor cannot be larger than vocab_size minus one "

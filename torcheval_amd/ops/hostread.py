@@ -1,0 +1,47 @@
+"""Low-latency host reads of small int32 device tensors (device error flags).
+
+``compute()`` of a metric whose GPU updates validate labels on the device has to read its
+error flag on the host before it may return (the reference raises at ``update()`` instead, on
+a host-synchronising check).  ``tensor.item()`` pays a D2H copy plus a stream synchronize
+(~17 us idle, ~21 us right behind an update kernel on MI355X); ``read_ints`` publishes the
+words into pinned, device-mapped host memory from a one-lane kernel and spins on a sequence
+word (~7 / ~12.6 us; ``profiles/host_poll_latency_r4.json``), falling back to a blocking
+stream synchronize after ``TORCHEVAL_AMD_HOST_POLL_US`` (default 1000; 0 disables the path).
+"""
+import os
+from typing import List
+
+import torch
+
+import torcheval_amd.ops as _ops
+
+_SPIN_US = int(os.environ.get("TORCHEVAL_AMD_HOST_POLL_US", "1000"))
+_MAX_WORDS = 14  # tea::kHostReadWords
+
+
+def _fast(t: torch.Tensor) -> bool:
+    return (
+        _SPIN_US > 0
+        and t.is_cuda
+        and t.dtype == torch.int32
+        and 1 <= t.numel() <= _MAX_WORDS
+        and t.is_contiguous()
+        and not _ops.DISABLE_HIP
+        and _ops.native_loaded()
+        and not _ops.compiling()
+        and not torch.cuda.is_current_stream_capturing()
+    )
+
+
+def read_ints(t: torch.Tensor) -> List[int]:
+    """The elements of ``t`` (flattened) as Python ints, after the work queued before this call."""
+    if _fast(t):
+        return list(_ops.native().read_small_ints(t, _SPIN_US))
+    return [int(v) for v in t.reshape(-1).tolist()]
+
+
+def read_int(t: torch.Tensor) -> int:
+    """The first element of ``t`` as a Python int."""
+    if _fast(t):
+        return int(_ops.native().read_small_ints(t.reshape(-1)[:1], _SPIN_US)[0])
+    return int(t.reshape(-1)[0].item())
