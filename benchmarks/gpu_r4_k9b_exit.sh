@@ -1,5 +1,6 @@
 #!/bin/bash
 # K9b early exit of finished workgroups: numerics, then the timing A/B in separate processes.
+# (The switch was removed after this A/B, profiles/k9b_early_exit_ab_r4.json: both arms now run the same kernel.)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
