@@ -74,6 +74,9 @@ def main() -> None:
         ("MulticlassConfusionMatrix(6).update bs=8", lambda m: m.update(xc, yc), "MulticlassConfusionMatrix",
          {"num_classes": 6}),
         ("BinaryAccuracy.update bs=8", lambda m: m.update(xb, yb), "BinaryAccuracy", {}),
+        ("BinaryPrecision.update bs=8", lambda m: m.update(xb, yb), "BinaryPrecision", {}),
+        ("BinaryRecall.update bs=8", lambda m: m.update(xb, yb), "BinaryRecall", {}),
+        ("BinaryF1Score.update bs=8", lambda m: m.update(xb, yb), "BinaryF1Score", {}),
         ("BinaryAUROC.update bs=8", lambda m: m.update(xb, yb), "BinaryAUROC", {}),
         ("BinaryAUPRC.update bs=8", lambda m: m.update(xb, yb), "BinaryAUPRC", {}),
     ]

@@ -11,6 +11,7 @@
 #include <torch/extension.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdint>
 #include <tuple>
@@ -439,6 +440,120 @@ void cpu_binary_accuracy_update(const at::Tensor& input, const at::Tensor& targe
   total.data_ptr<float>()[0] += static_cast<float>(target.size(0));
 }
 
+// ---- binary precision / recall / F1 (small CPU batches, integer / bool targets) ----
+
+// target [N] as int64 values
+void target_as_i64(const at::Tensor& t, std::vector<int64_t>& out) {
+  const int64_t n = t.size(0), st = t.stride(0);
+  out.resize(n);
+  switch (t.scalar_type()) {
+#define TEA_T(ST, CT)                                                          \
+  case ST: {                                                                   \
+    const CT* p = t.data_ptr<CT>();                                            \
+    for (int64_t i = 0; i < n; ++i) out[i] = static_cast<int64_t>(p[i * st]);  \
+    break;                                                                     \
+  }
+    TEA_T(at::kLong, int64_t)
+    TEA_T(at::kInt, int32_t)
+    TEA_T(at::kShort, int16_t)
+    TEA_T(at::kChar, int8_t)
+    TEA_T(at::kByte, uint8_t)
+    TEA_T(at::kBool, bool)
+#undef TEA_T
+    default: TORCH_CHECK(false, "cpu_binary_prf: integer / bool target expected");
+  }
+}
+
+template <typename S>
+void prf_sums(const S* x, int64_t n, int64_t sx, S thr, const std::vector<int64_t>& t, int64_t& s_prod,
+              int64_t& s_and, int64_t& s_t, int64_t& s_pred) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t pred = x[i * sx] < thr ? 0 : 1;  // torch.where(input < threshold, 0, 1)
+    s_prod += pred * t[i];
+    s_and += pred & t[i];
+    s_t += t[i];
+    s_pred += pred;
+  }
+}
+
+void prf_all_sums(const at::Tensor& input, const at::Tensor& target, double threshold, int64_t* sums) {
+  TORCH_CHECK(!input.is_cuda() && !target.is_cuda() && input.dim() == 1 && target.dim() == 1 &&
+                  input.size(0) == target.size(0), "cpu_binary_prf: CPU [N] input and target");
+  std::vector<int64_t> tv;
+  target_as_i64(target, tv);
+  const int64_t n = input.size(0);
+  if (input.scalar_type() == at::kFloat)
+    prf_sums(input.data_ptr<float>(), n, input.stride(0), static_cast<float>(threshold), tv, sums[0], sums[1],
+             sums[2], sums[3]);
+  else if (input.scalar_type() == at::kDouble)
+    prf_sums(input.data_ptr<double>(), n, input.stride(0), threshold, tv, sums[0], sums[1], sums[2], sums[3]);
+  else
+    TORCH_CHECK(false, "cpu_binary_prf: float32 / float64 input");
+}
+
+// class updates: 0-d float32 states += this batch's counts (each count cast to float32 first, as
+// ``state += int64_sum`` does).  kind 0 precision: (num_tp, num_fp) += (sum(pred * t),
+// sum(pred) - sum(pred * t)); kind 1 recall: (num_tp, num_true_labels) += (sum(pred & t), sum(t));
+// kind 2 F1: (num_tp, num_label, num_prediction) += (sum(pred * t), sum(t), sum(pred))
+void cpu_binary_prf_update(const at::Tensor& input, const at::Tensor& target, double threshold, int64_t kind,
+                           at::Tensor& a, at::Tensor& b, const c10::optional<at::Tensor>& c) {
+  TORCH_CHECK(kind >= 0 && kind <= 2 && (kind != 2 || c.has_value()), "cpu_binary_prf_update: bad kind / states");
+  const at::Tensor* states[3] = {&a, &b, c.has_value() ? &*c : &a};
+  for (const at::Tensor* st : states)
+    TORCH_CHECK(st->dim() == 0 && st->scalar_type() == at::kFloat && !st->is_cuda(),
+                "cpu_binary_prf_update: 0-d float32 CPU states");
+  int64_t sm[4] = {0, 0, 0, 0};  // sum(pred * t), sum(pred & t), sum(t), sum(pred)
+  prf_all_sums(input, target, threshold, sm);
+  float* pa = a.data_ptr<float>();
+  float* pb = b.data_ptr<float>();
+  if (kind == 0) {
+    pa[0] += static_cast<float>(sm[0]);
+    pb[0] += static_cast<float>(sm[3] - sm[0]);
+  } else if (kind == 1) {
+    pa[0] += static_cast<float>(sm[1]);
+    pb[0] += static_cast<float>(sm[2]);
+  } else {
+    pa[0] += static_cast<float>(sm[0]);
+    pb[0] += static_cast<float>(sm[2]);
+    c->data_ptr<float>()[0] += static_cast<float>(sm[3]);
+  }
+}
+
+// kind 0: precision = sum(pred * t) / sum(pred)            (NaN -> 0)
+// kind 1: recall    = sum(pred & t) / sum(t)               (NaN -> 0, warn)
+// kind 2: F1 from p = sum(pred * t) / sum(pred), r = sum(pred * t) / sum(t):
+//         nan_to_num(2 * p * r / (p + r)), warn when sum(t) == 0
+// -> (0-d float32 value, warn); every division and product in float32 in the reference's order
+std::tuple<at::Tensor, bool> cpu_binary_prf(const at::Tensor& input, const at::Tensor& target, double threshold,
+                                            int64_t kind) {
+  TORCH_CHECK(kind >= 0 && kind <= 2, "cpu_binary_prf: kind 0 (precision), 1 (recall) or 2 (F1)");
+  int64_t sm[4] = {0, 0, 0, 0};
+  prf_all_sums(input, target, threshold, sm);
+  const int64_t s_prod = sm[0], s_and = sm[1], s_t = sm[2], s_pred = sm[3];
+  float v = 0.f;
+  bool warn = false;
+  auto nz = [](float x) {  // torch.nan_to_num: NaN -> 0, +-inf -> +-FLT_MAX
+    return std::isnan(x) ? 0.f : (std::isinf(x) ? (x > 0 ? FLT_MAX : -FLT_MAX) : x);
+  };
+  if (kind == 0) {
+    v = nz(static_cast<float>(s_prod) / static_cast<float>(s_pred));
+  } else if (kind == 1) {
+    v = static_cast<float>(s_and) / static_cast<float>(s_t);
+    if (std::isnan(v)) {
+      warn = true;
+      v = 0.f;
+    }
+  } else {
+    warn = s_t == 0;
+    const float p = static_cast<float>(s_prod) / static_cast<float>(s_pred);
+    const float r = static_cast<float>(s_prod) / static_cast<float>(s_t);
+    v = nz(2.f * p * r / (p + r));
+  }
+  at::Tensor out = at::empty({}, at::TensorOptions().dtype(at::kFloat));
+  out.data_ptr<float>()[0] = v;
+  return {out, warn};
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
@@ -447,6 +562,13 @@ void tea_register_cpu_metrics(pybind11::module_& m) {
   m.def("cpu_binary_accuracy_update", &cpu_binary_accuracy_update,
         "host fast path of BinaryAccuracy.update: counts added into the 0-d float32 states", pybind11::arg("input"),
         pybind11::arg("target"), pybind11::arg("threshold"), pybind11::arg("correct"), pybind11::arg("total"));
+  m.def("cpu_binary_prf", &cpu_binary_prf,
+        "host fast path of binary_precision / binary_recall / binary_f1_score (integer / bool targets)",
+        pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("threshold"), pybind11::arg("kind"));
+  m.def("cpu_binary_prf_update", &cpu_binary_prf_update,
+        "host fast path of BinaryPrecision / BinaryRecall / BinaryF1Score.update (0-d float32 states)",
+        pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("threshold"), pybind11::arg("kind"),
+        pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c") = pybind11::none());
   m.def("cpu_binary_auc", &cpu_binary_auc, "host twin of the K3 AUROC / AUPRC rows for small CPU batches",
         pybind11::arg("x"), pybind11::arg("t"), pybind11::arg("w") = pybind11::none());
   m.def("cpu_binned_counts", &cpu_binned_counts, "host twin of binned_counts for small CPU batches");

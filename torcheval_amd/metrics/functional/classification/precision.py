@@ -9,13 +9,17 @@ from typing import Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops.classification import binary_counts, cls_counts, native_binary, native_cls
+from torcheval_amd.ops import native
+from torcheval_amd.ops.classification import _cpu_prf_ok, binary_counts, cls_counts, native_binary, native_cls
 
 
 @torch.inference_mode()
 def binary_precision(input: torch.Tensor, target: torch.Tensor, *, threshold: float = 0.5) -> torch.Tensor:
     """Precision of thresholded ``input`` (``input >= threshold`` is positive) vs ``target``.
     Class version: ``torcheval_amd.metrics.BinaryPrecision``."""
+    if _cpu_prf_ok(input, target):
+        _binary_precision_update_input_check(input, target)
+        return native().cpu_binary_prf(input, target, float(threshold), 0)[0]
     num_tp, num_fp, num_label = _binary_precision_update(input, target, threshold)
     return _precision_compute(num_tp, num_fp, num_label, "micro")
 

@@ -63,6 +63,34 @@ def native_cls(
     return _cpu_cls(input, target, num_classes)
 
 
+_CPU_PRF_TARGETS = (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
+_CPU_PRF_MAX = 1 << 16
+
+
+def _cpu_prf_ok(input: torch.Tensor, target: torch.Tensor) -> bool:
+    """Small 1-D CPU batches with integer / bool targets: binary precision / recall / F1 in one
+    host call (csrc/runtime/cpu_metrics.cpp cpu_binary_prf) instead of ~10 ATen dispatches.
+    Float targets keep the ATen path (its float sums and its bitwise-op errors)."""
+    return (
+        input.device.type == "cpu"
+        and target.device.type == "cpu"
+        and input.dim() == 1
+        and target.dim() == 1
+        and input.shape == target.shape
+        and input.dtype in (torch.float32, torch.float64)
+        and target.dtype in _CPU_PRF_TARGETS
+        and input.numel() <= _CPU_PRF_MAX
+        and not input.requires_grad
+        and not compiling()
+        and native_loaded()
+    )
+
+
+def _f32_scalars(*states: torch.Tensor) -> bool:
+    """0-d float32 CPU states (the host twins' in-place contract)."""
+    return all(s.dim() == 0 and s.dtype == torch.float32 and s.device.type == "cpu" for s in states)
+
+
 def native_binary(input: torch.Tensor, target: torch.Tensor, *states: torch.Tensor) -> bool:
     return (
         use_native(input)
