@@ -19,6 +19,15 @@ def test_values_match_tolist():
         assert hostread.read_int(t) == t[0].item()
 
 
+def test_int64_values():
+    vals = [0, 1, -1, 2**31, -(2**31) - 1, 2**40 + 3, -(2**62), 2**63 - 1]
+    for n in range(1, 8):
+        t = torch.tensor(vals[:n], dtype=torch.int64, device=DEV)
+        assert hostread._fast(t)
+        assert hostread.read_ints(t) == vals[:n]
+    assert not hostread._fast(torch.zeros(8, dtype=torch.int64, device=DEV))  # 16 words
+
+
 def test_sees_work_queued_before_it():
     t = torch.zeros(3, dtype=torch.int32, device=DEV)
     for v in range(1, 200):
@@ -49,7 +58,7 @@ def test_side_stream_is_the_current_stream():
 
 def test_fallbacks_take_tolist():
     assert not hostread._fast(torch.zeros(15, dtype=torch.int32, device=DEV))  # too many words
-    assert not hostread._fast(torch.zeros(2, dtype=torch.int64, device=DEV))
+    assert not hostread._fast(torch.zeros(2, dtype=torch.int16, device=DEV))
     assert hostread.read_ints(torch.arange(20, dtype=torch.int32, device=DEV)) == list(range(20))
     assert hostread.read_int(torch.tensor([7, 8], device=DEV)) == 7
 

@@ -12,6 +12,7 @@ from typing import List, Optional, Tuple
 import torch
 
 from torcheval_amd.ops import native
+from torcheval_amd.ops.hostread import read_ints
 from torcheval_amd.ops.sortscan import PAYLOAD_LABEL, PAYLOAD_TARGET, _sort_rows
 
 Curves = Tuple[List[torch.Tensor], List[torch.Tensor], List[torch.Tensor]]
@@ -45,7 +46,7 @@ def _curves(x: torch.Tensor, payload: torch.Tensor, kind: int, class_mode: bool,
     sizes = torch.empty(rows, dtype=torch.int64, device=dev)
     native().curve_count(s, idx, target, class_mode, k, ws, sizes)
     row_off = sizes.cumsum(0) - sizes
-    sz = sizes.tolist()  # the one host synchronisation
+    sz = read_ints(sizes)  # the one host synchronisation (pinned-memory path for <= 7 rows)
     total = int(sum(sz))
     prec = torch.empty(total + rows, dtype=torch.float32, device=dev)
     rec = torch.empty(total + rows, dtype=torch.float32, device=dev)

@@ -1,4 +1,4 @@
-"""Low-latency host reads of small int32 device tensors (device error flags).
+"""Low-latency host reads of small int32 / int64 device tensors (error flags, curve sizes).
 
 ``compute()`` of a metric whose GPU updates validate labels on the device has to read its
 error flag on the host before it may return (the reference raises at ``update()`` instead, on
@@ -20,11 +20,12 @@ _MAX_WORDS = 14  # tea::kHostReadWords
 
 
 def _fast(t: torch.Tensor) -> bool:
+    words = t.numel() * (2 if t.dtype == torch.int64 else 1)
     return (
         _SPIN_US > 0
         and t.is_cuda
-        and t.dtype == torch.int32
-        and 1 <= t.numel() <= _MAX_WORDS
+        and t.dtype in (torch.int32, torch.int64)
+        and 1 <= words <= _MAX_WORDS
         and t.is_contiguous()
         and not _ops.DISABLE_HIP
         and _ops.native_loaded()
@@ -36,12 +37,15 @@ def _fast(t: torch.Tensor) -> bool:
 def read_ints(t: torch.Tensor) -> List[int]:
     """The elements of ``t`` (flattened) as Python ints, after the work queued before this call."""
     if _fast(t):
-        return list(_ops.native().read_small_ints(t, _SPIN_US))
+        if t.dtype == torch.int64:  # little-endian (lo, hi) int32 pairs
+            w = _ops.native().read_small_ints(t.reshape(-1).view(torch.int32), _SPIN_US)
+            return [(w[2 * i] & 0xFFFFFFFF) | (w[2 * i + 1] << 32) for i in range(len(w) // 2)]
+        return list(_ops.native().read_small_ints(t.reshape(-1), _SPIN_US))
     return [int(v) for v in t.reshape(-1).tolist()]
 
 
 def read_int(t: torch.Tensor) -> int:
     """The first element of ``t`` as a Python int."""
     if _fast(t):
-        return int(_ops.native().read_small_ints(t.reshape(-1)[:1], _SPIN_US)[0])
+        return read_ints(t.reshape(-1)[:1])[0]
     return int(t.reshape(-1)[0].item())
