@@ -16,6 +16,15 @@ __all__ = ["perplexity"]
 def perplexity(input: torch.Tensor, target: torch.Tensor, ignore_index: Optional[int] = None) -> torch.Tensor:
     """exp(mean token negative log-likelihood) of [B, S, V] logits vs [B, S] targets (float64).
     Class version: ``Perplexity``."""
+    if use_native(input) and target.is_cuda:
+        # K7 records out-of-range targets on the device; the exp / divide is enqueued before the
+        # flag is read, so the host read waits once for everything instead of gating the launch
+        flag = torch.zeros(1, dtype=torch.int32, device=input.device)
+        sum_log_probs, num_total = _perplexity_update(input, target, ignore_index, err=flag)
+        out = _perplexity_compute(sum_log_probs, num_total)
+        if read_int(flag) != 0:
+            _perplexity_label_check(input, target, ignore_index)
+        return out
     sum_log_probs, num_total = _perplexity_update(input, target, ignore_index)
     return _perplexity_compute(sum_log_probs, num_total)
 
