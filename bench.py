@@ -29,6 +29,7 @@ the secondary sync timings.
 
 import argparse
 from datetime import timedelta
+import gc
 import json
 import os
 import time
@@ -197,12 +198,16 @@ def main() -> None:
         device_sync()
         metric.reset()
 
+    # no Python garbage-collection pass inside the ~140 us region (as timeit does)
+    gc.collect()
+    gc.disable()
     barrier()
     device_sync()
     t0 = time.perf_counter()
     acc = run(args.steps)  # ends in sync_and_compute at N > 1: the closing rendezvous
     device_sync()
     elapsed = time.perf_counter() - t0
+    gc.enable()
 
     # correctness guard: the synced count must equal world * steps * batch
     total = float(metric.num_total) if world == 1 else None
