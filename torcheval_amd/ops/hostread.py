@@ -46,6 +46,8 @@ def read_ints(t: torch.Tensor) -> List[int]:
 
 def read_int(t: torch.Tensor) -> int:
     """The first element of ``t`` as a Python int."""
+    if t.numel() == 1 and not t.is_cuda:
+        return int(t.item())
     if _fast(t):
         return read_ints(t.reshape(-1)[:1])[0]
     return int(t.reshape(-1)[0].item())
