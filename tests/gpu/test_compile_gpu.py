@@ -4,7 +4,16 @@
 import pytest
 import torch
 
-from torcheval_amd.metrics import BinaryBinnedAUPRC, MulticlassAccuracy, MulticlassConfusionMatrix
+from torcheval_amd.metrics import (
+    BinaryAccuracy,
+    BinaryBinnedAUPRC,
+    Mean,
+    MeanSquaredError,
+    MulticlassAccuracy,
+    MulticlassConfusionMatrix,
+    MultilabelAccuracy,
+    R2Score,
+)
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -20,10 +29,25 @@ def _bin_data(i):
     return torch.rand(4096, device=DEV, generator=g), torch.randint(0, 2, (4096,), device=DEV, generator=g)
 
 
+def _reg_data(i):
+    g = torch.Generator(device=DEV).manual_seed(200 + i)
+    return torch.randn(4096, 8, device=DEV, generator=g), torch.randn(4096, 8, device=DEV, generator=g)
+
+
+def _ml_data(i):
+    g = torch.Generator(device=DEV).manual_seed(300 + i)
+    return torch.rand(1024, 50, device=DEV, generator=g), torch.randint(0, 2, (1024, 50), device=DEV, generator=g)
+
+
 CASES = {
     "accuracy": (lambda: MulticlassAccuracy(device=DEV), _cls_data),
     "confusion": (lambda: MulticlassConfusionMatrix(100, device=DEV), _cls_data),
     "binned_auprc": (lambda: BinaryBinnedAUPRC(threshold=200, device=DEV), _bin_data),
+    "binary_accuracy": (lambda: BinaryAccuracy(device=DEV), _bin_data),
+    "mse": (lambda: MeanSquaredError(device=DEV), _reg_data),
+    "r2": (lambda: R2Score(device=DEV), _reg_data),
+    "multilabel_hamming": (lambda: MultilabelAccuracy(criteria="hamming", device=DEV), _ml_data),
+    "mean": (lambda: Mean(device=DEV), lambda i: (_bin_data(i)[0],)),
 }
 
 
@@ -34,13 +58,13 @@ def test_compiled_update_loop_matches_eager(name):
     torch._dynamo.reset()
 
     @torch.compile(fullgraph=True)
-    def step(x, y):
-        comp.update(x, y)
+    def step(*args):
+        comp.update(*args)
 
     for i in range(4):
-        x, y = data(i)
-        eager.update(x, y)
-        step(x, y)
+        args = data(i)
+        eager.update(*args)
+        step(*args)
     torch.testing.assert_close(comp.compute(), eager.compute())
 
 

@@ -178,6 +178,11 @@ def binary_counts(
     destination and to its optional second destination (``*2``); ``total`` += N.  With
     ``strict`` a target outside {0, 1} counts nowhere; otherwise it is a wrong prediction.
     """
+    if compiling() and tp2 is None and fp2 is None and tn2 is None and fn2 is None:
+        # the dispatcher op (Meta kernel) keeps a compiled update in one graph
+        torch.ops.torcheval_amd.binary_counts(input, target, weight, float(threshold), tp, fp, tn, fn, total,
+                                              int(strict))
+        return
     native().binary_counts(
         input, target, weight, float(threshold), tp, fp, tn, fn, total, int(strict), MAX_BLOCKS,
         tp2, fp2, tn2, fn2,
@@ -219,6 +224,7 @@ def multilabel_counts(
 ) -> None:
     """K2: add the update's correct count (and total) into float32 scalar states."""
     total = float(target.numel() if criteria == "hamming" else target.shape[0])
-    native().multilabel_counts(
+    _ml = torch.ops.torcheval_amd.multilabel_counts if compiling() else native().multilabel_counts
+    _ml(
         input, target, float(threshold), int(k), ML_CRITERIA[criteria], num_correct, num_total, total
     )

@@ -4,7 +4,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops import native
+from torcheval_amd.ops import compiling, native
 
 _FLOATISH = (torch.float32, torch.float64, torch.float16, torch.bfloat16)
 _ANY = _FLOATISH + (torch.int64, torch.int32, torch.int16, torch.int8, torch.uint8, torch.bool)
@@ -34,6 +34,9 @@ def column_moments(
         t = t[:, None]
     if t is not None and t.dtype == torch.bool:
         t = t.to(torch.uint8)
+    if compiling():  # the dispatcher op (Meta kernel): keeps a compiled update in one graph
+        torch.ops.torcheval_amd.column_moments(x, t, w, sse, st, stt, sx, sw, int(overwrite), 0, None, 0)
+        return
     native().column_moments(x, t, w, sse, st, stt, sx, sw, int(overwrite))
 
 
@@ -50,7 +53,8 @@ def mse_fused(
         t2 = t2.to(torch.uint8)
     buf = torch.empty(d + 1, dtype=torch.float32, device=x.device)
     out = torch.empty(d if raw_values else (), dtype=torch.float32, device=x.device)
-    native().column_moments(x2, t2, w, buf[:d], None, None, None, buf[d:], 1, 1 if raw_values else 2, out)
+    _cm = torch.ops.torcheval_amd.column_moments if compiling() else native().column_moments
+    _cm(x2, t2, w, buf[:d], None, None, None, buf[d:], 1, 1 if raw_values else 2, out, 0)
     if raw_values and x.dim() == 1:
         return out[0]  # [1] -> scalar, as sse.sum(dim=0) of a 1-D error is 0-d
     return out
@@ -70,7 +74,8 @@ def r2_fused(x: torch.Tensor, t: torch.Tensor, multioutput: str, num_regressors:
     buf = torch.empty(3, d, dtype=torch.float32, device=x.device)
     mode = _R2_MODES[multioutput]
     out = torch.empty(d if mode == 3 else (), dtype=torch.float32, device=x.device)
-    native().column_moments(x2, t2, None, buf[0], buf[1], buf[2], None, None, 1, mode, out, int(num_regressors))
+    _cm = torch.ops.torcheval_amd.column_moments if compiling() else native().column_moments
+    _cm(x2, t2, None, buf[0], buf[1], buf[2], None, None, 1, mode, out, int(num_regressors))
     if mode == 3 and x.dim() == 1:
         return out[0]
     return out
@@ -96,5 +101,6 @@ def ne_sums(
     flag = err if err is not None else torch.zeros(1, dtype=torch.int32, device=x.device)
     from torcheval_amd.config import config
 
-    native().ne_sums(x, t, w, bool(from_logits), out, flag, config.deterministic)
+    _ne = torch.ops.torcheval_amd.ne_sums if compiling() else native().ne_sums
+    _ne(x, t, w, bool(from_logits), out, flag, bool(config.deterministic))
     return out, flag
