@@ -201,6 +201,9 @@ def main() -> None:
     # no Python garbage-collection pass inside the ~140 us region (as timeit does)
     gc.collect()
     gc.disable()
+    presleep = float(os.environ.get("BENCH_PRESLEEP_MS", "0"))
+    if presleep > 0:
+        time.sleep(presleep / 1e3)
     barrier()
     device_sync()
     t0 = time.perf_counter()
