@@ -190,6 +190,13 @@ def main() -> None:
         rate = _reference_eager_rate(x_pool, y_pool, 2000)
         ref_rate = rate if rank == 0 else None
 
+    # No Python garbage-collection pass inside the ~140 us region (as timeit does).  The collect
+    # runs BEFORE the warmup: any idle gap between the warmup and t0 lets the GPU drop its clocks
+    # (a collect placed right before the region made it 190-270 us instead of 141-143 us,
+    # profiles/bench_region_gc_placement_r4.json).
+    gc.collect()
+    gc.disable()
+
     # Warmup runs the exact timed sequence (updates + compute / sync_and_compute), twice, so
     # every one-time cost - lazy load of a kernel's code object, allocator growth, RCCL
     # communicator setup - is paid here and not inside the timed region.
@@ -198,12 +205,6 @@ def main() -> None:
         device_sync()
         metric.reset()
 
-    # no Python garbage-collection pass inside the ~140 us region (as timeit does)
-    gc.collect()
-    gc.disable()
-    presleep = float(os.environ.get("BENCH_PRESLEEP_MS", "0"))
-    if presleep > 0:
-        time.sleep(presleep / 1e3)
     barrier()
     device_sync()
     t0 = time.perf_counter()
