@@ -190,11 +190,10 @@ def main() -> None:
         rate = _reference_eager_rate(x_pool, y_pool, 2000)
         ref_rate = rate if rank == 0 else None
 
-    # No Python garbage-collection pass inside the ~140 us region (as timeit does).  The collect
-    # runs BEFORE the warmup: any idle gap between the warmup and t0 lets the GPU drop its clocks
-    # (a collect placed right before the region made it 190-270 us instead of 141-143 us,
+    # No automatic Python garbage-collection pass inside the warmup + ~140 us region (as timeit
+    # does), and no explicit collect either: any idle gap between the warmup and t0 lets the GPU
+    # drop its clocks (a collect right before the region made it 190-270 us instead of 139-143,
     # profiles/bench_region_gc_placement_r4.json).
-    gc.collect()
     gc.disable()
 
     # Warmup runs the exact timed sequence (updates + compute / sync_and_compute), twice, so
