@@ -554,6 +554,72 @@ std::tuple<at::Tensor, bool> cpu_binary_prf(const at::Tensor& input, const at::T
   return {out, warn};
 }
 
+// ---- functional mean_squared_error (small CPU batches) ----
+
+template <typename S>
+void mse_sums(const at::Tensor& x, const at::Tensor& t, const c10::optional<at::Tensor>& w, std::vector<double>& sse,
+              double& sw) {
+  const int64_t n = x.size(0), d = x.dim() == 2 ? x.size(1) : 1;
+  const int64_t xs0 = x.stride(0), xs1 = x.dim() == 2 ? x.stride(1) : 0;
+  const int64_t ts0 = t.stride(0), ts1 = t.dim() == 2 ? t.stride(1) : 0;
+  const S* px = x.data_ptr<S>();
+  const S* pt = t.data_ptr<S>();
+  const S* pw = w.has_value() ? w->data_ptr<S>() : nullptr;
+  const int64_t ws0 = w.has_value() ? w->stride(0) : 0;
+  sse.assign(d, 0.0);
+  sw = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double wi = pw ? static_cast<double>(pw[i * ws0]) : 1.0;
+    sw += wi;
+    for (int64_t c = 0; c < d; ++c) {
+      const double e = static_cast<double>(pt[i * ts0 + c * ts1]) - static_cast<double>(px[i * xs0 + c * xs1]);
+      sse[c] += wi * e * e;
+    }
+  }
+}
+
+// sse / (clamp(|sw|, eps) * sign(sw)) per column in the input dtype (the reference's
+// _mean_squared_error_compute; sw = N without weights), then the column mean unless raw_values
+at::Tensor cpu_mse(const at::Tensor& x, const at::Tensor& t, const c10::optional<at::Tensor>& w, bool raw_values) {
+  TORCH_CHECK(!x.is_cuda() && !t.is_cuda() && x.sizes() == t.sizes() && (x.dim() == 1 || x.dim() == 2) &&
+                  x.scalar_type() == t.scalar_type() &&
+                  (x.scalar_type() == at::kFloat || x.scalar_type() == at::kDouble),
+              "cpu_mse: CPU float32 / float64 [n] or [n, d] input and target of one dtype");
+  TORCH_CHECK(!w.has_value() || (w->dim() == 1 && w->size(0) == x.size(0) && w->scalar_type() == x.scalar_type()),
+              "cpu_mse: weight [n] of the input dtype");
+  std::vector<double> sse;
+  double sw = 0.0;
+  if (x.scalar_type() == at::kFloat) mse_sums<float>(x, t, w, sse, sw);
+  else mse_sums<double>(x, t, w, sse, sw);
+  const int64_t d = static_cast<int64_t>(sse.size());
+  const bool f32 = x.scalar_type() == at::kFloat;
+  const double eps = 2.220446049250313e-16;  // torch.finfo(torch.float64).eps
+  // the divisor is float32 without weights (int64 count -> clamp(min=eps) promotes to float32)
+  // and in the weights' dtype with them
+  const double den_d = (std::fabs(sw) < eps ? eps : std::fabs(sw)) * (sw > 0 ? 1.0 : (sw < 0 ? -1.0 : 0.0));
+  const bool den_f32 = f32 || !w.has_value();
+  const double den = den_f32 ? static_cast<double>(static_cast<float>(den_d)) : den_d;
+  at::Tensor raw = at::empty(x.dim() == 2 ? std::vector<int64_t>{d} : std::vector<int64_t>{}, x.options());
+  double acc = 0.0;
+  for (int64_t c = 0; c < d; ++c) {
+    double r;
+    if (f32) {
+      const float v = static_cast<float>(sse[c]) / static_cast<float>(den);
+      r = v;
+      raw.data_ptr<float>()[c] = v;
+    } else {
+      r = sse[c] / den;
+      raw.data_ptr<double>()[c] = r;
+    }
+    acc += r;
+  }
+  if (raw_values) return raw;
+  at::Tensor out = at::empty({}, x.options());
+  if (f32) out.data_ptr<float>()[0] = static_cast<float>(acc / static_cast<double>(d));
+  else out.data_ptr<double>()[0] = acc / static_cast<double>(d);
+  return out;
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
@@ -569,6 +635,8 @@ void tea_register_cpu_metrics(pybind11::module_& m) {
         "host fast path of BinaryPrecision / BinaryRecall / BinaryF1Score.update (0-d float32 states)",
         pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("threshold"), pybind11::arg("kind"),
         pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c") = pybind11::none());
+  m.def("cpu_mse", &cpu_mse, "host fast path of the functional mean_squared_error for small CPU batches",
+        pybind11::arg("x"), pybind11::arg("t"), pybind11::arg("w") = pybind11::none(), pybind11::arg("raw_values") = false);
   m.def("cpu_binary_auc", &cpu_binary_auc, "host twin of the K3 AUROC / AUPRC rows for small CPU batches",
         pybind11::arg("x"), pybind11::arg("t"), pybind11::arg("w") = pybind11::none());
   m.def("cpu_binned_counts", &cpu_binned_counts, "host twin of binned_counts for small CPU batches");

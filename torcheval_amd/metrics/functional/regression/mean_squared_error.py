@@ -5,6 +5,7 @@ from typing import Optional, Tuple
 import torch
 
 from torcheval_amd.metrics.functional.regression._common import _native, _update
+from torcheval_amd.ops import compiling, native, native_loaded
 
 __all__ = ["mean_squared_error"]
 
@@ -25,8 +26,34 @@ def mean_squared_error(
         from torcheval_amd.ops.reductions import mse_fused
 
         return mse_fused(input, target, sample_weight, multioutput == "raw_values")
+    if _cpu_mse_ok(input, target, sample_weight):
+        _mean_squared_error_update_input_check(input, target, sample_weight)
+        return native().cpu_mse(input, target, sample_weight, multioutput == "raw_values")
     sse, sum_weight = _mean_squared_error_update(input, target, sample_weight)
     return _mean_squared_error_compute(sse, multioutput, sum_weight)
+
+
+_CPU_MSE_MAX = 1 << 16
+
+
+def _cpu_mse_ok(input: torch.Tensor, target: torch.Tensor, w: Optional[torch.Tensor]) -> bool:
+    """Small CPU batches of one float dtype: one C++ call (csrc/runtime/cpu_metrics.cpp cpu_mse)
+    instead of ~10 ATen dispatches."""
+    return (
+        input.device.type == "cpu"
+        and target.device.type == "cpu"
+        and input.dtype in (torch.float32, torch.float64)
+        and target.dtype == input.dtype
+        and input.shape == target.shape
+        and input.dim() in (1, 2)
+        and input.shape[0] > 0
+        and input.numel() <= _CPU_MSE_MAX
+        and (w is None or (isinstance(w, torch.Tensor) and w.dim() == 1 and w.dtype == input.dtype
+                           and w.device.type == "cpu" and w.shape[0] == input.shape[0]))
+        and not input.requires_grad
+        and not compiling()
+        and native_loaded()
+    )
 
 
 def _mean_squared_error_update(
