@@ -620,6 +620,62 @@ at::Tensor cpu_mse(const at::Tensor& x, const at::Tensor& t, const c10::optional
   return out;
 }
 
+// ---- functional r2_score (small CPU batches) ----
+
+template <typename S>
+at::Tensor r2_impl(const at::Tensor& x, const at::Tensor& t, int64_t mode, int64_t k) {
+  const int64_t n = x.size(0), d = x.dim() == 2 ? x.size(1) : 1;
+  const int64_t xs0 = x.stride(0), xs1 = x.dim() == 2 ? x.stride(1) : 0;
+  const int64_t ts0 = t.stride(0), ts1 = t.dim() == 2 ? t.stride(1) : 0;
+  const S* px = x.data_ptr<S>();
+  const S* pt = t.data_ptr<S>();
+  std::vector<double> sso(d, 0.0), so(d, 0.0), rss(d, 0.0);
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t c = 0; c < d; ++c) {
+      const double tv = static_cast<double>(pt[i * ts0 + c * ts1]);
+      const double e = tv - static_cast<double>(px[i * xs0 + c * xs1]);
+      sso[c] += tv * tv;
+      so[c] += tv;
+      rss[c] += e * e;
+    }
+  // the reference's arithmetic in the input dtype: tss = sso - so^2 / n, r2 = 1 - rss / tss
+  std::vector<S> tss(d), r2(d);
+  S tss_sum = 0;
+  for (int64_t c = 0; c < d; ++c) {
+    const S a = static_cast<S>(sso[c]), b = static_cast<S>(so[c]), r = static_cast<S>(rss[c]);
+    tss[c] = a - (b * b) / static_cast<S>(n);
+    r2[c] = S(1) - r / tss[c];
+    tss_sum += tss[c];
+  }
+  at::Tensor out;
+  if (mode == 0) {  // raw_values
+    out = at::empty(x.dim() == 2 ? std::vector<int64_t>{d} : std::vector<int64_t>{}, x.options());
+    for (int64_t c = 0; c < d; ++c) out.data_ptr<S>()[c] = r2[c];
+  } else {
+    double acc = 0.0;
+    for (int64_t c = 0; c < d; ++c) acc += mode == 1 ? static_cast<double>(r2[c]) : static_cast<double>(r2[c] * tss[c] / tss_sum);
+    out = at::empty({}, x.options());
+    out.data_ptr<S>()[0] = static_cast<S>(mode == 1 ? acc / static_cast<double>(d) : acc);
+  }
+  if (k != 0) {
+    S* po = out.data_ptr<S>();
+    for (int64_t c = 0; c < out.numel(); ++c)
+      po[c] = S(1) - (S(1) - po[c]) * static_cast<S>(n - 1) / static_cast<S>(n - k - 1);
+  }
+  return out;
+}
+
+// mode 0 raw_values, 1 uniform_average, 2 variance_weighted; k = num_regressors (adjusted R2);
+// the caller has checked n >= 2 and k < n - 1 (the reference's ValueErrors)
+at::Tensor cpu_r2(const at::Tensor& x, const at::Tensor& t, int64_t mode, int64_t k) {
+  TORCH_CHECK(!x.is_cuda() && !t.is_cuda() && x.sizes() == t.sizes() && (x.dim() == 1 || x.dim() == 2) &&
+                  x.scalar_type() == t.scalar_type() &&
+                  (x.scalar_type() == at::kFloat || x.scalar_type() == at::kDouble) && x.size(0) >= 2 &&
+                  mode >= 0 && mode <= 2 && k >= 0 && k < x.size(0) - 1,
+              "cpu_r2: CPU float32 / float64 [n >= 2] or [n, d] input and target of one dtype");
+  return x.scalar_type() == at::kFloat ? r2_impl<float>(x, t, mode, k) : r2_impl<double>(x, t, mode, k);
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
@@ -635,6 +691,8 @@ void tea_register_cpu_metrics(pybind11::module_& m) {
         "host fast path of BinaryPrecision / BinaryRecall / BinaryF1Score.update (0-d float32 states)",
         pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("threshold"), pybind11::arg("kind"),
         pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("c") = pybind11::none());
+  m.def("cpu_r2", &cpu_r2, "host fast path of the functional r2_score for small CPU batches", pybind11::arg("x"),
+        pybind11::arg("t"), pybind11::arg("mode"), pybind11::arg("num_regressors"));
   m.def("cpu_mse", &cpu_mse, "host fast path of the functional mean_squared_error for small CPU batches",
         pybind11::arg("x"), pybind11::arg("t"), pybind11::arg("w") = pybind11::none(), pybind11::arg("raw_values") = false);
   m.def("cpu_binary_auc", &cpu_binary_auc, "host twin of the K3 AUROC / AUPRC rows for small CPU batches",

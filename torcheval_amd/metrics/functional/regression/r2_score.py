@@ -5,6 +5,7 @@ from typing import Tuple
 import torch
 
 from torcheval_amd.metrics.functional.regression._common import _native
+from torcheval_amd.ops import compiling, native, native_loaded
 
 __all__ = ["r2_score"]
 
@@ -20,7 +21,8 @@ def r2_score(
     """Coefficient of determination; ``multioutput`` in uniform_average | raw_values |
     variance_weighted; ``num_regressors`` > 0 gives adjusted R2.  Class: ``R2Score``."""
     _r2_score_param_check(multioutput, num_regressors)
-    if _native(input, target):
+    cpu_twin = _cpu_r2_ok(input, target)
+    if _native(input, target) or cpu_twin:
         # the sample count is known on the host: the reference's checks need no device sync
         _r2_score_update_input_check(input, target)
         n = target.size(0)
@@ -33,11 +35,31 @@ def r2_score(
                 "The `num_regressors` must be smaller than n_samples - 1, "
                 f"got num_regressors={num_regressors}, n_samples={torch.tensor(n)}."
             )
+        if cpu_twin:  # small CPU batches: one C++ call instead of ~12 ATen dispatches
+            return native().cpu_r2(input, target, _R2_MODES[multioutput], num_regressors)
         from torcheval_amd.ops.reductions import r2_fused
 
         return r2_fused(input, target, multioutput, num_regressors)
     stats = _r2_score_update(input, target)
     return _r2_score_compute(*stats, multioutput, num_regressors)
+
+
+_R2_MODES = {"raw_values": 0, "uniform_average": 1, "variance_weighted": 2}
+
+
+def _cpu_r2_ok(input: torch.Tensor, target: torch.Tensor) -> bool:
+    return (
+        input.device.type == "cpu"
+        and target.device.type == "cpu"
+        and input.dtype in (torch.float32, torch.float64)
+        and target.dtype == input.dtype
+        and input.shape == target.shape
+        and input.dim() in (1, 2)
+        and input.numel() <= (1 << 16)
+        and not input.requires_grad
+        and not compiling()
+        and native_loaded()
+    )
 
 
 def _r2_score_update(
