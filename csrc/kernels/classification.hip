@@ -486,14 +486,14 @@ __device__ __forceinline__ bool micro_row(const MicroPendArgs& a, const char* __
   return __ballot(tie) == 0;
 }
 
-template <int KIND, typename TGT>
-__global__ __launch_bounds__(kBlock) void cls_micro_pend_kernel(MicroPendArgs a) {
+template <int KIND, typename TGT, int WPB>
+__global__ __launch_bounds__(WPB * kWave) void cls_micro_pend_kernel(MicroPendArgs a) {
   constexpr int ELSIZE = KIND == 0 ? 4 : 2;
   const int lane = lane_id();
-  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  const int64_t nwaves = static_cast<int64_t>(gridDim.x) * WPB;
   // the wave's first row is loaded unconditionally (clamped to the last row), so nothing
   // branches on `n` before the loads and every kernel argument arrives in one scalar round trip
-  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id();
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * WPB + wave_id();
   const int64_t r0 = row0 < a.n ? row0 : a.n - 1;  // the launcher guarantees n >= 1
   const bool c0 = micro_row<KIND, TGT>(a, static_cast<const char*>(a.input) + r0 * a.row_stride * ELSIZE,
                                        static_cast<const TGT*>(a.target)[r0], lane);
@@ -506,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void cls_micro_pend_kernel(MicroPendArgs a)
   // block barrier, no returning atomic on the kernel's tail (the fold's ~0.6 us + the block
   // reduction's ~0.45 us in the A/B harness); the metric folds the cells at compute / sync
   if (lane == 0 && correct_acc)
-    atomicAdd(a.pend + ((blockIdx.x * kWavesPerBlock + wave_id()) % kPendCells) * kPendStride,
+    atomicAdd(a.pend + ((blockIdx.x * WPB + wave_id()) % kPendCells) * kPendStride,
               static_cast<unsigned long long>(correct_acc));
   if (blockIdx.x == 0 && threadIdx.x == 0 && a.total) atomicAdd(a.total, static_cast<float>(a.n));
 }
@@ -662,10 +662,24 @@ void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
                           a.cls_label == nullptr && a.err == nullptr && a.err_max == nullptr && !a.check_target;
   if (micro_only && a.pend && (a.tg_dt == DType::i64 || a.tg_dt == DType::i32)) {
     const MicroPendArgs m{a.input, a.target, a.pend, a.micro_total, a.n, a.row_stride, static_cast<int32_t>(a.c), 0};
+    // TORCHEVAL_AMD_K1_WPB=8: 512-thread workgroups (the same one wave per row; A/B of the
+    // workgroup size, profiles/k1_floor_launch_overhead_r4.txt)
+    static const int wpb = [] {
+      const char* e = std::getenv("TORCHEVAL_AMD_K1_WPB");
+      return (e && std::atoi(e) == 8) ? 8 : 4;
+    }();
+    if (wpb == 8) {
+      const int g8 = stream_grid(a.n, 8, a.max_blocks > 0 ? (a.max_blocks + 1) / 2 : 1024);
+      if (a.tg_dt == DType::i64)
+        hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t, 8>), dim3(g8), dim3(8 * kWave), 0, s, m);
+      else
+        hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t, 8>), dim3(g8), dim3(8 * kWave), 0, s, m);
+      return;
+    }
     if (a.tg_dt == DType::i64)
-      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t>), dim3(grid), dim3(kBlock), 0, s, m);
+      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t, kWavesPerBlock>), dim3(grid), dim3(kBlock), 0, s, m);
     else
-      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t>), dim3(grid), dim3(kBlock), 0, s, m);
+      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t, kWavesPerBlock>), dim3(grid), dim3(kBlock), 0, s, m);
     return;
   }
   if (micro_only && a.tg_dt == DType::i64) {
