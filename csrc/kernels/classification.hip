@@ -662,11 +662,13 @@ void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
                           a.cls_label == nullptr && a.err == nullptr && a.err_max == nullptr && !a.check_target;
   if (micro_only && a.pend && (a.tg_dt == DType::i64 || a.tg_dt == DType::i32)) {
     const MicroPendArgs m{a.input, a.target, a.pend, a.micro_total, a.n, a.row_stride, static_cast<int32_t>(a.c), 0};
-    // TORCHEVAL_AMD_K1_WPB=8: 512-thread workgroups (the same one wave per row; A/B of the
-    // workgroup size, profiles/k1_floor_launch_overhead_r4.txt)
+    // 512-thread workgroups (8 waves, still one wave per row, 1024 blocks): the driver command
+    // 144.9k vs 142.7k updates/s with 4-wave workgroups, interleaved on one box, and the floor
+    // harness 6.23 vs 6.30 us per launch (profiles/k1_wpb_ab_r4.txt).  TORCHEVAL_AMD_K1_WPB=4
+    // selects the 256-thread form.
     static const int wpb = [] {
       const char* e = std::getenv("TORCHEVAL_AMD_K1_WPB");
-      return (e && std::atoi(e) == 8) ? 8 : 4;
+      return (e && std::atoi(e) == 4) ? 4 : 8;
     }();
     if (wpb == 8) {
       const int g8 = stream_grid(a.n, 8, a.max_blocks > 0 ? (a.max_blocks + 1) / 2 : 1024);
