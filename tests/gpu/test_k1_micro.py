@@ -89,3 +89,14 @@ def test_graph_replays_are_folded():
     for _ in range(5):
         step(xd, yd)
     assert float(m.num_correct) == 5 * hits and float(m.num_total) == 5 * 8192
+
+
+@pytest.mark.parametrize("n", [1, 7, 9, 8191, 8193, 20001])
+def test_micro_kernel_ragged_and_grid_stride_rows(n):
+    """8-wave workgroups, one wave per row: a partial last workgroup (n % 8 != 0) and more rows
+    than the 1024 x 8 waves of one grid pass (grid-stride)."""
+    x, y = _adversarial(n, 1000, torch.float32, 3)
+    want = (_ref_argmax(x) == y).sum().item()
+    m = MulticlassAccuracy(device=DEV)
+    m.update(x.to(DEV), y.to(DEV))
+    assert float(m.num_correct) == want and float(m.num_total) == n
