@@ -921,7 +921,7 @@ void perplexity_sums(const Tensor& input, const Tensor& target, optional<int64_t
   if (err.has_value()) a.err = err->data_ptr<int>();
   Tensor ws;
   if (deterministic && a.rows > 0) {
-    ws = at::empty({2 * tea::perplexity_blocks(a.rows)}, out.options());
+    ws = at::empty({2 * tea::perplexity_blocks(a)}, out.options());
     a.ordered_ws = ws.data_ptr<double>();
   }
   const int rc = tea::launch_perplexity(a, stream_for(input));

@@ -324,7 +324,7 @@ struct PerplexityArgs {
   int* err = nullptr;
   double* ordered_ws = nullptr;  // deterministic mode: [2, perplexity_blocks] partials
 };
-int perplexity_blocks(int64_t rows);
+int perplexity_blocks(const PerplexityArgs& a);  // grid of the launch launch_perplexity makes
 int launch_perplexity(const PerplexityArgs& a, hipStream_t stream);
 
 }  // namespace tea

@@ -11,6 +11,8 @@
 #include "tea_common.h"
 #include "tea_kernels.h"
 
+#include <cstdlib>
+
 namespace tea {
 
 namespace {
@@ -144,19 +146,39 @@ void launch_kind(const PerplexityArgs& a, int grid, bool vec, hipStream_t s) {
 
 }  // namespace
 
-int perplexity_blocks(int64_t rows) {
-  int64_t grid = (rows + kWpb - 1) / kWpb;
-  if (grid > 512) grid = 512;
+namespace {
+
+bool vec_ok(const PerplexityArgs& a) {
+  const uintptr_t base = reinterpret_cast<uintptr_t>(a.input);
+  const int vw = a.in_dt == DType::f32 ? 4 : 8;
+  return a.v % 16 == 0 && a.row_stride % vw == 0 && base % 16 == 0;
+}
+
+}  // namespace
+
+// Grid cap in 4-wave blocks; rows past cap * 4 waves are grid-strided.  1024 (one row per wave
+// up to 4096 rows) except 16-B fp32 batches of <= 8192 rows, where 512 (two rows per wave)
+// streams faster: measured per shape (profiles/k7_grid_cap_ab_r4.json): 16384 x 32000 bf16
+// 251 -> 189 us, 4096 x 50257 fp32 (scalar path) 769 -> 429 us, 65536 x 4096 fp32 188 -> 178 us,
+// but 4096 x 32000 fp32 92 vs 98.6 us and 8192 x 1024 fp32 16 vs 19.5 us with 512.
+// TORCHEVAL_AMD_PPL_MAXGRID overrides (A/B).
+int perplexity_blocks(const PerplexityArgs& a) {
+  static const int64_t forced = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_PPL_MAXGRID");
+    const long v = e ? std::atol(e) : 0;
+    return v > 0 ? static_cast<int64_t>(v) : int64_t(0);
+  }();
+  const int64_t cap = forced > 0 ? forced : (a.in_dt == DType::f32 && vec_ok(a) && a.rows <= 8192 ? 512 : 1024);
+  int64_t grid = (a.rows + kWpb - 1) / kWpb;
+  if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
   return static_cast<int>(grid);
 }
 
 int launch_perplexity(const PerplexityArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
-  const int64_t grid = perplexity_blocks(a.rows);
-  const uintptr_t base = reinterpret_cast<uintptr_t>(a.input);
-  const int vw = a.in_dt == DType::f32 ? 4 : 8;
-  const bool vec = a.v % 16 == 0 && a.row_stride % vw == 0 && base % 16 == 0;
+  const int64_t grid = perplexity_blocks(a);
+  const bool vec = vec_ok(a);
   switch (a.in_dt) {
     case DType::f32: launch_kind<0>(a, static_cast<int>(grid), vec, stream); break;
     case DType::bf16: launch_kind<1>(a, static_cast<int>(grid), vec, stream); break;
