@@ -926,6 +926,7 @@ void perplexity_sums(const Tensor& input, const Tensor& target, optional<int64_t
   }
   const int rc = tea::launch_perplexity(a, stream_for(input));
   TORCH_CHECK(rc != -1, "perplexity: unsupported logits dtype ", input.scalar_type());
+  TORCH_CHECK(rc != -2, "perplexity: logits storage is not element-aligned");
   check_launch(rc, "perplexity");
 }
 

@@ -6,7 +6,8 @@
 // once with 16-B loads, keeping a per-lane online (max, sum-exp) pair that is rescaled once per
 // 16-value chunk; lanes combine their pairs with xor shuffles; lane 0 adds
 //   -log p(target) = logsumexp(row) - row[target]
-// in FP64.  ``ignore_index`` rows are skipped and counted out; targets outside [0, V) are
+// in FP64.  Rows that do not start 16-B aligned (odd vocabularies) stream a scalar head, a 16-B
+// body and a scalar tail.  ``ignore_index`` rows are skipped and counted out; targets outside [0, V) are
 // flagged on device (``err``) instead of the reference's host-synchronising max() check.
 #include "tea_common.h"
 #include "tea_kernels.h"
@@ -64,6 +65,34 @@ __device__ __forceinline__ void combine(float& m, float& s, float m2, float s2) 
   m = mn;
 }
 
+// One 16-value chunk at p[base .. base + 16) (16-B aligned; the upper 8 only when below n).
+template <int KIND>
+__device__ __forceinline__ void chunk16(const void* p, int64_t base, int64_t n, float& m, float& s) {
+  float v[2][8];
+  load8<KIND>(p, base, v[0]);
+  if (base + 8 < n) {
+    load8<KIND>(p, base + 8, v[1]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[1][e] = -__builtin_huge_valf();
+  }
+  float cm = v[0][0];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cm = fmaxf(cm, v[h][e]);
+  float cs = 0.f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs += __expf(v[h][e] - cm);
+  combine(m, s, cm, cs);
+}
+
+// VEC: every row starts 16-B aligned and V % 16 == 0.  Otherwise (odd vocabularies such as
+// GPT-2's 50257, or row strides that break 16-B alignment) each row is split into a scalar head
+// up to the next 16-B boundary (< 16 / ELS values, one per lane), a 16-B-load body of whole
+// 16-value chunks and a scalar tail (< 16 values); rows are element-aligned (checked on the host).
 template <int KIND, bool VEC>
 __global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
   const int lane = lane_id();
@@ -76,32 +105,19 @@ __global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
     const void* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELS;
     float m = -__builtin_huge_valf(), s = 0.f;
     if constexpr (VEC) {
-      for (int64_t base = static_cast<int64_t>(lane) * 16; base < a.v; base += kWave * 16) {
-        float v[2][8];
-        load8<KIND>(rp, base, v[0]);
-        if (base + 8 < a.v) {
-          load8<KIND>(rp, base + 8, v[1]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[1][e] = -__builtin_huge_valf();
-        }
-        float cm = v[0][0];
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) cm = fmaxf(cm, v[h][e]);
-        float cs = 0.f;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-          for (int e = 0; e < 8; ++e) cs += __expf(v[h][e] - cm);
-        combine(m, s, cm, cs);
-      }
+      for (int64_t base = static_cast<int64_t>(lane) * 16; base < a.v; base += kWave * 16)
+        chunk16<KIND>(rp, base, a.v, m, s);
     } else {
-      for (int64_t c = lane; c < a.v; c += kWave) {
-        const float x = load1<KIND>(rp, c);
-        combine(m, s, x, 1.f);
-      }
+      const uintptr_t addr = reinterpret_cast<uintptr_t>(rp);
+      int64_t head = static_cast<int64_t>(((16u - (addr & 15u)) & 15u) / ELS);
+      if (head > a.v) head = a.v;
+      const int64_t nb = ((a.v - head) / 16) * 16;
+      if (lane < head) combine(m, s, load1<KIND>(rp, lane), 1.f);
+      const void* bp = static_cast<const char*>(rp) + head * ELS;
+      for (int64_t base = static_cast<int64_t>(lane) * 16; base < nb; base += kWave * 16)
+        chunk16<KIND>(bp, base, nb, m, s);
+      const int64_t c = head + nb + lane;
+      if (c < a.v) combine(m, s, load1<KIND>(rp, c), 1.f);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -157,18 +173,18 @@ bool vec_ok(const PerplexityArgs& a) {
 }  // namespace
 
 // Grid cap in 4-wave blocks; rows past cap * 4 waves are grid-strided.  1024 (one row per wave
-// up to 4096 rows) except 16-B fp32 batches of <= 8192 rows, where 512 (two rows per wave)
-// streams faster: measured per shape (profiles/k7_grid_cap_ab_r4.json): 16384 x 32000 bf16
-// 251 -> 189 us, 4096 x 50257 fp32 (scalar path) 769 -> 429 us, 65536 x 4096 fp32 188 -> 178 us,
-// but 4096 x 32000 fp32 92 vs 98.6 us and 8192 x 1024 fp32 16 vs 19.5 us with 512.
-// TORCHEVAL_AMD_PPL_MAXGRID overrides (A/B).
+// up to 4096 rows) except fp32 batches of <= 8192 rows, where 512 (two rows per wave) streams
+// faster: measured per shape (profiles/k7_grid_cap_ab_r4.json): 16384 x 32000 bf16 251 -> 189 us,
+// 65536 x 4096 fp32 184 -> 177 us with 1024, but 4096 x 32000 fp32 92 vs 99 us, 4096 x 50257
+// fp32 139 vs 150 us and 8192 x 1024 fp32 16 vs 19 us with 512.  TORCHEVAL_AMD_PPL_MAXGRID
+// overrides (A/B).
 int perplexity_blocks(const PerplexityArgs& a) {
   static const int64_t forced = [] {
     const char* e = std::getenv("TORCHEVAL_AMD_PPL_MAXGRID");
     const long v = e ? std::atol(e) : 0;
     return v > 0 ? static_cast<int64_t>(v) : int64_t(0);
   }();
-  const int64_t cap = forced > 0 ? forced : (a.in_dt == DType::f32 && vec_ok(a) && a.rows <= 8192 ? 512 : 1024);
+  const int64_t cap = forced > 0 ? forced : (a.in_dt == DType::f32 && a.rows <= 8192 ? 512 : 1024);
   int64_t grid = (a.rows + kWpb - 1) / kWpb;
   if (grid > cap) grid = cap;
   if (grid < 1) grid = 1;
@@ -179,6 +195,8 @@ int launch_perplexity(const PerplexityArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
   const int64_t grid = perplexity_blocks(a);
   const bool vec = vec_ok(a);
+  const int els = a.in_dt == DType::f32 ? 4 : 2;
+  if (reinterpret_cast<uintptr_t>(a.input) % els != 0) return -2;  // split path needs element alignment
   switch (a.in_dt) {
     case DType::f32: launch_kind<0>(a, static_cast<int>(grid), vec, stream); break;
     case DType::bf16: launch_kind<1>(a, static_cast<int>(grid), vec, stream); break;

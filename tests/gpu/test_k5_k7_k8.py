@@ -148,6 +148,25 @@ def test_k7_many_long_rows_strided_and_deterministic():
     assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("off", [1, 2, 3, 5])
+@pytest.mark.parametrize("vocab", [3, 5, 40, 1000, 50257])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_k7_split_rows_head_body_tail(off, vocab, dtype):
+    """Rows that do not start 16-B aligned (column offset into a wider buffer, odd vocab) take
+    the scalar head / 16-B body / scalar tail split; the max sits in the head of one row and
+    in the tail of another, and V smaller than the head is covered by vocab 3 and 5."""
+    g = torch.Generator().manual_seed(off * 100 + vocab)
+    big = (torch.randn(3, 37, vocab + off + 7, generator=g) * 4).to(dtype)
+    x = big[..., off:off + vocab]
+    x[0, 0, 0] = 40.0
+    x[0, 1, vocab - 1] = 40.0
+    t = torch.randint(0, vocab, (3, 37), generator=g)
+    t[0, 0], t[0, 1] = 0, vocab - 1
+    xd = big.to(DEV)[..., off:off + vocab]
+    got = float(perplexity(xd, t.to(DEV)))
+    assert got == pytest.approx(_ppl_ref(x, t), rel=2e-5)
+
+
 def test_k7_long_row_invalid_target_raises():
     x = torch.randn(2, 2, 4096, device=DEV)
     with pytest.raises(ValueError, match="vocab_size minus one"):
