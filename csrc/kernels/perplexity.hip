@@ -89,11 +89,41 @@ __device__ __forceinline__ void chunk16(const void* p, int64_t base, int64_t n, 
   combine(m, s, cm, cs);
 }
 
+// Stream n values (n % 16 == 0, p 16-B aligned) as 16-value chunks per lane.  U2: two chunks a
+// wave-stride apart are loaded before either is reduced (four 16-B loads in flight per lane),
+// for batches with too few rows to fill the CUs with waves.
+template <int KIND, bool U2>
+__device__ __forceinline__ void stream_row(const void* p, int64_t n, int lane, float& m, float& s) {
+  constexpr int64_t step = kWave * 16;
+  int64_t base = static_cast<int64_t>(lane) * 16;
+  if constexpr (U2) {
+    for (; base + step < n; base += 2 * step) {
+      float v[4][8];
+      load8<KIND>(p, base, v[0]);
+      load8<KIND>(p, base + 8, v[1]);
+      load8<KIND>(p, base + step, v[2]);
+      load8<KIND>(p, base + step + 8, v[3]);
+      float cm = v[0][0];
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cm = fmaxf(cm, v[h][e]);
+      float cs = 0.f;
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) cs += __expf(v[h][e] - cm);
+      combine(m, s, cm, cs);
+    }
+  }
+  for (; base < n; base += step) chunk16<KIND>(p, base, n, m, s);
+}
+
 // VEC: every row starts 16-B aligned and V % 16 == 0.  Otherwise (odd vocabularies such as
 // GPT-2's 50257, or row strides that break 16-B alignment) each row is split into a scalar head
 // up to the next 16-B boundary (< 16 / ELS values, one per lane), a 16-B-load body of whole
 // 16-value chunks and a scalar tail (< 16 values); rows are element-aligned (checked on the host).
-template <int KIND, bool VEC>
+template <int KIND, bool VEC, bool U2>
 __global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
   const int lane = lane_id();
   const int64_t nw = static_cast<int64_t>(gridDim.x) * kWpb;
@@ -105,8 +135,7 @@ __global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
     const void* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELS;
     float m = -__builtin_huge_valf(), s = 0.f;
     if constexpr (VEC) {
-      for (int64_t base = static_cast<int64_t>(lane) * 16; base < a.v; base += kWave * 16)
-        chunk16<KIND>(rp, base, a.v, m, s);
+      stream_row<KIND, U2>(rp, a.v, lane, m, s);
     } else {
       const uintptr_t addr = reinterpret_cast<uintptr_t>(rp);
       int64_t head = static_cast<int64_t>(((16u - (addr & 15u)) & 15u) / ELS);
@@ -114,8 +143,7 @@ __global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
       const int64_t nb = ((a.v - head) / 16) * 16;
       if (lane < head) combine(m, s, load1<KIND>(rp, lane), 1.f);
       const void* bp = static_cast<const char*>(rp) + head * ELS;
-      for (int64_t base = static_cast<int64_t>(lane) * 16; base < nb; base += kWave * 16)
-        chunk16<KIND>(bp, base, nb, m, s);
+      stream_row<KIND, U2>(bp, nb, lane, m, s);
       const int64_t c = head + nb + lane;
       if (c < a.v) combine(m, s, load1<KIND>(rp, c), 1.f);
     }
@@ -153,11 +181,15 @@ __global__ __launch_bounds__(kB) void perplexity_kernel(PerplexityArgs a) {
 }
 
 template <int KIND>
-void launch_kind(const PerplexityArgs& a, int grid, bool vec, hipStream_t s) {
-  if (vec)
-    hipLaunchKernelGGL((perplexity_kernel<KIND, true>), dim3(grid), dim3(kB), 0, s, a);
+void launch_kind(const PerplexityArgs& a, int grid, bool vec, bool u2, hipStream_t s) {
+  if (vec && u2)
+    hipLaunchKernelGGL((perplexity_kernel<KIND, true, true>), dim3(grid), dim3(kB), 0, s, a);
+  else if (vec)
+    hipLaunchKernelGGL((perplexity_kernel<KIND, true, false>), dim3(grid), dim3(kB), 0, s, a);
+  else if (u2)
+    hipLaunchKernelGGL((perplexity_kernel<KIND, false, true>), dim3(grid), dim3(kB), 0, s, a);
   else
-    hipLaunchKernelGGL((perplexity_kernel<KIND, false>), dim3(grid), dim3(kB), 0, s, a);
+    hipLaunchKernelGGL((perplexity_kernel<KIND, false, false>), dim3(grid), dim3(kB), 0, s, a);
 }
 
 }  // namespace
@@ -195,12 +227,19 @@ int launch_perplexity(const PerplexityArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
   const int64_t grid = perplexity_blocks(a);
   const bool vec = vec_ok(a);
+  static const int u2_env = [] {  // A/B: TORCHEVAL_AMD_PPL_U2=0/1 forces the unrolled body off/on
+    const char* e = std::getenv("TORCHEVAL_AMD_PPL_U2");
+    return e ? std::atoi(e) : -1;
+  }();
   const int els = a.in_dt == DType::f32 ? 4 : 2;
+  // Unrolled body unless the batch already fills the CUs with many short rows (profiles/
+  // k7_grid_cap_ab_r4.json: 2048 x 128256 bf16 125 -> 92 us, 65536 x 4096 fp32 177 vs 184 us).
+  const bool u2 = u2_env >= 0 ? u2_env != 0 : (a.rows <= 16384 || a.v * els >= 65536);
   if (reinterpret_cast<uintptr_t>(a.input) % els != 0) return -2;  // split path needs element alignment
   switch (a.in_dt) {
-    case DType::f32: launch_kind<0>(a, static_cast<int>(grid), vec, stream); break;
-    case DType::bf16: launch_kind<1>(a, static_cast<int>(grid), vec, stream); break;
-    case DType::f16: launch_kind<2>(a, static_cast<int>(grid), vec, stream); break;
+    case DType::f32: launch_kind<0>(a, static_cast<int>(grid), vec, u2, stream); break;
+    case DType::bf16: launch_kind<1>(a, static_cast<int>(grid), vec, u2, stream); break;
+    case DType::f16: launch_kind<2>(a, static_cast<int>(grid), vec, u2, stream); break;
     default: return -1;
   }
   if (a.ordered_ws) return launch_ordered_sum(a.ordered_ws, 2, grid, a.out, stream);
