@@ -698,18 +698,22 @@ void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<T
     return;
   }
   c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
-  // long rows: partials + ordered combine (two launches) by default; TORCHEVAL_AMD_K5B_FOLD=1
-  // selects the one-launch fold (half the host cost, same device time at 8192 x 1000:
-  // 18.0 vs 11.2 + 5.7 us; profiles/k5b_rowsums_r2.md)
-  static const bool two_launch = [] {
-    const char* e = std::getenv("TORCHEVAL_AMD_K5B_FOLD");
-    return !(e != nullptr && e[0] == '1');
+  // long rows: partials + ordered combine in two launches by default (TORCHEVAL_AMD_K5B_MODE=1:
+  // the fat-block fold with a release fence per block; =2: one launch with write-through
+  // partials and a last-block combine - measured 14.5 vs 11.4 us for Sum 8192 x 1000,
+  // profiles/odd_width_cliff_r5_k5.json: the hand-off sits on the launch's tail)
+  static const int mode = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K5B_MODE");
+    return (e != nullptr && e[0] != '\0') ? std::atoi(e) : 0;
   }();
-  a.blocks = two_launch ? tea::row_sums_blocks(a.rows, a.n) : tea::row_sums_fold_blocks(a.rows, a.n);
+  a.blocks = mode == 0 ? tea::row_sums_blocks(a.rows, a.n)
+                       : mode == 1 ? tea::row_sums_fold_blocks(a.rows, a.n) : tea::row_sums_wt_blocks(a.rows, a.n);
   if (a.blocks > 1) {  // stream-ordered scratch, fully rewritten by every call: cached, no allocation
     a.ws = static_cast<double*>(zeroed_workspace(x, stream_for(x), a.rows * a.blocks * tea::kRowRaw * 8, 3));
-    if (!two_launch)  // self-cleaning arrival tickets
+    if (mode != 0) {  // self-cleaning arrival tickets
       a.ticket = static_cast<unsigned*>(zeroed_workspace(x, stream_for(x), a.rows * 4, 4));
+      a.wt = mode == 2;
+    }
   }
   if (a.n == 0 && a.rows > 0) a.blocks = 1;
   check_launch(tea::launch_row_sums(a, stream_for(x)), "row_sums");
@@ -777,15 +781,12 @@ void binned_counts(const Tensor& input, const Tensor& target, const Tensor& thr,
 // ---------------------------------------------------------------- K5 / K6 reductions
 // x, t: [n, d] views (t optional); w: optional [n]; outputs float32 (accumulated):
 // sse/st/stt/sx as [d] views sharing one stride, sw scalar.
-void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
-                    const optional<Tensor>& w, const optional<Tensor>& sse,
-                    const optional<Tensor>& st, const optional<Tensor>& stt,
-                    const optional<Tensor>& sx, const optional<Tensor>& sw, int64_t overwrite,
-                    int64_t mse_mode, const optional<Tensor>& mse_out, int64_t num_regressors) {
-  const Tensor& ref = x.has_value() ? *x : *t;
-  check_gpu(ref, "x/t");
-  TORCH_CHECK(ref.dim() == 2, "column_moments: inputs must be [n, d] views");
-  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ref.device());
+// x, t: [n, d] views; w: [n]; outputs float32 [d] sharing a stride, sw scalar (shared by
+// column_moments / column_moments_pend / column_moments_fold)
+static tea::MomentsArgs moments_args(const optional<Tensor>& x, const optional<Tensor>& t,
+                                     const optional<Tensor>& w, const optional<Tensor>& sse,
+                                     const optional<Tensor>& st, const optional<Tensor>& stt,
+                                     const optional<Tensor>& sx, const optional<Tensor>& sw, const Tensor& ref) {
   tea::MomentsArgs a;
   a.n = ref.size(0);
   a.d = ref.size(1);
@@ -828,6 +829,59 @@ void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
     TORCH_CHECK(sw->scalar_type() == at::kFloat && sw->numel() == 1, "column_moments: sw scalar f32");
     a.sw = sw->data_ptr<float>();
   }
+  return a;
+}
+
+static void bind_pend(tea::MomentsArgs& a, const Tensor& pend, const Tensor& ref) {
+  TORCH_CHECK(pend.scalar_type() == at::kDouble && pend.is_contiguous() && pend.device() == ref.device() &&
+                  pend.numel() >= tea::kMomentsPendSlots * (tea::moments_ns(a) * a.d + 1),
+              "column_moments: pend must be a contiguous float64 buffer of slots * (ns * d + 1)");
+  a.pend = pend.data_ptr<double>();
+  a.pend_slots = tea::kMomentsPendSlots;
+}
+
+// deferred-mode class update: FP64 column partials ADDED to the slots of `pend` (zero-initialised
+// by the caller, zeroed again by column_moments_fold); the states are only the statistic
+// selection here.  Returns the slots used (0: not applicable, the caller takes another path).
+int64_t column_moments_pend(const optional<Tensor>& x, const optional<Tensor>& t, const optional<Tensor>& w,
+                            const optional<Tensor>& sse, const optional<Tensor>& st, const optional<Tensor>& stt,
+                            const optional<Tensor>& sx, const optional<Tensor>& sw, const Tensor& pend) {
+  const Tensor& ref = x.has_value() ? *x : *t;
+  check_gpu(ref, "x/t");
+  TORCH_CHECK(ref.dim() == 2, "column_moments: inputs must be [n, d] views");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ref.device());
+  tea::MomentsArgs a = moments_args(x, t, w, sse, st, stt, sx, sw, ref);
+  if (a.n == 0 || a.d == 0) return 0;
+  bind_pend(a, pend, ref);
+  int64_t wsd = 0, tk = 0;
+  if (!tea::column_moments_v2_plan(a, &wsd, &tk)) return 0;
+  check_launch(tea::launch_column_moments(a, stream_for(ref)), "column_moments_pend");
+  return a.v2_r;
+}
+
+// fold the first `slots` pending slots into the states (float32 +=) and zero them
+void column_moments_fold(const Tensor& pend, int64_t slots, const optional<Tensor>& sse,
+                         const optional<Tensor>& st, const optional<Tensor>& stt, const optional<Tensor>& sx,
+                         const optional<Tensor>& sw) {
+  const Tensor& like = sse.has_value() ? *sse : st.has_value() ? *st : *stt;
+  check_gpu(like, "states");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(like.device());
+  const Tensor ref = at::empty({0, like.numel()}, like.options());  // shape carrier: n = 0, d
+  tea::MomentsArgs a = moments_args(c10::nullopt, c10::nullopt, c10::nullopt, sse, st, stt, sx, sw, ref);
+  bind_pend(a, pend, like);
+  check_launch(tea::launch_moments_fold(a, static_cast<int>(slots), stream_for(like)), "column_moments_fold");
+}
+
+void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
+                    const optional<Tensor>& w, const optional<Tensor>& sse,
+                    const optional<Tensor>& st, const optional<Tensor>& stt,
+                    const optional<Tensor>& sx, const optional<Tensor>& sw, int64_t overwrite,
+                    int64_t mse_mode, const optional<Tensor>& mse_out, int64_t num_regressors) {
+  const Tensor& ref = x.has_value() ? *x : *t;
+  check_gpu(ref, "x/t");
+  TORCH_CHECK(ref.dim() == 2, "column_moments: inputs must be [n, d] views");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(ref.device());
+  tea::MomentsArgs a = moments_args(x, t, w, sse, st, stt, sx, sw, ref);
   a.overwrite = overwrite != 0;
   a.mse_mode = static_cast<int>(mse_mode);
   Tensor raw_scratch;
@@ -847,6 +901,14 @@ void column_moments(const optional<Tensor>& x, const optional<Tensor>& t,
     }
   }
   if (a.n == 0 || a.d == 0) return;
+  int64_t v2_doubles = 0, v2_tickets = 0;
+  if (tea::column_moments_v2_plan(a, &v2_doubles, &v2_tickets)) {  // one launch (K5 v2)
+    hipStream_t st = stream_for(ref);
+    a.part = static_cast<double*>(scratch_workspace(ref, st, v2_doubles * 8, 8));
+    a.tickets = static_cast<unsigned*>(zeroed_workspace(ref, st, v2_tickets * 4, 8));
+    check_launch(tea::launch_column_moments(a, st), "column_moments");
+    return;
+  }
   a.ws_blocks = tea::column_moments_blocks(a.n, a.d);
   const int64_t nstats = (a.sse != nullptr) + (a.st != nullptr) + (a.stt != nullptr) + (a.sx != nullptr);
   Tensor ws = at::empty({a.ws_blocks * (nstats * a.d + 1)}, ref.options().dtype(at::kDouble));
@@ -1323,6 +1385,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"),
         py::arg("sx"), py::arg("sw"), py::arg("overwrite") = 0, py::arg("mse_mode") = 0,
         py::arg("mse_out") = py::none(), py::arg("num_regressors") = 0);
+  m.def("column_moments_pend", &column_moments_pend,
+        "K5 deferred-mode class update: FP64 column partials added to pending slots; returns the slots used",
+        py::arg("x"), py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),
+        py::arg("sw"), py::arg("pend"));
+  m.def("column_moments_fold", &column_moments_fold, "K5 pending slots -> float32 states (+=), slots zeroed",
+        py::arg("pend"), py::arg("slots"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),
+        py::arg("sw"));
   m.def("ne_sums", &ne_sums, "K6 normalized-entropy row sums", py::arg("x"), py::arg("t"),
         py::arg("w"), py::arg("from_logits"), py::arg("out"), py::arg("err"),
         py::arg("deterministic") = false);

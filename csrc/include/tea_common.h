@@ -133,6 +133,57 @@ __device__ __forceinline__ T block_sum(T v, T* lds /* >= 16 entries */) {
   return s;
 }
 
+// ------------------------------------------------------------------ 16-B loads at 4-B alignment
+// gfx950 serves a global_load_dwordx4 from any 4-B-aligned address at the aligned rate
+// (csrc/bench/unaligned_probe.hip, profiles/unaligned_probe_r5.txt: 8192 x 1001 f32 rows 6.0-6.1 us
+// vs 5.9 us for 8192 x 1000; a column walk 5.8 us at both widths).  Rows of an odd width therefore
+// keep 16-B loads: the type below tells the compiler the address is only 4-B aligned (so it must
+// not assume more), and the load is still one dwordx4.
+typedef float f4u_t __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ float4 load_f4u(const float* p) {
+  const f4u_t v = *reinterpret_cast<const f4u_t*>(p);
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+
+// ------------------------------------------------------------------ write-through hand-off
+// Per-block partials handed to the block that arrives last on a ticket, inside one launch
+// (MI355X_MICROARCH.md, visibility table row 1): every partial is stored write-through (sc1:
+// an agent-scope relaxed atomic store, GLOBAL address space so it is never a flat store),
+// every storing wave drains (vmcnt(0)), the workgroup barrier, then ONE lane adds to the
+// ticket; the block whose add returns the last count reads the partials with sc1 loads only.
+// No release / acquire fence (each costs a buffer_wbl2 / buffer_inv of ~1.7 us).
+typedef __attribute__((address_space(1))) unsigned long long wt_u64;
+typedef __attribute__((address_space(1))) unsigned wt_u32;
+
+__device__ __forceinline__ void wt_store(double* p, double v) {
+  __hip_atomic_store((wt_u64*)(p), static_cast<unsigned long long>(__double_as_longlong(v)),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double wt_load(const double* p) {
+  return __longlong_as_double(static_cast<long long>(
+      __hip_atomic_load((wt_u64*)(const_cast<double*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)));
+}
+__device__ __forceinline__ void wt_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Called by EVERY thread after its write-through stores: drains, joins the barrier, and returns
+// (block-uniformly) whether this block drew the last of `expected` tickets.  The last block
+// resets the ticket (self-cleaning workspace) and may then wt_load every partial.
+__device__ __forceinline__ bool wt_arrive_last(unsigned* ticket, unsigned expected) {
+  __shared__ int s_last;
+  wt_drain();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned t = __hip_atomic_fetch_add((wt_u32*)(ticket), 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    const bool last = t == expected - 1;
+    if (last) __hip_atomic_store((wt_u32*)(ticket), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = last ? 1 : 0;
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
 // Grid sizing for streaming kernels: enough waves to fill 256 CUs, capped (Guideline 11).
 inline int stream_grid(int64_t work_items, int items_per_block, int cap) {
   int64_t g = (work_items + items_per_block - 1) / items_per_block;

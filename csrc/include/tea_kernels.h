@@ -226,8 +226,33 @@ struct MomentsArgs {
   float* mse_part_f = nullptr;  // [2 d] scratch: per-column values (+ tss) for the scalar modes
   int64_t num_obs = 0;
   int num_regressors = 0;
+  // one-launch form (f32 x / t with unit column stride, d >= 4, f32 or no weight): per column
+  // tile, R row-chunk blocks hand FP64 partials to the tile's last arriver (write-through
+  // stores + ticket); the scalar modes add one more ticket over the tiles.
+  double* part = nullptr;       // column_moments_v2_ws_doubles(...) doubles
+  unsigned* tickets = nullptr;  // [tiles + 1], zero, left zero
+  int v2_cg = 0;                // column groups (of 4) per tile: 4 / 16 / 64; 0 = two-launch form
+  int v2_r = 0;                 // row chunks per tile
+  int64_t v2_chunk = 0;         // rows per chunk
+  int v2_pipe = 0;              // two batches of loads in flight per thread (0: one)
+  // deferred mode (class updates): each block ADDS its FP64 column partials to its own slot of
+  // pend ([slots][ns][d] then [slots] weight totals / row counts) and the launch ends there;
+  // launch_moments_fold folds the slots into the float32 states when they are read
+  double* pend = nullptr;
+  int pend_slots = 0;
+  int v2_skip_fold = 0;         // A/B only: stop after the partial stores (results invalid)
 };
 int column_moments_blocks(int64_t n, int64_t d);
+// v2 plan: whether it applies, and its geometry / workspace size (doubles and tickets)
+bool column_moments_v2_plan(MomentsArgs& a, int64_t* ws_doubles, int64_t* tickets);
+constexpr int kMomentsPendSlots = 64;
+inline int moments_ns(const MomentsArgs& a) {
+  const int need = (a.sse ? 1 : 0) | (a.st ? 2 : 0) | (a.stt ? 4 : 0) | (a.sx ? 8 : 0);
+  return need == 1 ? 1 : need == 7 ? 3 : 4;
+}
+// pending slots r < rows_used of a deferred-mode pend buffer -> outputs (+= in float32; sse /
+// st / stt / sx at out_stride, sw scalar), slots zeroed
+int launch_moments_fold(const MomentsArgs& a, int rows_used, hipStream_t stream);
 int launch_column_moments(const MomentsArgs& a, hipStream_t stream);
 
 // ------------------------------------------------------------------ K5b per-row weighted sums
@@ -272,10 +297,12 @@ struct RowSumsArgs {
   RowSumsOut out[kRowSumsMaxOut];
   double* ws = nullptr;  // [rows, blocks, kRowRaw] partials when blocks > 1
   unsigned* ticket = nullptr;  // [rows] zeroed arrival counters: one-launch fold (left zeroed)
+  int wt = 0;            // with ticket: write-through partials (default) instead of the fat-block fold
   int blocks = 1;        // blocks per row
 };
 int row_sums_blocks(int64_t rows, int64_t n);       // two-launch grid (partials + combine)
-int row_sums_fold_blocks(int64_t rows, int64_t n);  // one-launch fold (needs a ticket)
+int row_sums_fold_blocks(int64_t rows, int64_t n);
+int row_sums_wt_blocks(int64_t rows, int64_t n);  // one-launch fold (needs a ticket)
 int launch_row_sums(const RowSumsArgs& a, hipStream_t stream);
 // the same update on host memory (CPU tensors): the small-batch twin of the kernel
 void row_sums_host(const RowSumsArgs& a);

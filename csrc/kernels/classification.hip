@@ -73,6 +73,40 @@ __device__ __forceinline__ void load_vec(const void* row, int col, float (&v)[VE
   }
 }
 
+// UNAL rows (f32, any width >= 4, any 4-B alignment): 16-B loads at 4-B-aligned addresses
+// (tea_common.h load_f4u).  The lane whose 4 columns straddle the row end (C % 4 != 0) loads
+// the row's LAST 4 columns (shifted back by sh) and rotates them into place, so element e
+// still holds nominal column col + e and the columns past C read -inf: every consumer below
+// (max, target select, tie / rank counts, argmax indices) is unchanged.  Lanes wholly past C
+// keep the aligned paths' convention (clamped copies of columns 0..3, caller-masked).
+__device__ __forceinline__ void load_f32_unal(const void* row, int col, int C, float (&v)[4]) {
+  const float* rp = static_cast<const float*>(row);
+  const int sh = (col < C && col + 4 > C) ? col + 4 - C : 0;
+  const int lc = col + 4 <= C ? col : (col < C ? C - 4 : 0);
+  const float4 q = load_f4u(rp + lc);
+  const float f[4] = {q.x, q.y, q.z, q.w};
+  const float ninf = -__builtin_huge_valf();
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float r = f[e];
+    r = sh == 1 ? (e + 1 < 4 ? f[e + 1 < 4 ? e + 1 : 3] : ninf) : r;
+    r = sh == 2 ? (e + 2 < 4 ? f[e + 2 < 4 ? e + 2 : 3] : ninf) : r;
+    r = sh == 3 ? (e + 3 < 4 ? f[e + 3 < 4 ? e + 3 : 3] : ninf) : r;
+    v[e] = r;
+  }
+}
+
+// row loads of the wide kernels: the aligned form (16-B aligned rows, C % VEC == 0) or UNAL
+template <int KIND, int VEC, bool UNAL>
+__device__ __forceinline__ void load_row_vec(const void* row, int col, int C, float (&v)[VEC]) {
+  if constexpr (UNAL) {
+    static_assert(KIND == 0 && VEC == 4, "UNAL rows are f32");
+    load_f32_unal(row, col, C, v);
+  } else {
+    load_vec<KIND, VEC>(row, col < C ? col : 0, v);
+  }
+}
+
 template <int KIND>
 __device__ __forceinline__ float load_one(const void* row, int64_t col) {
   if constexpr (KIND == 0) return static_cast<const float*>(row)[col];
@@ -174,7 +208,7 @@ __device__ __noinline__ int row_argmax_exact(const void* rp, int C, int lane) {
 // Then the wave compares the row max with the target's own score first: a row whose target is
 // not the max is incorrect without locating the argmax (the v2 index pass + min-reduce is only
 // run when they are equal, to apply torch.argmax's first-index rule to ties).
-template <int KIND, int VEC, bool TOPK, bool PRED = true>
+template <int KIND, int VEC, bool TOPK, bool PRED = true, bool UNAL = false>
 __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
   const int lane = lane_id();
   const int64_t nwaves = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
@@ -198,10 +232,7 @@ __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
       // unconditional loads, masked to -inf afterwards.
       float v[kChunkLoads][VEC];
 #pragma unroll
-      for (int u = 0; u < kChunkLoads; ++u) {
-        const int col = u * STEP + lane * VEC;
-        load_vec<KIND, VEC>(rp, col < C ? col : 0, v[u]);
-      }
+      for (int u = 0; u < kChunkLoads; ++u) load_row_vec<KIND, VEC, UNAL>(rp, u * STEP + lane * VEC, C, v[u]);
       t = load_target(a.target, a.tg_dt, row);
 #pragma unroll
       for (int u = 0; u < kChunkLoads; ++u) {
@@ -253,7 +284,7 @@ __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
         for (int u = 0; u < kChunkLoads; ++u) {
           const int col = base + u * STEP + lane * VEC;
           if (col < C) {
-            load_vec<KIND, VEC>(rp, col, v[u]);
+            load_row_vec<KIND, VEC, UNAL>(rp, col, C, v[u]);
           } else {
 #pragma unroll
             for (int e = 0; e < VEC; ++e) v[u][e] = -__builtin_huge_valf();
@@ -299,7 +330,7 @@ __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
         for (int u = 0; u < kChunkLoads; ++u) {
           const int col = base + u * STEP + lane * VEC;
           if (col < C) {
-            load_vec<KIND, VEC>(rp, col, v[u]);
+            load_row_vec<KIND, VEC, UNAL>(rp, col, C, v[u]);
           } else {
 #pragma unroll
             for (int e = 0; e < VEC; ++e) v[u][e] = -__builtin_huge_valf();
@@ -367,7 +398,7 @@ struct RowVals<32> {
 
 // The micro rows of one wave (grid-stride over rows): correct / row counts on lane 0.
 // KIND 0: f32 (4 floats per 16-B load), 1: bf16, 2: f16 (8 per load); TGT: int64_t / int32_t
-template <int KIND, typename TGT>
+template <int KIND, typename TGT, bool UNAL = false>
 __device__ __forceinline__ void micro_rows(const void* __restrict__ input, const TGT* __restrict__ target, int64_t n,
                                            int C, int64_t row_stride, uint32_t& correct_acc, uint32_t& rows_acc) {
   constexpr int VEC = KIND == 0 ? 4 : 8;
@@ -381,10 +412,7 @@ __device__ __forceinline__ void micro_rows(const void* __restrict__ input, const
     const char* rp = static_cast<const char*>(input) + row * row_stride * ELSIZE;
     float f[kChunkLoads][VEC];
 #pragma unroll
-    for (int u = 0; u < kChunkLoads; ++u) {
-      const int col = u * STEP + lane * VEC;
-      load_vec<KIND, VEC>(rp, col < C ? col : 0, f[u]);
-    }
+    for (int u = 0; u < kChunkLoads; ++u) load_row_vec<KIND, VEC, UNAL>(rp, u * STEP + lane * VEC, C, f[u]);
     const int64_t t = target[row];
     vec_t v;
 #pragma unroll
@@ -421,10 +449,10 @@ __device__ __forceinline__ void micro_rows(const void* __restrict__ input, const
   }
 }
 
-template <int KIND, typename TGT>
+template <int KIND, typename TGT, bool UNAL>
 __global__ __launch_bounds__(kBlock) void cls_micro_kernel(ClsCountsArgs a) {
   uint32_t correct_acc = 0, rows_acc = 0;
-  micro_rows<KIND, TGT>(a.input, static_cast<const TGT*>(a.target), a.n, static_cast<int>(a.c), a.row_stride,
+  micro_rows<KIND, TGT, UNAL>(a.input, static_cast<const TGT*>(a.target), a.n, static_cast<int>(a.c), a.row_stride,
                         correct_acc, rows_acc);
   block_micro(a, correct_acc, rows_acc);
 }
@@ -446,7 +474,7 @@ struct MicroPendArgs {
   int32_t pad;
 };
 
-template <int KIND, typename TGT>
+template <int KIND, typename TGT, bool UNAL>
 __device__ __forceinline__ bool micro_row(const MicroPendArgs& a, const char* __restrict__ rp, int64_t t, int lane) {
   constexpr int VEC = KIND == 0 ? 4 : 8;
   constexpr int NV = kChunkLoads * VEC;
@@ -455,10 +483,7 @@ __device__ __forceinline__ bool micro_row(const MicroPendArgs& a, const char* __
   const int C = a.c;
   float f[kChunkLoads][VEC];
 #pragma unroll
-  for (int u = 0; u < kChunkLoads; ++u) {
-    const int col = u * STEP + lane * VEC;
-    load_vec<KIND, VEC>(rp, col < C ? col : 0, f[u]);
-  }
+  for (int u = 0; u < kChunkLoads; ++u) load_row_vec<KIND, VEC, UNAL>(rp, u * STEP + lane * VEC, C, f[u]);
   vec_t v;
 #pragma unroll
   for (int u = 0; u < kChunkLoads; ++u)
@@ -486,7 +511,7 @@ __device__ __forceinline__ bool micro_row(const MicroPendArgs& a, const char* __
   return __ballot(tie) == 0;
 }
 
-template <int KIND, typename TGT, int WPB>
+template <int KIND, typename TGT, int WPB, bool UNAL>
 __global__ __launch_bounds__(WPB * kWave) void cls_micro_pend_kernel(MicroPendArgs a) {
   constexpr int ELSIZE = KIND == 0 ? 4 : 2;
   const int lane = lane_id();
@@ -495,12 +520,12 @@ __global__ __launch_bounds__(WPB * kWave) void cls_micro_pend_kernel(MicroPendAr
   // branches on `n` before the loads and every kernel argument arrives in one scalar round trip
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * WPB + wave_id();
   const int64_t r0 = row0 < a.n ? row0 : a.n - 1;  // the launcher guarantees n >= 1
-  const bool c0 = micro_row<KIND, TGT>(a, static_cast<const char*>(a.input) + r0 * a.row_stride * ELSIZE,
+  const bool c0 = micro_row<KIND, TGT, UNAL>(a, static_cast<const char*>(a.input) + r0 * a.row_stride * ELSIZE,
                                        static_cast<const TGT*>(a.target)[r0], lane);
   uint32_t correct_acc = (row0 < a.n && c0) ? 1u : 0u;
   for (int64_t row = row0 + nwaves; row < a.n; row += nwaves) {
     const char* rp = static_cast<const char*>(a.input) + row * a.row_stride * ELSIZE;
-    correct_acc += micro_row<KIND, TGT>(a, rp, static_cast<const TGT*>(a.target)[row], lane);
+    correct_acc += micro_row<KIND, TGT, UNAL>(a, rp, static_cast<const TGT*>(a.target)[row], lane);
   }
   // deferred fold: one no-return atomic per wave into one of 64 pending cells, no LDS, no
   // block barrier, no returning atomic on the kernel's tail (the fold's ~0.6 us + the block
@@ -523,11 +548,11 @@ __global__ __launch_bounds__(kWave) void micro_finish_kernel(unsigned long long*
   }
 }
 
-template <int KIND, int VEC, bool TOPK, bool PRED = true>
+template <int KIND, int VEC, bool TOPK, bool PRED = true, bool UNAL = false>
 __global__ __launch_bounds__(kBlock) void cls_wide_kernel(ClsCountsArgs a) {
   // (amdgpu_waves_per_eu(8, 8) on the f32 kernels - 64 VGPRs, every row of an 8192-row batch
   // resident at once - measured slower: 8.9 vs 7.8 us per 8192 x 1000 update)
-  cls_wide_body<KIND, VEC, TOPK, PRED>(a);
+  cls_wide_body<KIND, VEC, TOPK, PRED, UNAL>(a);
 }
 
 // Narrow rows (C <= 32): one thread per row, class histograms privatised in LDS.
@@ -647,7 +672,7 @@ __global__ __launch_bounds__(kBlock) void binary_counts_kernel(BinaryCountsArgs 
   if (threadIdx.x == 0 && blockIdx.x == 0 && a.total) atomicAdd(a.total, static_cast<float>(a.n));
 }
 
-template <int KIND, int VEC>
+template <int KIND, int VEC, bool UNAL = false>
 void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
   constexpr int kChunkCols = kWave * VEC * kChunkLoads;
   const bool pred_free = a.cls_pred == nullptr && a.cls_fp == nullptr && a.confusion == nullptr &&
@@ -673,31 +698,31 @@ void launch_wide(const ClsCountsArgs& a, int grid, hipStream_t s) {
     if (wpb == 8) {
       const int g8 = stream_grid(a.n, 8, a.max_blocks > 0 ? (a.max_blocks + 1) / 2 : 1024);
       if (a.tg_dt == DType::i64)
-        hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t, 8>), dim3(g8), dim3(8 * kWave), 0, s, m);
+        hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t, 8, UNAL>), dim3(g8), dim3(8 * kWave), 0, s, m);
       else
-        hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t, 8>), dim3(g8), dim3(8 * kWave), 0, s, m);
+        hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t, 8, UNAL>), dim3(g8), dim3(8 * kWave), 0, s, m);
       return;
     }
     if (a.tg_dt == DType::i64)
-      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t, kWavesPerBlock>), dim3(grid), dim3(kBlock), 0, s, m);
+      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int64_t, kWavesPerBlock, UNAL>), dim3(grid), dim3(kBlock), 0, s, m);
     else
-      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t, kWavesPerBlock>), dim3(grid), dim3(kBlock), 0, s, m);
+      hipLaunchKernelGGL((cls_micro_pend_kernel<KIND, int32_t, kWavesPerBlock, UNAL>), dim3(grid), dim3(kBlock), 0, s, m);
     return;
   }
   if (micro_only && a.tg_dt == DType::i64) {
-    hipLaunchKernelGGL((cls_micro_kernel<KIND, int64_t>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((cls_micro_kernel<KIND, int64_t, UNAL>), dim3(grid), dim3(kBlock), 0, s, a);
     return;
   }
   if (micro_only && a.tg_dt == DType::i32) {
-    hipLaunchKernelGGL((cls_micro_kernel<KIND, int32_t>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((cls_micro_kernel<KIND, int32_t, UNAL>), dim3(grid), dim3(kBlock), 0, s, a);
     return;
   }
   if (a.k > 1)
-    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, true>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, true, true, UNAL>), dim3(grid), dim3(kBlock), 0, s, a);
   else if (pred_free)
-    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, false, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, false, false, UNAL>), dim3(grid), dim3(kBlock), 0, s, a);
   else
-    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, false>), dim3(grid), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((cls_wide_kernel<KIND, VEC, false, true, UNAL>), dim3(grid), dim3(kBlock), 0, s, a);
 }
 
 template <int KIND>
@@ -728,7 +753,9 @@ int launch_cls_counts(const ClsCountsArgs& a, hipStream_t stream) {
       const int grid = stream_grid(a.n, kWavesPerBlock, cap);
       const int vw = kind == 0 ? 4 : 8;
       const bool vec = (a.c % vw == 0) && (a.row_stride % vw == 0) && (base % 16 == 0);
-      if (kind == 0) vec ? launch_wide<0, 4>(a, grid, stream) : launch_wide<0, 1>(a, grid, stream);
+      // f32 rows of any width / alignment keep 16-B loads (UNAL); 16-bit rows that are not
+      // 16-B aligned take the scalar form
+      if (kind == 0) vec ? launch_wide<0, 4>(a, grid, stream) : launch_wide<0, 4, true>(a, grid, stream);
       else if (kind == 1) vec ? launch_wide<1, 8>(a, grid, stream) : launch_wide<1, 1>(a, grid, stream);
       else vec ? launch_wide<2, 8>(a, grid, stream) : launch_wide<2, 1>(a, grid, stream);
     }

@@ -116,10 +116,10 @@ __device__ Acc block_merge(Acc a) {
   return a;
 }
 
-// [lo, hi) of row r; VEC: f32 rows with unit stride, 16-B aligned (x, t, w as present)
-template <int NEED, bool HAS_W, bool VEC, int BS = kB>
+// [lo, hi) of row r; VEC: f32 rows with unit stride (x, t, w as present; any 4-B alignment)
+template <int NEED, bool HAS_W, bool VEC, int BS = kB, int VPT = kVecPerThread>
 __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t hi) {
-  constexpr int64_t kChunk = static_cast<int64_t>(BS) * kVecPerThread * 4;
+  constexpr int64_t kChunk = static_cast<int64_t>(BS) * VPT * 4;
   constexpr bool HAS_T = (NEED & kNeedT) != 0;
   Acc a;
   acc_init(a);
@@ -128,25 +128,26 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
     const float* xr = static_cast<const float*>(g.x) + r * g.x_rs;
     const float* tr = HAS_T ? static_cast<const float*>(g.t) + r * g.t_rs : nullptr;
     const float* wr = HAS_W ? static_cast<const float*>(g.w) + r * g.w_rs : nullptr;
-    const int64_t vlo = (lo + 3) / 4 * 4, vhi = hi / 4 * 4;
+    // 16-B loads at any 4-B alignment: the body is every whole group of 4 from lo
+    const int64_t vlo = lo, vhi = lo + (hi - lo) / 4 * 4;
     // every float4 of the chunk is issued before any arithmetic: one memory round trip
     for (int64_t base = vlo; base < vhi; base += kChunk) {
-      float4 xv[kVecPerThread], tv[kVecPerThread], wv[kVecPerThread];
+      float4 xv[VPT], tv[VPT], wv[VPT];
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       // unconditional loads from a clamped (always valid) address: a per-lane `ok ? load : 0`
       // makes hipcc branch around each load and wait vmcnt(0) after it - one serial memory
       // round trip per float4 (the consumers below skip the out-of-range lanes)
 #pragma unroll
-      for (int u = 0; u < kVecPerThread; ++u) {
+      for (int u = 0; u < VPT; ++u) {
         const int64_t i = base + 4 * (static_cast<int64_t>(u) * BS + threadIdx.x);
         const int64_t ic = i < vhi ? i : vlo;
-        xv[u] = *reinterpret_cast<const float4*>(xr + ic);
-        tv[u] = HAS_T ? *reinterpret_cast<const float4*>(tr + ic) : z;
-        wv[u] = HAS_W ? *reinterpret_cast<const float4*>(wr + ic) : z;
+        xv[u] = load_f4u(xr + ic);  // 4-B alignment suffices (tea_common.h)
+        tv[u] = HAS_T ? load_f4u(tr + ic) : z;
+        wv[u] = HAS_W ? load_f4u(wr + ic) : z;
       }
       if (base + kChunk <= vhi) {  // whole chunk in range (block-uniform): no per-lane branch
 #pragma unroll
-        for (int u = 0; u < kVecPerThread; ++u) {
+        for (int u = 0; u < VPT; ++u) {
           acc_elem<NEED, HAS_W>(a, need, xv[u].x, tv[u].x, wv[u].x);
           acc_elem<NEED, HAS_W>(a, need, xv[u].y, tv[u].y, wv[u].y);
           acc_elem<NEED, HAS_W>(a, need, xv[u].z, tv[u].z, wv[u].z);
@@ -158,7 +159,7 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
         // every row's last block ran ~4 serial round trips: CTR 64 x 128000 took 17.7 us
         // against 8.1 us for the same bytes in one row)
 #pragma unroll
-        for (int u = 0; u < kVecPerThread; ++u) {
+        for (int u = 0; u < VPT; ++u) {
           const int64_t i = base + 4 * (static_cast<int64_t>(u) * BS + threadIdx.x);
           const bool ok = i < vhi;
           const float4 xm = make_float4(ok ? xv[u].x : 0.f, ok ? xv[u].y : 0.f, ok ? xv[u].z : 0.f, ok ? xv[u].w : 0.f);
@@ -357,8 +358,50 @@ __global__ __launch_bounds__(kFB) void row_sums_fold_kernel(RowSumsArgs g, int64
   }
 }
 
-bool vec_ok(const void* p, DType dt, int64_t rs, int64_t cs) {
-  return p == nullptr || (dt == DType::f32 && cs == 1 && rs % 4 == 0 && reinterpret_cast<uintptr_t>(p) % 16 == 0);
+// one launch for long rows (the default): grid blocks fold their span with 8 x 16-B loads per
+// operand per thread in flight, store their FP64 partials WRITE-THROUGH and take a ticket; the
+// row's last arriving block reads the partials back (sc1 loads), combines them in a fixed
+// order (deterministic) and applies the outputs (tea_common.h wt_*: no release / acquire
+// fence, whose buffer_wbl2 made the fat-block fold above no faster than two launches).
+constexpr int kWtVPT = 8;
+constexpr int64_t kWtChunk = static_cast<int64_t>(kB) * kWtVPT * 4;
+
+template <int NEED, bool HAS_W, bool VEC>
+__global__ __launch_bounds__(kB) void row_sums_wt_kernel(RowSumsArgs g, int64_t span) {
+  const int64_t r = blockIdx.y;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * span;
+  const int64_t hi = min(g.n, lo + span);
+  const Acc a = block_merge<NEED>(reduce_range<NEED, HAS_W, VEC, kB, kWtVPT>(g, r, lo, hi));
+  double* p = g.ws + r * kNStat * g.blocks + blockIdx.x;
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < kNStat; ++k)
+      if (NEED & bit(k)) wt_store(p + k * g.blocks, a.v[k]);
+  }
+  if (!wt_arrive_last(g.ticket + r, static_cast<unsigned>(g.blocks))) return;
+  const double* src = g.ws + r * kNStat * g.blocks;
+  Acc m;
+  acc_init(m);
+  for (int b0 = threadIdx.x; b0 < g.blocks; b0 += 2 * kB) {  // two partials' loads in flight
+    const int b1 = b0 + kB;
+    Acc q0, q1;
+    acc_init(q0);
+    acc_init(q1);
+#pragma unroll
+    for (int k = 0; k < kNStat; ++k) {
+      if (!(NEED & bit(k))) continue;
+      q0.v[k] = wt_load(src + k * g.blocks + b0);
+      if (b1 < g.blocks) q1.v[k] = wt_load(src + k * g.blocks + b1);
+    }
+    acc_merge<NEED>(m, q0);
+    if (b1 < g.blocks) acc_merge<NEED>(m, q1);
+  }
+  m = block_merge<NEED>(m);
+  if (threadIdx.x == 0) finish_row<HAS_W>(g, r, m);
+}
+
+bool vec_ok(const void* p, DType dt, int64_t /*rs*/, int64_t cs) {
+  return p == nullptr || (dt == DType::f32 && cs == 1);  // 16-B loads need only 4-B alignment
 }
 
 template <int NEED, bool HAS_W>
@@ -366,6 +409,12 @@ int launch_need(const RowSumsArgs& a, bool vec, hipStream_t stream) {
   if (a.blocks <= 1) {
     if (vec) hipLaunchKernelGGL((row_sums_single_kernel<NEED, HAS_W, true>), dim3(a.rows), dim3(kB), 0, stream, a);
     else hipLaunchKernelGGL((row_sums_single_kernel<NEED, HAS_W, false>), dim3(a.rows), dim3(kB), 0, stream, a);
+  } else if (a.ticket && a.wt) {  // one launch: write-through partials + last-block combine
+    const int64_t chunks = (a.n + kWtChunk - 1) / kWtChunk;
+    const int64_t span = (chunks + a.blocks - 1) / a.blocks * kWtChunk;
+    const dim3 grid(static_cast<unsigned>(a.blocks), static_cast<unsigned>(a.rows));
+    if (vec) hipLaunchKernelGGL((row_sums_wt_kernel<NEED, HAS_W, true>), grid, dim3(kB), 0, stream, a, span);
+    else hipLaunchKernelGGL((row_sums_wt_kernel<NEED, HAS_W, false>), grid, dim3(kB), 0, stream, a, span);
   } else if (a.ticket) {  // one launch: fat blocks + last-block combine
     const int64_t span = (a.n + a.blocks - 1) / a.blocks;
     const int64_t span_c = (span + kFoldChunk - 1) / kFoldChunk * kFoldChunk;
@@ -403,6 +452,15 @@ int row_sums_blocks(int64_t rows, int64_t n) {
   int64_t cap = 512;
   if (const char* e = std::getenv("TORCHEVAL_AMD_K5B_GRID")) cap = std::max(1, std::atoi(e));
   const int64_t chunks = (n + kPerBlock - 1) / kPerBlock;
+  const int64_t per_row = std::max<int64_t>(2, cap / std::max<int64_t>(rows, 1));
+  return static_cast<int>(std::min(chunks, per_row));
+}
+
+int row_sums_wt_blocks(int64_t rows, int64_t n) {
+  if (n <= kSingle) return 1;
+  int64_t cap = 512;
+  if (const char* e = std::getenv("TORCHEVAL_AMD_K5B_GRID")) cap = std::max(1, std::atoi(e));
+  const int64_t chunks = (n + kWtChunk - 1) / kWtChunk;
   const int64_t per_row = std::max<int64_t>(2, cap / std::max<int64_t>(rows, 1));
   return static_cast<int>(std::min(chunks, per_row));
 }

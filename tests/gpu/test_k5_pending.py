@@ -1,0 +1,100 @@
+"""K5 deferred mode (metrics/_pending.py): MeanSquaredError / R2Score class updates add FP64
+partials to pending slots and the states fold them when read.  Every way a state can be read
+or replaced sees exactly the folded sums: compute, direct reads, state_dict / load_state_dict,
+merge_state, reset, copies / pickle, to(), a 1-D update after 2-D ones, and HIP-graph replays;
+all against fp64 references of reference mean_squared_error.py:82-111 / r2_score.py:97-130."""
+
+import copy
+import pickle
+
+import pytest
+import torch
+
+from torcheval_amd.metrics import MeanSquaredError, R2Score
+from torcheval_amd.metrics.functional import r2_score
+from torcheval_amd.metrics.toolkit import sync_and_compute
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _data(n, d, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(n, d, generator=g), torch.randn(n, d, generator=g) + 1.0
+
+
+def _sse(xs, ys):
+    return sum(((y.double() - x.double()) ** 2).sum(0) for x, y in zip(xs, ys))
+
+
+def test_pending_then_every_read():
+    xs, ys = zip(*[_data(4096, 1001, s) for s in range(3)])
+    m = MeanSquaredError(multioutput="raw_values", device=DEV)
+    for x, y in zip(xs, ys):
+        m.update(x.to(DEV), y.to(DEV))
+    assert m.__dict__["_pend_dirty"]  # the updates ran in deferred mode
+    ref = _sse(xs, ys)
+    torch.testing.assert_close(m.sum_squared_error.cpu().double(), ref, rtol=1e-6, atol=1e-4)
+    assert not m.__dict__["_pend_dirty"]
+    assert float(m.sum_weight) == 3 * 4096
+    torch.testing.assert_close(m.compute().cpu().double(), ref / (3 * 4096), rtol=1e-6, atol=1e-6)
+    # more updates after a fold, then state_dict / load_state_dict
+    m.update(xs[0].to(DEV), ys[0].to(DEV))
+    sd = m.state_dict()
+    torch.testing.assert_close(sd["sum_squared_error"].cpu().double(), ref + _sse(xs[:1], ys[:1]), rtol=1e-6, atol=1e-4)
+    m2 = MeanSquaredError(multioutput="raw_values", device=DEV)
+    m2.update(xs[1].to(DEV), ys[1].to(DEV))  # pending in m2 ...
+    m2.load_state_dict(sd)  # ... replaced: the loaded states win for the replaced states
+    torch.testing.assert_close(m2.sum_squared_error.cpu(), sd["sum_squared_error"].cpu())
+
+
+def test_reset_drops_pending_and_copies_fold():
+    x, y = _data(2048, 64, 7)
+    m = MeanSquaredError(device=DEV)
+    m.update(x.to(DEV), y.to(DEV))
+    c = copy.deepcopy(m)
+    p = pickle.loads(pickle.dumps(m))
+    for other in (c, p):
+        torch.testing.assert_close(other.sum_squared_error.cpu().double(), _sse([x], [y]), rtol=1e-6, atol=1e-4)
+    m.update(x.to(DEV), y.to(DEV))
+    m.reset()
+    assert float(m.sum_weight) == 0.0 and not bool(m.sum_squared_error.any())
+    m.update(x.to(DEV), y.to(DEV))
+    torch.testing.assert_close(m.sum_squared_error.cpu().double(), _sse([x], [y]), rtol=1e-6, atol=1e-4)
+
+
+def test_merge_to_and_mixed_rank_updates():
+    xs, ys = zip(*[_data(1500, 17, s) for s in range(4)])
+    ms = [MeanSquaredError(multioutput="raw_values", device=DEV) for _ in range(4)]
+    for m, x, y in zip(ms, xs, ys):
+        m.update(x.to(DEV), y.to(DEV))
+    ms[0].merge_state(ms[1:])
+    torch.testing.assert_close(ms[0].sum_squared_error.cpu().double(), _sse(xs, ys), rtol=1e-6, atol=1e-4)
+    for m, x, y in zip(ms[1:], xs[1:], ys[1:]):  # inputs to merge unchanged
+        torch.testing.assert_close(m.sum_squared_error.cpu().double(), _sse([x], [y]), rtol=1e-6, atol=1e-4)
+    ms[1].update(xs[0].to(DEV), ys[0].to(DEV))
+    cpu = ms[1].to("cpu")
+    torch.testing.assert_close(cpu.sum_squared_error.double(), _sse(xs[:2], ys[:2]), rtol=1e-6, atol=1e-4)
+    # R2: 2-D deferred updates, then a fold through compute, a sync at ws=1
+    r = R2Score(multioutput="raw_values", device=DEV)
+    for x, y in zip(xs, ys):
+        r.update(x.to(DEV), y.to(DEV))
+    ref = r2_score(torch.cat(xs).double(), torch.cat(ys).double(), multioutput="raw_values")
+    torch.testing.assert_close(r.compute().cpu().double(), ref, rtol=1e-5, atol=1e-6)
+    r.update(xs[0].to(DEV), ys[0].to(DEV))
+    ref2 = r2_score(torch.cat(xs + xs[:1]).double(), torch.cat(ys + ys[:1]).double(), multioutput="raw_values")
+    torch.testing.assert_close(sync_and_compute(r).cpu().double(), ref2, rtol=1e-5, atol=1e-6)
+
+
+def test_weighted_and_variable_batches():
+    g = torch.Generator().manual_seed(3)
+    m = MeanSquaredError(multioutput="raw_values", device=DEV)
+    num, den = 0.0, 0.0
+    for n in (1, 300, 70001, 5):
+        x, y = torch.randn(n, 33, generator=g), torch.randn(n, 33, generator=g)
+        w = torch.rand(n, generator=g)
+        m.update(x.to(DEV), y.to(DEV), sample_weight=w.to(DEV))
+        num = num + (((y.double() - x.double()) ** 2) * w.double()[:, None]).sum(0)
+        den += float(w.double().sum())
+    torch.testing.assert_close(m.sum_squared_error.cpu().double(), num, rtol=1e-6, atol=1e-4)
+    assert float(m.sum_weight) == pytest.approx(den, rel=1e-6)

@@ -4,7 +4,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops import use_native
+from torcheval_amd.ops import compiling, native, use_native
 
 
 def _native(input: torch.Tensor, target: torch.Tensor, w: Optional[torch.Tensor] = None) -> bool:
@@ -24,12 +24,18 @@ def _update(
     return (squared_error * sample_weight).sum(dim=0), sample_weight.sum(dim=0).squeeze()
 
 
+def _state(metric, name: str) -> torch.Tensor:
+    """A state without folding pending device sums (metrics/_pending.py), else getattr."""
+    v = metric.__dict__.get("_pv_" + name)
+    return v if v is not None else getattr(metric, name)
+
+
 def _promote_lazy(metric, names, input: torch.Tensor) -> bool:
     """The reference's lazy shape promotion of 0-d states to [d] on the first 2-D update
     (done here up front so the fused kernels can accumulate in place).  False when the states
     and the batch disagree in shape (the ATen path then reproduces the reference's broadcast)."""
     d = input.shape[1] if input.ndim == 2 else 1
-    states = [getattr(metric, n) for n in names]
+    states = [_state(metric, n) for n in names]
     if input.ndim == 2 and all(s.ndim == 0 for s in states):
         for n, s in zip(names, states):
             setattr(metric, n, torch.zeros(d, dtype=s.dtype, device=s.device) + s)
@@ -52,17 +58,31 @@ def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w
     if w is not None and (w.dtype != torch.float32 or w.ndim != 1):
         return False
     names = [n for n, _ in sums] + [n for n, _ in scalars]
-    if not all(getattr(metric, n).dtype == torch.float32 and getattr(metric, n).device == input.device for n in names):
+    if not all(_state(metric, n).dtype == torch.float32 and _state(metric, n).device == input.device for n in names):
         return False
     if input.is_cuda and input.ndim == 2:
         if not _native(input, target, w) or not _promote_lazy(metric, [n for n, _ in sums], input):
             return False
+        key = {_rs.WSSE: "sse", _rs.SSE: "sse", _rs.WT: "st", _rs.WTT: "stt", _rs.W: "sw", _rs.COUNT: "sw"}
+        spec = {key[stat]: n for n, stat in list(sums) + list(scalars)}
+        kw = {"sse": None, "st": None, "stt": None, "sw": None}
+        for k, n in spec.items():
+            kw[k] = _state(metric, n)
+        if getattr(metric, "_pend_states", ()) and not compiling():
+            # deferred mode (metrics/_pending.py): the launch only adds FP64 partials to the
+            # metric's pending slots; the states fold them in when read
+            d = input.shape[1]
+            need = sum(b for k, b in (("sse", 1), ("st", 2), ("stt", 4)) if kw[k] is not None)
+            ns = 1 if need == 1 else 3 if need == 7 else 4  # tea_kernels.h moments_ns
+            from torcheval_amd.metrics._pending import PEND_SLOTS
+
+            pend = metric._pend_buffer(PEND_SLOTS * (ns * d + 1), input.device)
+            slots = native().column_moments_pend(input, target, w, kw["sse"], kw["st"], kw["stt"], None, kw["sw"], pend)
+            if slots:
+                metric._pend_mark(slots, spec)
+                return True
         from torcheval_amd.ops.reductions import column_moments
 
-        kw = {"sse": None, "st": None, "stt": None, "sw": None}
-        key = {_rs.WSSE: "sse", _rs.SSE: "sse", _rs.WT: "st", _rs.WTT: "stt", _rs.W: "sw", _rs.COUNT: "sw"}
-        for n, stat in list(sums) + list(scalars):
-            kw[key[stat]] = getattr(metric, n)
         column_moments(input, target, w, **kw)
         return True
     if not _rs.supported(input, target, w) or input.numel() == 0:

@@ -12,12 +12,17 @@ from torcheval_amd.metrics.functional.regression import (
 )
 from torcheval_amd.metrics.functional.regression._common import fused_regression_update
 from torcheval_amd.ops import rowsums as _rs
+from torcheval_amd.metrics._pending import PendingMixin, pending_states
 from torcheval_amd.metrics.metric import Metric
 
 __all__ = ["MeanSquaredError"]
 
+# states folded from the K5 deferred-mode pending sums when read (metrics/_pending.py)
+_PEND = ("sum_squared_error", "sum_weight")
 
-class MeanSquaredError(Metric[torch.Tensor]):
+
+@pending_states(*_PEND)
+class MeanSquaredError(PendingMixin, Metric[torch.Tensor]):
     """Mean squared error; ``multioutput`` in uniform_average | raw_values.
     Functional version: ``mean_squared_error``."""
 

@@ -12,12 +12,17 @@ from torcheval_amd.metrics.functional.regression import (
 )
 from torcheval_amd.metrics.functional.regression._common import fused_regression_update
 from torcheval_amd.ops import rowsums as _rs
+from torcheval_amd.metrics._pending import PendingMixin, pending_states
 from torcheval_amd.metrics.metric import Metric
 
 __all__ = ["R2Score"]
 
+# states folded from the K5 deferred-mode pending sums when read (metrics/_pending.py)
+_PEND = ("sum_squared_obs", "sum_obs", "sum_squared_residual", "num_obs")
 
-class R2Score(Metric[torch.Tensor]):
+
+@pending_states(*_PEND)
+class R2Score(PendingMixin, Metric[torch.Tensor]):
     """Coefficient of determination (optionally adjusted).  Functional version: ``r2_score``."""
 
     def __init__(
