@@ -644,8 +644,9 @@ void retrieval_topk_update(const Tensor& x, const Tensor& t, const optional<Tens
 // of the code = row 0 only (a scalar state): f32 / f64 tensors of `rows` elements (any stride:
 // a ring-buffer column works), or of one element for row-0-only outputs.  CUDA tensors
 // run K5b (one launch, two for rows > 64K elements); CPU tensors the host twin.
-void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<Tensor>& w_in, double w_scalar,
-              const std::vector<Tensor>& outs, const std::vector<int64_t>& codes, int64_t rows) {
+static tea::RowSumsArgs row_sums_args(const Tensor& x_in, const optional<Tensor>& t_in, const optional<Tensor>& w_in,
+                                      double w_scalar, const std::vector<Tensor>& outs,
+                                      const std::vector<int64_t>& codes, int64_t rows, Tensor* x_out) {
   // any shape: a [rows, n] view is used as is, anything else is viewed as rows x (numel / rows)
   auto as_rows = [&](const Tensor& v) -> Tensor {
     if (v.dim() == 2 && v.size(0) == rows) return v;
@@ -693,6 +694,15 @@ void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<T
     if (a.out[k].stat == tea::kRANGE) need |= (1 << tea::kTMIN) | (1 << tea::kTMAX);
   }
   a.need = need;
+  *x_out = x;
+  return a;
+}
+
+void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<Tensor>& w_in, double w_scalar,
+              const std::vector<Tensor>& outs, const std::vector<int64_t>& codes, int64_t rows) {
+  Tensor x;
+  tea::RowSumsArgs a = row_sums_args(x_in, t_in, w_in, w_scalar, outs, codes, rows, &x);
+  const bool gpu = x.is_cuda();
   if (!gpu) {
     tea::row_sums_host(a);
     return;
@@ -717,6 +727,84 @@ void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<T
   }
   if (a.n == 0 && a.rows > 0) a.blocks = 1;
   check_launch(tea::launch_row_sums(a, stream_for(x)), "row_sums");
+}
+
+// deferred-mode K5b update (rows longer than one block; ADD outputs of sums / W / COUNT): the
+// grid blocks add their pre-scaled FP64 partials to their slots of `pend` (float64, zeroed,
+// rows * kRowPendStats * kRowPendBlocks); returns the blocks used (0: not applicable, the
+// caller runs row_sums).  row_sums_fold applies the slots to the same outputs and zeroes them.
+int64_t row_sums_pend(const Tensor& x_in, const optional<Tensor>& t_in, const optional<Tensor>& w_in,
+                      double w_scalar, const std::vector<Tensor>& outs, const std::vector<int64_t>& codes,
+                      int64_t rows, const Tensor& pend) {
+  Tensor x;
+  tea::RowSumsArgs a = row_sums_args(x_in, t_in, w_in, w_scalar, outs, codes, rows, &x);
+  if (!x.is_cuda() || a.n == 0) return 0;
+  for (int k = 0; k < a.nout; ++k)
+    if (a.out[k].op != tea::kAdd || a.out[k].stat == tea::kTMIN || a.out[k].stat == tea::kTMAX ||
+        a.out[k].stat == tea::kRANGE)
+      return 0;
+  const int blocks = tea::row_sums_blocks(a.rows, a.n);
+  if (blocks < 2 || blocks > tea::kRowPendBlocks) return 0;
+  TORCH_CHECK(pend.scalar_type() == at::kDouble && pend.is_contiguous() && pend.device() == x.device() &&
+                  pend.numel() >= a.rows * tea::kRowPendStats * tea::kRowPendBlocks,
+              "row_sums_pend: pend must be float64 [rows * ", tea::kRowPendStats, " * ", tea::kRowPendBlocks, "]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  a.blocks = blocks;
+  a.pend = pend.data_ptr<double>();
+  a.pend_blocks = tea::kRowPendBlocks;
+  check_launch(tea::launch_row_sums(a, stream_for(x)), "row_sums_pend");
+  return blocks;
+}
+
+void row_sums_fold(const Tensor& pend, int64_t used, const std::vector<Tensor>& outs,
+                   const std::vector<int64_t>& codes, int64_t rows) {
+  TORCH_CHECK(!outs.empty(), "row_sums_fold: no outputs");
+  const Tensor carrier = at::empty({rows, 0}, pend.options().dtype(at::kFloat));
+  Tensor x;
+  tea::RowSumsArgs a = row_sums_args(carrier, c10::nullopt, c10::nullopt, 1.0, outs, codes, rows, &x);
+  TORCH_CHECK(pend.scalar_type() == at::kDouble && pend.is_cuda() &&
+                  pend.numel() >= a.rows * tea::kRowPendStats * tea::kRowPendBlocks,
+              "row_sums_fold: bad pend buffer");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(pend.device());
+  a.pend = pend.data_ptr<double>();
+  a.pend_blocks = tea::kRowPendBlocks;
+  check_launch(tea::launch_row_sums_fold(a, static_cast<int>(used), stream_for(pend)), "row_sums_fold");
+}
+
+// ---------------------------------------------------------------- K4b per-sample binned AUROC
+// input float32 [n, c] (unit column stride), target int64 / int32 [n], thr float32 [T] ascending
+// (contiguous), out float32 [n], err int32 [>= 1] (bit 0: a label outside [0, c))
+void sample_binned_auroc(const Tensor& input, const Tensor& target, const Tensor& thr, const Tensor& out,
+                         const Tensor& err) {
+  check_gpu(input, "input");
+  TORCH_CHECK(input.dim() == 2 && input.scalar_type() == at::kFloat && input.stride(1) == 1,
+              "sample_binned_auroc: input must be float32 [n, c] with unit column stride");
+  TORCH_CHECK(target.dim() == 1 && target.size(0) == input.size(0) && target.device() == input.device() &&
+                  (target.scalar_type() == at::kLong || target.scalar_type() == at::kInt),
+              "sample_binned_auroc: target must be int64 / int32 [n] on the input's device");
+  TORCH_CHECK(thr.dim() == 1 && thr.scalar_type() == at::kFloat && thr.is_contiguous() && thr.device() == input.device(),
+              "sample_binned_auroc: thresholds must be a contiguous float32 vector on the input's device");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == input.size(0) &&
+                  out.device() == input.device(),
+              "sample_binned_auroc: out must be float32 [n]");
+  TORCH_CHECK(err.scalar_type() == at::kInt && err.numel() >= 1 && err.device() == input.device(),
+              "sample_binned_auroc: err must be int32");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(input.device());
+  tea::SampleAurocArgs a;
+  a.input = input.data_ptr<float>();
+  a.n = input.size(0);
+  a.c = input.size(1);
+  a.row_stride = input.stride(0);
+  a.target = target.data_ptr();
+  a.tg_dt = dt_of(target);
+  a.tg_stride = target.stride(0);
+  a.thr = thr.data_ptr<float>();
+  a.T = static_cast<int>(thr.numel());
+  a.out = out.data_ptr<float>();
+  a.err = err.data_ptr<int>();
+  const int rc = tea::launch_sample_binned_auroc(a, stream_for(input));
+  TORCH_CHECK(rc != -1, "sample_binned_auroc: unsupported arguments (needs c >= 1, T >= 1)");
+  check_launch(rc, "sample_binned_auroc");
 }
 
 // ---------------------------------------------------------------- K4 binned histograms
@@ -1385,6 +1473,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"),
         py::arg("sx"), py::arg("sw"), py::arg("overwrite") = 0, py::arg("mse_mode") = 0,
         py::arg("mse_out") = py::none(), py::arg("num_regressors") = 0);
+  m.def("sample_binned_auroc", &sample_binned_auroc,
+        "K4b per-sample multiclass binned AUROC (the reference default), labels checked into err",
+        py::arg("input"), py::arg("target"), py::arg("thr"), py::arg("out"), py::arg("err"));
+  m.def("row_sums_pend", &row_sums_pend,
+        "K5b deferred-mode update: pre-scaled FP64 block partials added to pending slots; returns blocks used",
+        py::arg("x"), py::arg("t"), py::arg("w"), py::arg("w_scalar"), py::arg("outs"), py::arg("codes"),
+        py::arg("rows"), py::arg("pend"));
+  m.def("row_sums_fold", &row_sums_fold, "K5b pending slots -> outputs (ADD), slots zeroed", py::arg("pend"),
+        py::arg("used"), py::arg("outs"), py::arg("codes"), py::arg("rows"));
   m.def("column_moments_pend", &column_moments_pend,
         "K5 deferred-mode class update: FP64 column partials added to pending slots; returns the slots used",
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),

@@ -184,6 +184,12 @@ __device__ __forceinline__ bool wt_arrive_last(unsigned* ticket, unsigned expect
   return s_last != 0;
 }
 
+// Deferred-mode partial: ADD v to a pending slot this block alone writes in this launch, as a
+// no-return FP64 atomic (global_atomic_add_f64): fire and forget, where a plain += would wait a
+// full memory round trip for the old value at the end of every block.  One writer per slot per
+// launch and stream-ordered launches keep the sums deterministic.
+__device__ __forceinline__ void pend_add(double* p, double v) { unsafeAtomicAdd(p, v); }
+
 // Grid sizing for streaming kernels: enough waves to fill 256 CUs, capped (Guideline 11).
 inline int stream_grid(int64_t work_items, int items_per_block, int cap) {
   int64_t g = (work_items + items_per_block - 1) / items_per_block;

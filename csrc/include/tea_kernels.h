@@ -297,9 +297,35 @@ struct RowSumsArgs {
   RowSumsOut out[kRowSumsMaxOut];
   double* ws = nullptr;  // [rows, blocks, kRowRaw] partials when blocks > 1
   unsigned* ticket = nullptr;  // [rows] zeroed arrival counters: one-launch fold (left zeroed)
-  int wt = 0;            // with ticket: write-through partials (default) instead of the fat-block fold
+  int wt = 0;            // with ticket: write-through partials instead of the fat-block fold
   int blocks = 1;        // blocks per row
+  // deferred mode (long rows, ADD outputs of sums / W / COUNT only): every grid block ADDS its
+  // FP64 partials - already scaled by a scalar weight, W and COUNT included - to its own slot of
+  // pend ([rows][kRowPendStats][pend_blocks]) and the launch ends there; launch_row_sums_fold
+  // applies the slots to the outputs when the states are read
+  double* pend = nullptr;
+  int pend_blocks = 0;
 };
+// ------------------------------------------------------------------ K4b per-sample binned AUROC
+// the reference-default multiclass_binned_auroc (binned_auroc.py:189-215): out[i] = the binned
+// AUROC of sample i's true-class score against its other classes (csrc/kernels/binned_auroc.hip)
+struct SampleAurocArgs {
+  const float* input = nullptr;  // [n, c], unit column stride
+  int64_t n = 0, c = 0, row_stride = 0;
+  const void* target = nullptr;  // [n] int64 / int32
+  DType tg_dt = DType::i64;
+  int64_t tg_stride = 1;
+  const float* thr = nullptr;  // [T] ascending
+  int T = 0;
+  float* out = nullptr;  // [n]
+  int* err = nullptr;    // bit 0: a label outside [0, c)
+};
+int launch_sample_binned_auroc(const SampleAurocArgs& a, hipStream_t stream);
+
+constexpr int kRowPendStats = kRowSums + 1;  // the six sums, then COUNT
+constexpr int kRowPendBlocks = 2048;
+// pending slots b < blocks_used of every row -> the outputs of a (ADD), slots zeroed
+int launch_row_sums_fold(const RowSumsArgs& a, int blocks_used, hipStream_t stream);
 int row_sums_blocks(int64_t rows, int64_t n);       // two-launch grid (partials + combine)
 int row_sums_fold_blocks(int64_t rows, int64_t n);
 int row_sums_wt_blocks(int64_t rows, int64_t n);  // one-launch fold (needs a ticket)

@@ -74,36 +74,53 @@ __device__ __forceinline__ void load_vec(const void* row, int col, float (&v)[VE
 }
 
 // UNAL rows (f32, any width >= 4, any 4-B alignment): 16-B loads at 4-B-aligned addresses
-// (tea_common.h load_f4u).  The lane whose 4 columns straddle the row end (C % 4 != 0) loads
-// the row's LAST 4 columns (shifted back by sh) and rotates them into place, so element e
-// still holds nominal column col + e and the columns past C read -inf: every consumer below
-// (max, target select, tie / rank counts, argmax indices) is unchanged.  Lanes wholly past C
-// keep the aligned paths' convention (clamped copies of columns 0..3, caller-masked).
-__device__ __forceinline__ void load_f32_unal(const void* row, int col, int C, float (&v)[4]) {
-  const float* rp = static_cast<const float*>(row);
-  const int sh = (col < C && col + 4 > C) ? col + 4 - C : 0;
-  const int lc = col + 4 <= C ? col : (col < C ? C - 4 : 0);
-  const float4 q = load_f4u(rp + lc);
-  const float f[4] = {q.x, q.y, q.z, q.w};
-  const float ninf = -__builtin_huge_valf();
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    float r = f[e];
-    r = sh == 1 ? (e + 1 < 4 ? f[e + 1 < 4 ? e + 1 : 3] : ninf) : r;
-    r = sh == 2 ? (e + 2 < 4 ? f[e + 2 < 4 ? e + 2 : 3] : ninf) : r;
-    r = sh == 3 ? (e + 3 < 4 ? f[e + 3 < 4 ? e + 3 : 3] : ninf) : r;
-    v[e] = r;
-  }
-}
-
-// row loads of the wide kernels: the aligned form (16-B aligned rows, C % VEC == 0) or UNAL
+// (tea_common.h load_f4u).  Loads only compute an address (no use of the loaded registers, so
+// every load of a row stays in flight together); the lane whose 4 columns straddle the row end
+// (C % 4 != 0) loads the row's LAST 4 columns, and unal_fix_tail - run after all of a chunk's
+// loads are issued, on the one wave-load that holds the row end (a wave-uniform test) -
+// rotates them into place, so element e holds nominal column col + e and the columns past C
+// read -inf: every consumer below (max, target select, tie / rank counts, argmax indices) is
+// unchanged.  Lanes wholly past C keep the aligned paths' convention (clamped copies of
+// columns 0..3, masked where the consumer needs it).
 template <int KIND, int VEC, bool UNAL>
 __device__ __forceinline__ void load_row_vec(const void* row, int col, int C, float (&v)[VEC]) {
   if constexpr (UNAL) {
     static_assert(KIND == 0 && VEC == 4, "UNAL rows are f32");
-    load_f32_unal(row, col, C, v);
+    const int lc = col + 4 <= C ? col : (col < C ? C - 4 : 0);
+    const float4 q = load_f4u(static_cast<const float*>(row) + lc);
+    v[0] = q.x;
+    v[1] = q.y;
+    v[2] = q.z;
+    v[3] = q.w;
   } else {
     load_vec<KIND, VEC>(row, col < C ? col : 0, v);
+  }
+}
+
+// `n` wave-loads starting at column `base` (wave-load u covers base + u * 256 ...): rotate the
+// straddling lane's values of the wave-load holding column C & ~3 (only when C % 4 != 0)
+template <int N>
+__device__ __forceinline__ void unal_fix_tail(float (&v)[N][4], int base, int C, int lane) {
+  if ((C & 3) == 0) return;
+  const int cv = C & ~3, sh = 4 - (C & 3);
+  constexpr int STEP = kWave * 4;
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const int ub = base + u * STEP;
+    if (cv >= ub && cv < ub + STEP) {  // wave-uniform
+      const bool me = lane == (cv - ub) / 4;
+      const float ninf = -__builtin_huge_valf();
+      float r[4];  // r[e] = v[e + sh] (past the row end: -inf), selects on the uniform sh
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float s1 = e + 1 < 4 ? v[u][e + 1 < 4 ? e + 1 : 3] : ninf;
+        const float s2 = e + 2 < 4 ? v[u][e + 2 < 4 ? e + 2 : 3] : ninf;
+        const float s3 = e + 3 < 4 ? v[u][e + 3 < 4 ? e + 3 : 3] : ninf;
+        r[e] = sh == 1 ? s1 : sh == 2 ? s2 : s3;
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[u][e] = me ? r[e] : v[u][e];
+    }
   }
 }
 
@@ -203,6 +220,29 @@ __device__ __noinline__ int row_argmax_exact(const void* rp, int C, int lane) {
   return bi;
 }
 
+// one chunk of a row (kChunkLoads wave-loads from column `base`): unconditional clamped loads
+// only (a guarded load compiles to a branch and a vmcnt(0) per load, and any use of a loaded
+// register here would wait for it - serialising the next chunk's prefetch behind this one)
+template <int KIND, int VEC, bool UNAL>
+__device__ __forceinline__ void load_chunk(const void* rp, int base, int C, int lane, float (&v)[kChunkLoads][VEC]) {
+  constexpr int STEP = kWave * VEC;
+#pragma unroll
+  for (int u = 0; u < kChunkLoads; ++u) load_row_vec<KIND, VEC, UNAL>(rp, base + u * STEP + lane * VEC, C, v[u]);
+}
+
+// ... and when the chunk is consumed: the UNAL tail rotation, columns past C -> -inf
+template <int VEC, bool UNAL>
+__device__ __forceinline__ void finish_chunk(float (&v)[kChunkLoads][VEC], int base, int C, int lane) {
+  constexpr int STEP = kWave * VEC;
+  if constexpr (UNAL) unal_fix_tail<kChunkLoads>(v, base, C, lane);
+#pragma unroll
+  for (int u = 0; u < kChunkLoads; ++u) {
+    const bool in = base + u * STEP + lane * VEC < C;
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) v[u][e] = in ? v[u][e] : -__builtin_huge_valf();
+  }
+}
+
 // PRED = false: the caller needs only "was the prediction correct" (micro / macro accuracy:
 // no predicted-label histograms) and the row fits one chunk (C <= 1024 f32 / 2048 16-bit).
 // Then the wave compares the row max with the target's own score first: a row whose target is
@@ -234,6 +274,7 @@ __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
 #pragma unroll
       for (int u = 0; u < kChunkLoads; ++u) load_row_vec<KIND, VEC, UNAL>(rp, u * STEP + lane * VEC, C, v[u]);
       t = load_target(a.target, a.tg_dt, row);
+      if constexpr (UNAL) unal_fix_tail<kChunkLoads>(v, 0, C, lane);
 #pragma unroll
       for (int u = 0; u < kChunkLoads; ++u) {
         const bool in = u * STEP + lane * VEC < C;
@@ -278,18 +319,18 @@ __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
       float bv = -__builtin_huge_valf();
       int bi = 0x7fffffff;
       bool saw_nan = false;
+      // rows longer than one chunk: the next chunk's loads are issued before this chunk is
+      // reduced (two chunks in flight; v1 waited one full round trip per chunk)
+      float nx[kChunkLoads][VEC];
+      load_chunk<KIND, VEC, UNAL>(rp, 0, C, lane, nx);
       for (int base = 0; base < C; base += CHUNK) {
         float v[kChunkLoads][VEC];
 #pragma unroll
-        for (int u = 0; u < kChunkLoads; ++u) {
-          const int col = base + u * STEP + lane * VEC;
-          if (col < C) {
-            load_row_vec<KIND, VEC, UNAL>(rp, col, C, v[u]);
-          } else {
+        for (int u = 0; u < kChunkLoads; ++u)
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) v[u][e] = -__builtin_huge_valf();
-          }
-        }
+          for (int e = 0; e < VEC; ++e) v[u][e] = nx[u][e];
+        if (base + CHUNK < C) load_chunk<KIND, VEC, UNAL>(rp, base + CHUNK, C, lane, nx);
+        finish_chunk<VEC, UNAL>(v, base, C, lane);
         // phase 1: NaN-propagating lane max; phase 2: first column holding it
         float m = v[0][0];
 #pragma unroll
@@ -324,18 +365,16 @@ __device__ __forceinline__ void cls_wide_body(const ClsCountsArgs& a) {
       const bool t_ok = t >= 0 && t < C;
       const float xt = t_ok ? load_one<KIND>(rp, t) : __builtin_nanf("");
       int cnt = 0;
+      float nx[kChunkLoads][VEC];
+      load_chunk<KIND, VEC, UNAL>(rp, 0, C, lane, nx);
       for (int base = 0; base < C; base += CHUNK) {
         float v[kChunkLoads][VEC];
 #pragma unroll
-        for (int u = 0; u < kChunkLoads; ++u) {
-          const int col = base + u * STEP + lane * VEC;
-          if (col < C) {
-            load_row_vec<KIND, VEC, UNAL>(rp, col, C, v[u]);
-          } else {
+        for (int u = 0; u < kChunkLoads; ++u)
 #pragma unroll
-            for (int e = 0; e < VEC; ++e) v[u][e] = -__builtin_huge_valf();
-          }
-        }
+          for (int e = 0; e < VEC; ++e) v[u][e] = nx[u][e];
+        if (base + CHUNK < C) load_chunk<KIND, VEC, UNAL>(rp, base + CHUNK, C, lane, nx);
+        finish_chunk<VEC, UNAL>(v, base, C, lane);
 #pragma unroll
         for (int u = 0; u < kChunkLoads; ++u)
 #pragma unroll
@@ -414,6 +453,7 @@ __device__ __forceinline__ void micro_rows(const void* __restrict__ input, const
 #pragma unroll
     for (int u = 0; u < kChunkLoads; ++u) load_row_vec<KIND, VEC, UNAL>(rp, u * STEP + lane * VEC, C, f[u]);
     const int64_t t = target[row];
+    if constexpr (UNAL) unal_fix_tail<kChunkLoads>(f, 0, C, lane);
     vec_t v;
 #pragma unroll
     for (int u = 0; u < kChunkLoads; ++u)
@@ -484,6 +524,7 @@ __device__ __forceinline__ bool micro_row(const MicroPendArgs& a, const char* __
   float f[kChunkLoads][VEC];
 #pragma unroll
   for (int u = 0; u < kChunkLoads; ++u) load_row_vec<KIND, VEC, UNAL>(rp, u * STEP + lane * VEC, C, f[u]);
+  if constexpr (UNAL) unal_fix_tail<kChunkLoads>(f, 0, C, lane);
   vec_t v;
 #pragma unroll
   for (int u = 0; u < kChunkLoads; ++u)

@@ -597,16 +597,16 @@ __global__ __launch_bounds__(kB) void moments_v2_kernel(MomentsArgs a) {
   }
   if (a.pend) {
     // deferred mode: this block owns slot rc of every column of its tile; ADD the partials
-    // (plain read-modify-write: one writer per launch, launches ordered by the stream) - no
-    // ticket, no fold on the launch's tail (launch_moments_fold runs when a state is read)
+    // (tea_common.h pend_add: one no-return atomic per slot, one writer per launch, launches
+    // ordered by the stream: deterministic) - no ticket, no fold on the launch's tail
+    // (launch_moments_fold runs when a state is read)
     for (int p = threadIdx.x; p < NS * TC; p += kB) {
       const int s = p / TC, c = p % TC;
       if (tbase + c >= d) continue;
       double v = 0.0;
 #pragma unroll
       for (int r = 0; r < RPP; ++r) v += lds[s][r][c];
-      double* q = a.pend + (static_cast<int64_t>(rc) * NS + s) * d + tbase + c;
-      *q += v;
+      pend_add(a.pend + (static_cast<int64_t>(rc) * NS + s) * d + tbase + c, v);
     }
     if (tile == 0 && threadIdx.x == 0) {
       double v = 0.0;
@@ -615,7 +615,7 @@ __global__ __launch_bounds__(kB) void moments_v2_kernel(MomentsArgs a) {
       } else {
         v = static_cast<double>(r1 > r0 ? r1 - r0 : 0);
       }
-      a.pend[static_cast<int64_t>(a.pend_slots) * NS * d + rc] += v;
+      pend_add(a.pend + static_cast<int64_t>(a.pend_slots) * NS * d + rc, v);
     }
     return;
   }

@@ -253,12 +253,30 @@ __global__ __launch_bounds__(kB) void row_sums_single_kernel(RowSumsArgs g) {
 // stats, contiguously (combined by row_sums_combine_kernel in block order: deterministic).
 // A last-block-combines variant (agent release per block + ticket) was measured at 46 us for
 // 8192 x 1000 (2000 release fences) against 14.6 + 10 us for two launches.
-template <int NEED, bool HAS_W, bool VEC>
+template <int NEED, bool HAS_W, bool VEC, int VPT = kVecPerThread>
 __global__ __launch_bounds__(kB) void row_sums_grid_kernel(RowSumsArgs g, int64_t span) {
   const int64_t r = blockIdx.y;
   const int64_t lo = static_cast<int64_t>(blockIdx.x) * span;
   const int64_t hi = min(g.n, lo + span);
-  const Acc a = block_merge<NEED>(reduce_range<NEED, HAS_W, VEC>(g, r, lo, hi));
+  const Acc a = block_merge<NEED>(reduce_range<NEED, HAS_W, VEC, kB, VPT>(g, r, lo, hi));
+  if (g.pend) {
+    // deferred mode: this block's slot, pre-scaled (a scalar weight differs per update), ADDED
+    if (threadIdx.x == 0) {
+      double* p = g.pend + r * kRowPendStats * g.pend_blocks + blockIdx.x;
+      const double cnt = static_cast<double>(hi > lo ? hi - lo : 0);
+      const double ws = HAS_W ? 1.0 : g.w_scalar;
+#pragma unroll
+      for (int k = 0; k < kRowSums; ++k) {
+        if (k == kW) {
+          if (NEED & bit(kW) || !HAS_W) pend_add(p + k * g.pend_blocks, HAS_W ? a.v[kW] : ws * cnt);
+        } else if (NEED & bit(k)) {
+          pend_add(p + k * g.pend_blocks, k == kSSE ? a.v[k] : ws * a.v[k]);
+        }
+      }
+      pend_add(p + kRowSums * g.pend_blocks, cnt);
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
     double* p = g.ws + r * kNStat * g.blocks + blockIdx.x;
 #pragma unroll
@@ -400,6 +418,35 @@ __global__ __launch_bounds__(kB) void row_sums_wt_kernel(RowSumsArgs g, int64_t 
   if (threadIdx.x == 0) finish_row<HAS_W>(g, r, m);
 }
 
+// deferred-mode fold: one block per row; every thread sums a strided share of the slots of
+// each statistic (fixed partition + fixed LDS tree: deterministic), zeroes them, and thread 0
+// applies the ADD outputs
+__global__ __launch_bounds__(kB) void row_sums_pend_fold_kernel(RowSumsArgs g, int used) {
+  const int64_t r = blockIdx.x;
+  __shared__ double lds[kRowPendStats][kB];
+  double* base = g.pend + r * kRowPendStats * g.pend_blocks;
+  for (int k = 0; k < kRowPendStats; ++k) {
+    double v = 0.0;
+    for (int b = threadIdx.x; b < used; b += kB) {
+      v += base[k * g.pend_blocks + b];
+      base[k * g.pend_blocks + b] = 0.0;
+    }
+    lds[k][threadIdx.x] = v;
+  }
+  __syncthreads();
+  for (int h = kB / 2; h >= 1; h >>= 1) {
+    if (threadIdx.x < h)
+      for (int k = 0; k < kRowPendStats; ++k) lds[k][threadIdx.x] += lds[k][threadIdx.x + h];
+    __syncthreads();
+  }
+  if (threadIdx.x != 0) return;
+  for (int k = 0; k < g.nout; ++k) {
+    const RowSumsOut& o = g.out[k];
+    if (o.first_row_only && r != 0) continue;
+    store_out(o, r, o.stat == kCOUNT ? lds[kRowSums][0] : lds[o.stat][0]);
+  }
+}
+
 bool vec_ok(const void* p, DType dt, int64_t /*rs*/, int64_t cs) {
   return p == nullptr || (dt == DType::f32 && cs == 1);  // 16-B loads need only 4-B alignment
 }
@@ -425,6 +472,20 @@ int launch_need(const RowSumsArgs& a, bool vec, hipStream_t stream) {
     const int64_t chunks = (a.n + kPerBlock - 1) / kPerBlock;
     const int64_t span = (chunks + a.blocks - 1) / a.blocks * kPerBlock;
     const dim3 grid(static_cast<unsigned>(a.blocks), static_cast<unsigned>(a.rows));
+    if (a.pend) {  // deferred: no combine launch; 8 x 16-B loads per operand in flight per thread
+      static const int vpt = [] {
+        const char* e = std::getenv("TORCHEVAL_AMD_K5B_PEND_VPT");
+        return (e != nullptr && std::atoi(e) == 4) ? 4 : 8;
+      }();
+      if (vpt == 8) {
+        if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true, 8>), grid, dim3(kB), 0, stream, a, span);
+        else hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, false, 8>), grid, dim3(kB), 0, stream, a, span);
+      } else {
+        if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true>), grid, dim3(kB), 0, stream, a, span);
+        else hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, false>), grid, dim3(kB), 0, stream, a, span);
+      }
+      return static_cast<int>(hipGetLastError());
+    }
     if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true>), grid, dim3(kB), 0, stream, a, span);
     else hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, false>), grid, dim3(kB), 0, stream, a, span);
     if (a.rows == 1) {
@@ -471,9 +532,25 @@ int row_sums_fold_blocks(int64_t rows, int64_t n) {
   return static_cast<int>(std::min<int64_t>(per_row, (n + kFoldChunk - 1) / kFoldChunk));
 }
 
+int launch_row_sums_fold(const RowSumsArgs& a, int blocks_used, hipStream_t stream) {
+  if (a.rows <= 0 || blocks_used <= 0 || !a.pend) return 0;
+  if (blocks_used > a.pend_blocks) return -2;
+  for (int k = 0; k < a.nout; ++k)
+    if (a.out[k].op != kAdd || a.out[k].stat == kTMIN || a.out[k].stat == kTMAX || a.out[k].stat == kRANGE) return -2;
+  hipLaunchKernelGGL(row_sums_pend_fold_kernel, dim3(static_cast<unsigned>(a.rows)), dim3(kB), 0, stream, a,
+                     blocks_used);
+  return static_cast<int>(hipGetLastError());
+}
+
 int launch_row_sums(const RowSumsArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
-  if ((a.n > 0 && a.x == nullptr) || (a.blocks > 1 && !a.ws)) return -2;  // empty rows: outputs only
+  if (a.pend) {  // deferred mode: grid blocks only, within the slots, sums / W / COUNT ADD outputs
+    if (a.blocks < 2 || a.blocks > a.pend_blocks || a.ticket) return -2;
+    for (int k = 0; k < a.nout; ++k)
+      if (a.out[k].op != kAdd || a.out[k].stat == kTMIN || a.out[k].stat == kTMAX || a.out[k].stat == kRANGE)
+        return -2;
+  }
+  if ((a.n > 0 && a.x == nullptr) || (a.blocks > 1 && !a.ws && !a.pend)) return -2;  // empty rows: outputs only
   if (a.ticket && a.blocks < 2) return -2;
   const bool vec = vec_ok(a.x, a.x_dt, a.x_rs, a.x_cs) && vec_ok(a.t, a.t_dt, a.t_rs, a.t_cs) &&
                    vec_ok(a.w, a.w_dt, a.w_rs, a.w_cs);

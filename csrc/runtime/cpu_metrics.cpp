@@ -17,38 +17,18 @@
 #include <tuple>
 #include <vector>
 
+#include "tea_cpu_core.h"
 #include "tea_runtime.h"
 
 namespace {
 
 template <typename T>
 int64_t count_correct(const T* x, int64_t n, int64_t c, int64_t ld, const int64_t* t, int64_t ts, int64_t k) {
-  int64_t correct = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const T* row = x + i * ld;
-    const int64_t y = t[i * ts];
-    if (k == 1) {
-      int64_t best = 0;
-      T bv = row[0];
-      bool bnan = std::isnan(static_cast<double>(bv));
-      for (int64_t j = 1; j < c && !bnan; ++j) {
-        const T v = row[j];
-        if (std::isnan(static_cast<double>(v))) {
-          best = j;
-          bnan = true;
-        } else if (v > bv) {
-          bv = v;
-          best = j;
-        }
-      }
-      correct += (best == y);
-    } else {
-      TORCH_CHECK(y >= 0 && y < c, "index ", y, " is out of bounds for dimension 1 with size ", c);
-      const T ty = row[y];
-      int64_t above = 0;
-      for (int64_t j = 0; j < c; ++j) above += (row[j] > ty);
-      correct += (above < k);
-    }
+  int64_t bad = -1;
+  const int64_t correct = tea_cpu::count_correct(x, n, c, ld, t, ts, k, &bad);
+  if (bad >= 0) {
+    const int64_t y = t[bad * ts];
+    TORCH_CHECK(false, "index ", y, " is out of bounds for dimension 1 with size ", c);
   }
   return correct;
 }
@@ -129,21 +109,32 @@ bool cpu_labels_valid(const at::Tensor& input, const at::Tensor& target, int64_t
   return true;
 }
 
-// torch.argmax of one row: first index of the max, NaN counts as the max
-template <typename T>
-int64_t row_argmax(const T* row, int64_t c) {
-  int64_t best = 0;
-  T bv = row[0];
-  if (std::isnan(static_cast<double>(bv))) return 0;
-  for (int64_t j = 1; j < c; ++j) {
-    const T v = row[j];
-    if (std::isnan(static_cast<double>(v))) return j;
-    if (v > bv) {
-      bv = v;
-      best = j;
-    }
+tea_cpu::Labels labels_of(const at::Tensor& t) {
+  tea_cpu::Labels l;
+  l.p = t.data_ptr();
+  l.i64 = t.scalar_type() == at::kLong;
+  l.stride = t.stride(0);
+  return l;
+}
+
+// a 1-D / 2-D numeric tensor for tea_cpu::Doubles (unsupported dtypes raise with `who`)
+tea_cpu::Doubles doubles_of(const at::Tensor& t, const char* who) {
+  tea_cpu::Doubles d;
+  d.p = t.data_ptr();
+  d.s0 = t.dim() >= 1 ? t.stride(0) : 0;
+  d.s1 = t.dim() >= 2 ? t.stride(1) : 0;
+  switch (t.scalar_type()) {
+    case at::kFloat: d.dt = tea_cpu::Num::f32; break;
+    case at::kDouble: d.dt = tea_cpu::Num::f64; break;
+    case at::kLong: d.dt = tea_cpu::Num::i64; break;
+    case at::kInt: d.dt = tea_cpu::Num::i32; break;
+    case at::kShort: d.dt = tea_cpu::Num::i16; break;
+    case at::kChar: d.dt = tea_cpu::Num::i8; break;
+    case at::kByte: d.dt = tea_cpu::Num::u8; break;
+    case at::kBool: d.dt = tea_cpu::Num::b8; break;
+    default: TORCH_CHECK(false, who, ": unsupported dtype ", t.scalar_type());
   }
-  return best;
+  return d;
 }
 
 float* opt_f32(const c10::optional<at::Tensor>& t, int64_t numel, const char* name) {
@@ -193,87 +184,37 @@ void cpu_cls_counts(const at::Tensor& input, const at::Tensor& target, int64_t k
     TORCH_CHECK(!err->is_cuda() && err->scalar_type() == at::kInt && err->numel() >= 1, "cpu_cls_counts: err int32");
     eb = err->data_ptr<int>();
   }
-  int64_t correct_rows = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t t = label_at(target, i);
-    const bool t_ok = t >= 0 && t < C;
-    int64_t pred = -1;
-    bool correct;
-    if (!scores) {
-      pred = label_at(input, i);
-      correct = pred == t;
-    } else if (k == 1) {
-      pred = input.scalar_type() == at::kFloat
-                 ? row_argmax(input.data_ptr<float>() + i * input.stride(0), C)
-                 : row_argmax(input.data_ptr<double>() + i * input.stride(0), C);
-      correct = pred == t;
-    } else {
-      int64_t above = 0;
-      if (t_ok) {
-        if (input.scalar_type() == at::kFloat) {
-          const float* row = input.data_ptr<float>() + i * input.stride(0);
-          for (int64_t j = 0; j < C; ++j) above += row[j] > row[t];
-        } else {
-          const double* row = input.data_ptr<double>() + i * input.stride(0);
-          for (int64_t j = 0; j < C; ++j) above += row[j] > row[t];
-        }
-      }
-      correct = t_ok && above < k;
-    }
-    correct_rows += correct;
-    const bool p_ok = pred >= 0 && pred < C;
-    if (eb) {
-      if (!t_ok) *eb |= 1;
-      if (!p_ok && (cp || cm || (cf && !correct))) *eb |= 2;
-    }
-    if (t_ok) {
-      if (cc && correct) cc[t] += 1.f;
-      if (cl) cl[t] += 1.f;
-    }
-    if (p_ok && cp) cp[pred] += 1.f;
-    if (p_ok && cf && !correct) cf[pred] += 1.f;
-    if (t_ok && p_ok && cm) cm[t * C + pred] += 1.f;
-  }
-  if (mc) *mc += static_cast<float>(correct_rows);
-  if (mi) *mi += static_cast<float>(n - correct_rows);
-  if (mt) *mt += static_cast<float>(n);
-  if (mt2) *mt2 += static_cast<float>(n);
+  tea_cpu::ClsOut o;
+  o.mc = mc;
+  o.mt = mt;
+  o.mi = mi;
+  o.mt2 = mt2;
+  o.cc = cc;
+  o.cl = cl;
+  o.cp = cp;
+  o.cf = cf;
+  o.cm = cm;
+  o.err = eb;
+  const tea_cpu::Labels tl = labels_of(target);
+  const tea_cpu::Labels pl = scores ? tea_cpu::Labels{} : labels_of(input);
+  if (!scores)
+    tea_cpu::cls_counts<float>(nullptr, 0, pl, tl, n, C, k, o);
+  else if (input.scalar_type() == at::kFloat)
+    tea_cpu::cls_counts(input.data_ptr<float>(), input.stride(0), pl, tl, n, C, k, o);
+  else
+    tea_cpu::cls_counts(input.data_ptr<double>(), input.stride(0), pl, tl, n, C, k, o);
 }
 
 // ---- binned counts (the CPU twin of K4 for small batches, ops.binned) ----
 
-double as_double(const at::Tensor& t, int64_t off) {
-  switch (t.scalar_type()) {
-    case at::kLong: return static_cast<double>(t.data_ptr<int64_t>()[off]);
-    case at::kInt: return static_cast<double>(t.data_ptr<int32_t>()[off]);
-    case at::kBool: return t.data_ptr<bool>()[off] ? 1.0 : 0.0;
-    case at::kByte: return static_cast<double>(t.data_ptr<uint8_t>()[off]);
-    case at::kFloat: return static_cast<double>(t.data_ptr<float>()[off]);
-    case at::kDouble: return t.data_ptr<double>()[off];
-    default: TORCH_CHECK(false, "cpu_binned_counts: unsupported target dtype ", t.scalar_type());
-  }
-  return 0.0;
-}
-
 template <typename S>
 void binned_hist(const at::Tensor& scores, const at::Tensor& target, const at::Tensor& thr, int64_t mode,
                  std::vector<int64_t>& hist) {
-  const int64_t n = scores.size(0), C = scores.size(1), T = thr.size(0);
-  std::vector<S> th(T);  // thresholds in the score dtype, as thr.to(scores.dtype)
-  for (int64_t k = 0; k < T; ++k) th[k] = static_cast<S>(as_double(thr, k * thr.stride(0)));
-  const S* x = scores.data_ptr<S>();
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t lab = mode == 1 ? static_cast<int64_t>(as_double(target, i * target.stride(0))) : 0;
-    for (int64_t c = 0; c < C; ++c) {
-      const S v = x[i * scores.stride(0) + c * scores.stride(1)];
-      // searchsorted(thr, v, right=True): thresholds <= v; NaN sorts past every threshold
-      int64_t b = T;
-      if (!std::isnan(static_cast<double>(v))) b = std::upper_bound(th.begin(), th.end(), v) - th.begin();
-      const bool pos = mode == 1 ? lab == c
-                                 : as_double(target, i * target.stride(0) + c * target.stride(1)) == 1.0;
-      ++hist[(b * C + c) * 2 + (pos ? 1 : 0)];
-    }
-  }
+  const tea_cpu::Doubles tv = doubles_of(thr, "cpu_binned_counts");
+  std::vector<S> th(thr.size(0));  // thresholds in the score dtype, as thr.to(scores.dtype)
+  for (int64_t k = 0; k < thr.size(0); ++k) th[k] = static_cast<S>(tv.at(k));
+  tea_cpu::binned_hist(scores.data_ptr<S>(), scores.stride(0), scores.stride(1), scores.size(0), scores.size(1), th,
+                       mode, doubles_of(target, "cpu_binned_counts"), hist);
 }
 
 // scores [n, C] float32 / float64 (any strides), target [n, C] (mode 0) or [n] labels (mode 1),
@@ -290,25 +231,13 @@ void cpu_binned_counts(const at::Tensor& scores, const at::Tensor& target, const
   for (const at::Tensor* o : {&tp, &fp, &fn})
     TORCH_CHECK(o->scalar_type() == at::kFloat && !o->is_cuda() && o->dim() == 2 && o->size(0) == T &&
                     o->size(1) == C, "cpu_binned_counts: outputs must be float32 [T, C]");
-  std::vector<int64_t> hist((T + 1) * C * 2, 0);
+  TORCH_CHECK(tp.strides() == fp.strides() && tp.strides() == fn.strides(), "cpu_binned_counts: outputs share strides");
+  std::vector<int64_t> hist;
   if (scores.scalar_type() == at::kFloat) binned_hist<float>(scores, target, thr, mode, hist);
   else if (scores.scalar_type() == at::kDouble) binned_hist<double>(scores, target, thr, mode, hist);
   else TORCH_CHECK(false, "cpu_binned_counts: float32 / float64 scores");
-  float* ptp = tp.data_ptr<float>();
-  float* pfp = fp.data_ptr<float>();
-  float* pfn = fn.data_ptr<float>();
-  for (int64_t c = 0; c < C; ++c) {
-    int64_t pos_all = 0;
-    for (int64_t b = 0; b <= T; ++b) pos_all += hist[(b * C + c) * 2 + 1];
-    int64_t sp = 0, sn = 0;  // suffix sums over bins > k
-    for (int64_t k = T - 1; k >= 0; --k) {
-      sp += hist[((k + 1) * C + c) * 2 + 1];
-      sn += hist[((k + 1) * C + c) * 2];
-      ptp[k * tp.stride(0) + c * tp.stride(1)] += static_cast<float>(sp);
-      pfp[k * fp.stride(0) + c * fp.stride(1)] += static_cast<float>(sn);
-      pfn[k * fn.stride(0) + c * fn.stride(1)] += static_cast<float>(pos_all - sp);
-    }
-  }
+  tea_cpu::binned_suffix(hist, T, C, tp.data_ptr<float>(), fp.data_ptr<float>(), fn.data_ptr<float>(), tp.stride(0),
+                         tp.stride(1));
 }
 
 // ---- tie-aware binary AUROC / AUPRC rows (host twin of the K3 sort-scan, _curve.py) ----
@@ -335,38 +264,6 @@ void row_as_double(const at::Tensor& t, int64_t r, std::vector<double>& out) {
   }
 }
 
-template <typename S>
-void auc_row(const S* x, int64_t n, int64_t sx, const std::vector<double>& t, const std::vector<double>* w,
-             std::vector<int64_t>& idx, double& roc_out, double& pr_out) {
-  idx.resize(n);
-  for (int64_t i = 0; i < n; ++i) idx[i] = i;
-  // torch.sort(descending=True) order: NaN above everything; ties in any order (only the
-  // tie-group ends are used)
-  std::sort(idx.begin(), idx.end(), [&](int64_t i, int64_t j) {
-    const S a = x[i * sx], b = x[j * sx];
-    if (std::isnan(static_cast<double>(a))) return !std::isnan(static_cast<double>(b));
-    if (std::isnan(static_cast<double>(b))) return false;
-    return a > b;
-  });
-  double tp = 0.0, fp = 0.0, tp0 = 0.0, fp0 = 0.0, roc = 0.0, pr = 0.0;
-  for (int64_t k = 0; k < n; ++k) {
-    const int64_t i = idx[k];
-    const double wi = w ? (*w)[i] : 1.0;
-    tp += wi * t[i];
-    fp += wi * (1.0 - t[i]);
-    // a group ends where the next sorted score differs (NaN != NaN: every NaN ends its own)
-    if (k + 1 < n && x[idx[k + 1] * sx] == x[i * sx]) continue;
-    roc += (fp - fp0) * (tp + tp0);
-    const double den = tp + fp;
-    pr += (tp - tp0) * (den > 0 ? tp / den : 0.0);
-    tp0 = tp;
-    fp0 = fp;
-  }
-  roc /= 2;
-  roc_out = tp * fp == 0.0 ? 0.5 : roc / (tp * fp);
-  pr_out = tp == 0.0 ? 0.0 : pr / tp;
-}
-
 // x [rows, n] float32 / float64 scores, t [rows, n] targets, w optional [rows, n] weights ->
 // (roc, pr) float64 [rows]: AUROC (0.5 when a row has no positives or no negatives) and AUPRC
 // (0 without positives) with the reference's tie semantics
@@ -387,9 +284,9 @@ std::tuple<at::Tensor, at::Tensor> cpu_binary_auc(const at::Tensor& x, const at:
     if (w.has_value()) row_as_double(*w, r, wv);
     const std::vector<double>* wp = w.has_value() ? &wv : nullptr;
     if (x.scalar_type() == at::kFloat)
-      auc_row(x.data_ptr<float>() + r * x.stride(0), n, x.stride(1), tv, wp, idx, roc_[r], pr_[r]);
+      tea_cpu::auc_row(x.data_ptr<float>() + r * x.stride(0), n, x.stride(1), tv, wp, idx, roc_[r], pr_[r]);
     else if (x.scalar_type() == at::kDouble)
-      auc_row(x.data_ptr<double>() + r * x.stride(0), n, x.stride(1), tv, wp, idx, roc_[r], pr_[r]);
+      tea_cpu::auc_row(x.data_ptr<double>() + r * x.stride(0), n, x.stride(1), tv, wp, idx, roc_[r], pr_[r]);
     else
       TORCH_CHECK(false, "cpu_binary_auc: float32 / float64 scores");
   }
@@ -398,27 +295,16 @@ std::tuple<at::Tensor, at::Tensor> cpu_binary_auc(const at::Tensor& x, const at:
 
 // ---- binary accuracy (host twin of binary_counts' accuracy contract) ----
 
-template <typename S>
-int64_t count_binary_correct(const S* x, int64_t n, int64_t sx, const at::Tensor& target, S thr) {
-  std::vector<double> tv;
-  row_as_double(target.unsqueeze(0), 0, tv);
-  int64_t correct = 0;
-  for (int64_t i = 0; i < n; ++i) {
-    // torch.where(input < threshold, 0, 1) with the threshold in the input's dtype (NaN -> 1)
-    const double pred = x[i * sx] < thr ? 0.0 : 1.0;
-    correct += (pred == tv[i]);
-  }
-  return correct;
-}
-
 int64_t count_binary(const at::Tensor& input, const at::Tensor& target, double threshold) {
   TORCH_CHECK(!input.is_cuda() && !target.is_cuda() && input.dim() == 1 && target.dim() == 1 &&
                   input.size(0) == target.size(0), "cpu_binary_accuracy: CPU [N] input and target");
   const int64_t n = input.size(0);
   if (input.scalar_type() == at::kFloat)
-    return count_binary_correct(input.data_ptr<float>(), n, input.stride(0), target, static_cast<float>(threshold));
+    return tea_cpu::count_binary_correct(input.data_ptr<float>(), n, input.stride(0), doubles_of(target, "cpu_binary_accuracy"),
+                                         static_cast<float>(threshold));
   TORCH_CHECK(input.scalar_type() == at::kDouble, "cpu_binary_accuracy: float32 / float64 input");
-  return count_binary_correct(input.data_ptr<double>(), n, input.stride(0), target, threshold);
+  return tea_cpu::count_binary_correct(input.data_ptr<double>(), n, input.stride(0),
+                                       doubles_of(target, "cpu_binary_accuracy"), threshold);
 }
 
 // functional: 0-d float32 accuracy (NaN for an empty batch, like 0 / 0)
@@ -464,18 +350,6 @@ void target_as_i64(const at::Tensor& t, std::vector<int64_t>& out) {
   }
 }
 
-template <typename S>
-void prf_sums(const S* x, int64_t n, int64_t sx, S thr, const std::vector<int64_t>& t, int64_t& s_prod,
-              int64_t& s_and, int64_t& s_t, int64_t& s_pred) {
-  for (int64_t i = 0; i < n; ++i) {
-    const int64_t pred = x[i * sx] < thr ? 0 : 1;  // torch.where(input < threshold, 0, 1)
-    s_prod += pred * t[i];
-    s_and += pred & t[i];
-    s_t += t[i];
-    s_pred += pred;
-  }
-}
-
 void prf_all_sums(const at::Tensor& input, const at::Tensor& target, double threshold, int64_t* sums) {
   TORCH_CHECK(!input.is_cuda() && !target.is_cuda() && input.dim() == 1 && target.dim() == 1 &&
                   input.size(0) == target.size(0), "cpu_binary_prf: CPU [N] input and target");
@@ -483,10 +357,9 @@ void prf_all_sums(const at::Tensor& input, const at::Tensor& target, double thre
   target_as_i64(target, tv);
   const int64_t n = input.size(0);
   if (input.scalar_type() == at::kFloat)
-    prf_sums(input.data_ptr<float>(), n, input.stride(0), static_cast<float>(threshold), tv, sums[0], sums[1],
-             sums[2], sums[3]);
+    tea_cpu::prf_sums(input.data_ptr<float>(), n, input.stride(0), static_cast<float>(threshold), tv, sums);
   else if (input.scalar_type() == at::kDouble)
-    prf_sums(input.data_ptr<double>(), n, input.stride(0), threshold, tv, sums[0], sums[1], sums[2], sums[3]);
+    tea_cpu::prf_sums(input.data_ptr<double>(), n, input.stride(0), threshold, tv, sums);
   else
     TORCH_CHECK(false, "cpu_binary_prf: float32 / float64 input");
 }
@@ -560,22 +433,9 @@ template <typename S>
 void mse_sums(const at::Tensor& x, const at::Tensor& t, const c10::optional<at::Tensor>& w, std::vector<double>& sse,
               double& sw) {
   const int64_t n = x.size(0), d = x.dim() == 2 ? x.size(1) : 1;
-  const int64_t xs0 = x.stride(0), xs1 = x.dim() == 2 ? x.stride(1) : 0;
-  const int64_t ts0 = t.stride(0), ts1 = t.dim() == 2 ? t.stride(1) : 0;
-  const S* px = x.data_ptr<S>();
-  const S* pt = t.data_ptr<S>();
-  const S* pw = w.has_value() ? w->data_ptr<S>() : nullptr;
-  const int64_t ws0 = w.has_value() ? w->stride(0) : 0;
-  sse.assign(d, 0.0);
-  sw = 0.0;
-  for (int64_t i = 0; i < n; ++i) {
-    const double wi = pw ? static_cast<double>(pw[i * ws0]) : 1.0;
-    sw += wi;
-    for (int64_t c = 0; c < d; ++c) {
-      const double e = static_cast<double>(pt[i * ts0 + c * ts1]) - static_cast<double>(px[i * xs0 + c * xs1]);
-      sse[c] += wi * e * e;
-    }
-  }
+  tea_cpu::mse_sums(x.data_ptr<S>(), x.stride(0), x.dim() == 2 ? x.stride(1) : 0, t.data_ptr<S>(), t.stride(0),
+                    t.dim() == 2 ? t.stride(1) : 0, w.has_value() ? w->data_ptr<S>() : nullptr,
+                    w.has_value() ? w->stride(0) : 0, n, d, sse, sw);
 }
 
 // sse / (clamp(|sw|, eps) * sign(sw)) per column in the input dtype (the reference's
@@ -627,17 +487,8 @@ at::Tensor r2_impl(const at::Tensor& x, const at::Tensor& t, int64_t mode, int64
   const int64_t n = x.size(0), d = x.dim() == 2 ? x.size(1) : 1;
   const int64_t xs0 = x.stride(0), xs1 = x.dim() == 2 ? x.stride(1) : 0;
   const int64_t ts0 = t.stride(0), ts1 = t.dim() == 2 ? t.stride(1) : 0;
-  const S* px = x.data_ptr<S>();
-  const S* pt = t.data_ptr<S>();
-  std::vector<double> sso(d, 0.0), so(d, 0.0), rss(d, 0.0);
-  for (int64_t i = 0; i < n; ++i)
-    for (int64_t c = 0; c < d; ++c) {
-      const double tv = static_cast<double>(pt[i * ts0 + c * ts1]);
-      const double e = tv - static_cast<double>(px[i * xs0 + c * xs1]);
-      sso[c] += tv * tv;
-      so[c] += tv;
-      rss[c] += e * e;
-    }
+  std::vector<double> sso, so, rss;
+  tea_cpu::r2_sums(x.data_ptr<S>(), xs0, xs1, t.data_ptr<S>(), ts0, ts1, n, d, sso, so, rss);
   // the reference's arithmetic in the input dtype: tss = sso - so^2 / n, r2 = 1 - rss / tss
   std::vector<S> tss(d), r2(d);
   S tss_sum = 0;

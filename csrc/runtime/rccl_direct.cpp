@@ -39,6 +39,7 @@
 #include <torch/library.h>
 
 #include <algorithm>
+#include <map>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -54,6 +55,7 @@
 
 #include "tea_kernels.h"
 #include "tea_runtime.h"
+#include "tea_watchdog.h"
 
 namespace {
 
@@ -99,261 +101,9 @@ const RcclApi& api() {
 }
 
 // ------------------------------------------------------------------ communicator table
-enum CommState : int { kOk = 0, kFailed = 1, kAborted = 2, kDestroyed = 3 };
-
-struct Comm {
-  ncclComm_t comm = nullptr;
-  int device = 0;
-  int64_t timeout_ms = 600000;
-  std::atomic<int> state{kOk};
-  bool observed = false;  // a blocking waiter reported the failure itself (no teardown)
-  bool teardown = false;  // decided when the failure is detected (env read then, not at abort)
-  std::string reason;
-  // completion tracking (under g_mu): one probe event in flight per communicator.  Collectives
-  // enqueued while a probe is pending are counted; when the probe retires, the watchdog records
-  // a follow-up probe behind them on their stream (hipEventRecord costs ~5 us of host time, so
-  // a burst of syncs pays it once, not per sync)
-  int probes = 0;
-  uint64_t untracked = 0;
-  hipStream_t last_stream = nullptr;  // nullptr is a real stream here: the device's null stream
-  bool has_last = false;              // a collective was ever enqueued (last_stream is valid)
-};
-
-struct Pending {
-  hipEvent_t ev;
-  int64_t handle;
-  Clock::time_point deadline;
-  uint64_t seq;  // unique per tracked collective (events are pooled and reused)
-};
-
-// Process-lifetime state, never destroyed: a watchdog still running when static destructors
-// start (a program that skipped Python's atexit) must not find its mutex or queues gone.
-std::mutex& g_mu = *new std::mutex;
-std::condition_variable& g_cv = *new std::condition_variable;
-std::vector<std::unique_ptr<Comm>>& g_comms = *new std::vector<std::unique_ptr<Comm>>;  // handle = index
-std::deque<Pending>& g_pending = *new std::deque<Pending>;
-std::vector<hipEvent_t>& g_event_pool = *new std::vector<hipEvent_t>;
-std::vector<int64_t>& g_abort_queue = *new std::vector<int64_t>;
-uint64_t g_seq = 0;  // under g_mu
-std::thread* g_watchdog = nullptr;  // leaked on purpose: joined by rccl_shutdown, never destroyed at exit
-bool g_stop = false;
-
-Comm& comm_ref(int64_t handle) {
-  TORCH_CHECK(handle >= 0 && handle < static_cast<int64_t>(g_comms.size()) && g_comms[handle],
-              "rccl_direct: invalid communicator handle ", handle);
-  return *g_comms[handle];
-}
-
-ncclComm_t usable_comm(int64_t handle) {
-  std::lock_guard<std::mutex> lock(g_mu);
-  Comm& c = comm_ref(handle);
-  const int s = c.state.load();
-  TORCH_CHECK(s == kOk, "rccl_direct: communicator ", handle, " is unusable (",
-              s == kDestroyed ? std::string("destroyed") : c.reason, ")");
-  return c.comm;
-}
-
-void check(ncclResult_t rc, const char* what) {
-  TORCH_CHECK(rc == ncclSuccess, "rccl_direct: ", what, " failed: ", api().error_string(rc));
-}
-
-bool teardown_on_failure() {
-  const char* e = std::getenv("TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING");
-  return !(e && std::strcmp(e, "0") == 0);
-}
-
-// caller holds g_mu
-void mark_failed_locked(int64_t handle, const std::string& why, bool observed) {
-  Comm& c = *g_comms[handle];
-  int expect = kOk;
-  if (!c.state.compare_exchange_strong(expect, kFailed)) return;
-  c.reason = why;
-  c.observed = observed;
-  c.teardown = !observed && teardown_on_failure();
-  g_abort_queue.push_back(handle);
-  g_cv.notify_all();
-}
-
-void abort_comm(int64_t handle) {
-  ncclComm_t comm;
-  int device;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    comm = g_comms[handle]->comm;
-    device = g_comms[handle]->device;
-  }
-  (void)hipSetDevice(device);
-  (void)api().comm_abort(comm);  // unblocks the communicator's kernels, frees its resources
-  bool teardown;
-  std::string why;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    Comm& c = *g_comms[handle];
-    c.state.store(kAborted);
-    c.probes = 0;
-    c.untracked = 0;
-    teardown = c.teardown;
-    why = c.reason;
-    // the aborted collectives' events complete once the stream drains; drop them unqueried
-    for (auto it = g_pending.begin(); it != g_pending.end();) {
-      if (it->handle == handle) {
-        (void)hipEventDestroy(it->ev);
-        it = g_pending.erase(it);
-      } else {
-        ++it;
-      }
-    }
-    g_cv.notify_all();
-  }
-  if (teardown) {
-    // c10d's default (TORCH_NCCL_ASYNC_ERROR_HANDLING): a collective that failed behind the
-    // program's back leaves every later result suspect, so the process goes down loudly
-    std::fprintf(stderr,
-                 "[torcheval_amd] rccl_direct: communicator %lld failed (%s); aborted it and tearing the process "
-                 "down (set TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING=0 to raise on the next sync instead)\n",
-                 static_cast<long long>(handle), why.c_str());
-    std::fflush(stderr);
-    std::abort();
-  }
-}
-
-bool watchdog_enabled();
-void watchdog_loop();
-
-// a probe event from the pool (or a new one); caller does NOT hold g_mu
-hipEvent_t take_event() {
-  hipEvent_t ev = nullptr;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    if (!g_event_pool.empty()) {
-      ev = g_event_pool.back();
-      g_event_pool.pop_back();
-    }
-  }
-  if (!ev && hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) ev = nullptr;
-  return ev;
-}
-
-// record a probe for `handle` on `stream` and queue it (caller does NOT hold g_mu and has
-// already counted it in c.probes); its sequence number, or 0 when the record failed (count undone)
-uint64_t record_probe(int64_t handle, hipStream_t stream) {
-  hipEvent_t ev = take_event();
-  const bool ok = ev && hipEventRecord(ev, stream) == hipSuccess;
-  std::lock_guard<std::mutex> lock(g_mu);
-  Comm& c = *g_comms[handle];
-  if (!ok) {
-    --c.probes;
-    if (ev) g_event_pool.push_back(ev);
-    return 0;
-  }
-  const uint64_t seq = ++g_seq;
-  g_pending.push_back({ev, handle, Clock::now() + std::chrono::milliseconds(c.timeout_ms), seq});
-  if (!g_watchdog) {
-    g_stop = false;
-    g_watchdog = new std::thread(watchdog_loop);
-  }
-  g_cv.notify_all();
-  return seq;
-}
-
-void watchdog_loop() {
-  auto last_async_poll = Clock::now();
-  struct Probe {
-    uint64_t seq;
-    hipEvent_t ev;
-    int64_t handle;
-    Clock::time_point deadline;
-    hipError_t q;
-  };
-  std::vector<Probe> batch;
-  std::vector<std::pair<int64_t, hipStream_t>> follow_ups;
-  std::unique_lock<std::mutex> lk(g_mu);
-  while (!g_stop) {
-    if (!g_abort_queue.empty()) {
-      const int64_t h = g_abort_queue.back();
-      g_abort_queue.pop_back();
-      lk.unlock();
-      abort_comm(h);
-      lk.lock();
-      continue;
-    }
-    if (g_pending.empty()) {
-      g_cv.wait_for(lk, std::chrono::milliseconds(200));
-      continue;
-    }
-    // query a snapshot of the oldest probes WITHOUT the lock (hipEventQuery takes the runtime's
-    // own locks; holding g_mu here stalled every sync's enqueue behind the scan)
-    batch.clear();
-    for (const auto& p : g_pending) {
-      batch.push_back({p.seq, p.ev, p.handle, p.deadline, hipSuccess});
-      if (batch.size() >= 64) break;
-    }
-    lk.unlock();
-    for (auto& b : batch) b.q = hipEventQuery(b.ev);
-    const auto now = Clock::now();
-    lk.lock();
-    follow_ups.clear();
-    for (const auto& b : batch) {
-      auto it = g_pending.begin();
-      while (it != g_pending.end() && it->seq != b.seq) ++it;
-      if (it == g_pending.end()) continue;  // retired meanwhile (destroy / abort)
-      Comm& c = *g_comms[b.handle];
-      if (b.q == hipSuccess) {
-        g_event_pool.push_back(it->ev);
-        g_pending.erase(it);
-        --c.probes;
-        if (c.state.load() == kOk && c.probes == 0 && c.untracked > 0 && c.has_last) {
-          // collectives enqueued behind the retired probe: probe them now
-          c.untracked = 0;
-          ++c.probes;
-          follow_ups.emplace_back(b.handle, c.last_stream);
-        }
-        continue;
-      }
-      if (c.state.load() == kOk) {
-        if (b.q != hipErrorNotReady) {
-          mark_failed_locked(b.handle, std::string("completion query failed: ") + hipGetErrorString(b.q), false);
-        } else if (now > b.deadline) {
-          mark_failed_locked(b.handle,
-                             "a collective did not complete within " + std::to_string(c.timeout_ms) + " ms", false);
-        }
-      }
-    }
-    if (!follow_ups.empty()) {
-      lk.unlock();
-      for (const auto& fu : follow_ups) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        int dev = 0;
-        {
-          std::lock_guard<std::mutex> lock(g_mu);
-          dev = g_comms[fu.first]->device;
-        }
-        (void)hipSetDevice(dev);
-        // never insert into a stream that is being captured into a graph
-        const bool capturing = hipStreamIsCapturing(fu.second, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
-        const bool ok = !capturing && record_probe(fu.first, fu.second) != 0;  // a failed record undoes its count
-        if (!ok) {
-          std::lock_guard<std::mutex> lock(g_mu);
-          Comm& c = *g_comms[fu.first];
-          if (capturing) --c.probes;
-          ++c.untracked;  // probed at the next sync of this communicator
-        }
-      }
-      lk.lock();
-    }
-    if (now - last_async_poll > std::chrono::milliseconds(10)) {
-      last_async_poll = now;
-      for (const auto& p : g_pending) {
-        Comm& c = *g_comms[p.handle];
-        if (c.state.load() != kOk) continue;
-        ncclResult_t e = ncclSuccess;
-        if (api().async_error(c.comm, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress)
-          mark_failed_locked(p.handle, std::string("async error: ") + api().error_string(e), false);
-      }
-    }
-    g_cv.wait_for(lk, std::chrono::microseconds(500));
-  }
-}
+// The bookkeeping (communicator states, probe events, the watchdog thread, aborts) lives in
+// tea_watchdog.h, driven here by HIP events and RCCL calls; the same template runs under
+// ThreadSanitizer with a fake backend (csrc/tests/watchdog_tsan.cpp).
 
 // TORCHEVAL_AMD_RCCL_WATCHDOG=0: no completion events (no deadlines; A/B of the tracking cost)
 bool watchdog_enabled() {
@@ -361,28 +111,63 @@ bool watchdog_enabled() {
   return !(e && std::strcmp(e, "0") == 0);
 }
 
-// completion tracking of a collective just enqueued for `handle` on `stream` (caller does NOT
-// hold g_mu): a probe event when none is in flight, else counted for the watchdog's follow-up
-// probe.  `force`: always record (a host waiter needs a probe behind everything it enqueued:
-// the watchdog's follow-up for counted collectives may not be recorded yet).  Returns the
-// recorded probe's sequence number (0 = none recorded).
-uint64_t track(int64_t handle, hipStream_t stream, bool force = false) {
-  if (!watchdog_enabled() && !force) return 0;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    Comm& c = comm_ref(handle);
-    c.last_stream = stream;
-    c.has_last = true;
-    if (c.probes > 0 && !force) {
-      ++c.untracked;
-      return 0;
-    }
-    ++c.probes;
-    if (force) c.untracked = 0;  // the forced probe covers everything before it on the stream
+struct HipBackend {
+  using Event = hipEvent_t;
+  using Stream = hipStream_t;
+  using Comm = ncclComm_t;
+  Event create_event() {
+    hipEvent_t ev = nullptr;
+    return hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess ? ev : nullptr;
   }
-  const uint64_t seq = record_probe(handle, stream);
-  TORCH_CHECK(seq != 0, "rccl_direct: hipEventRecord failed");
-  return seq;
+  bool record(Event ev, Stream s) { return hipEventRecord(ev, s) == hipSuccess; }
+  int query(Event ev) {
+    const hipError_t q = hipEventQuery(ev);
+    return q == hipSuccess ? 0 : q == hipErrorNotReady ? 1 : 2;
+  }
+  void destroy_event(Event ev) { (void)hipEventDestroy(ev); }
+  bool capturing(Stream s) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+  }
+  void set_device(int d) { (void)hipSetDevice(d); }
+  void comm_abort(Comm c) { (void)api().comm_abort(c); }
+  bool async_error(Comm c, std::string* why) {
+    ncclResult_t e = ncclSuccess;
+    if (api().async_error(c, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress) {
+      *why = api().error_string(e);
+      return true;
+    }
+    return false;
+  }
+  bool tracking_enabled() { return watchdog_enabled(); }
+  bool teardown_on_failure() {
+    // c10d's default (TORCH_NCCL_ASYNC_ERROR_HANDLING): a collective that failed behind the
+    // program's back leaves every later result suspect, so the process goes down loudly
+    const char* e = std::getenv("TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING");
+    return !(e && std::strcmp(e, "0") == 0);
+  }
+  void teardown(const std::string& msg) {
+    std::fprintf(stderr, "%s\n", msg.c_str());
+    std::fflush(stderr);
+    std::abort();
+  }
+  void fail(const std::string& msg) { throw std::runtime_error(msg); }  // raises to the caller
+};
+
+// process-lifetime, never destroyed: a watchdog still running when static destructors start (a
+// program that skipped Python's atexit) must not find its state gone
+tea_wd::Watchdog<HipBackend>& wd() {
+  static HipBackend* b = new HipBackend;
+  static tea_wd::Watchdog<HipBackend>* w = new tea_wd::Watchdog<HipBackend>(*b);
+  return *w;
+}
+
+ncclComm_t usable_comm(int64_t handle) { return wd().usable(handle); }
+
+uint64_t track(int64_t handle, hipStream_t stream, bool force = false) { return wd().track(handle, stream, force); }
+
+void check(ncclResult_t rc, const char* what) {
+  TORCH_CHECK(rc == ncclSuccess, "rccl_direct: ", what, " failed: ", api().error_string(rc));
 }
 
 ncclDataType_t dtype_of(const at::Tensor& t) {
@@ -435,98 +220,37 @@ int64_t rccl_comm_init(const at::Tensor& id_bytes, int64_t nranks, int64_t rank,
   const ncclResult_t rc = api().comm_init_rank(&comm, static_cast<int>(nranks), id, static_cast<int>(rank));
   (void)hipSetDevice(prev);
   check(rc, "ncclCommInitRank");
-  auto c = std::make_unique<Comm>();
-  c->comm = comm;
-  c->device = static_cast<int>(device);
-  c->timeout_ms = timeout_ms;
-  std::lock_guard<std::mutex> lock(g_mu);
-  g_comms.push_back(std::move(c));
-  return static_cast<int64_t>(g_comms.size()) - 1;
+  return wd().add(comm, static_cast<int>(device), timeout_ms);
 }
 
 void rccl_set_timeout(int64_t handle, int64_t timeout_ms) {
   TORCH_CHECK(timeout_ms > 0, "rccl_direct: timeout must be positive");
-  std::lock_guard<std::mutex> lock(g_mu);
-  comm_ref(handle).timeout_ms = timeout_ms;
+  wd().set_timeout(handle, timeout_ms);
 }
 
 // 0 ok, 1 failed (abort pending), 2 aborted, 3 destroyed; -1 unknown handle
-int64_t rccl_comm_state(int64_t handle) {
-  std::lock_guard<std::mutex> lock(g_mu);
-  if (handle < 0 || handle >= static_cast<int64_t>(g_comms.size()) || !g_comms[handle]) return -1;
-  return g_comms[handle]->state.load();
-}
+int64_t rccl_comm_state(int64_t handle) { return wd().state(handle); }
 
-std::string rccl_comm_reason(int64_t handle) {
-  std::lock_guard<std::mutex> lock(g_mu);
-  return comm_ref(handle).reason;
-}
+std::string rccl_comm_reason(int64_t handle) { return wd().reason(handle); }
+
+// Abort a communicator this rank still considers healthy because a PEER's failed (the group's
+// health vote, parallel/rccl_direct.py agree): marked failed as observed (no teardown) and
+// aborted by the watchdog thread like any failure; rccl_wait_aborted waits for it.
+void rccl_comm_abort(int64_t handle) { wd().mark_failed(handle, "aborted: another rank's communicator failed", true); }
 
 // wait (bounded) until the background abort of a failed communicator has finished
-bool rccl_wait_aborted(int64_t handle, int64_t timeout_ms) {
-  std::unique_lock<std::mutex> lk(g_mu);
-  Comm& c = comm_ref(handle);
-  return g_cv.wait_for(lk, std::chrono::milliseconds(timeout_ms), [&] { return c.state.load() >= kAborted; });
-}
+bool rccl_wait_aborted(int64_t handle, int64_t timeout_ms) { return wd().wait_aborted(handle, timeout_ms); }
 
 // Destroy a healthy communicator after its pending work has drained (bounded); a communicator
 // whose work does not drain in time is aborted instead.
 void rccl_comm_destroy(int64_t handle) {
-  ncclComm_t comm;
-  int device;
-  hipStream_t s_last = nullptr;
-  bool has_last = false;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    if (handle >= 0 && handle < static_cast<int64_t>(g_comms.size()) && g_comms[handle] &&
-        g_comms[handle]->state.load() == kOk) {
-      s_last = g_comms[handle]->last_stream;
-      has_last = g_comms[handle]->has_last;
-    }
-  }
-  // a probe behind every collective enqueued so far, tracked or counted (a watchdog follow-up
-  // for counted ones may not be recorded yet, so never rely on it here)
-  if (has_last) track(handle, s_last, true);
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    if (handle < 0 || handle >= static_cast<int64_t>(g_comms.size()) || !g_comms[handle]) return;
-    Comm& c = *g_comms[handle];
-    if (c.state.load() != kOk) return;  // failed / aborted / destroyed: nothing left to free here
-    comm = c.comm;
-    device = c.device;
-  }
-  const auto deadline = Clock::now() + std::chrono::seconds(30);
-  for (;;) {
-    bool busy = false;
-    {
-      std::lock_guard<std::mutex> lock(g_mu);
-      for (const auto& p : g_pending)
-        if (p.handle == handle && hipEventQuery(p.ev) == hipErrorNotReady) busy = true;
-    }
-    if (!busy) break;
-    if (Clock::now() > deadline) {
-      std::lock_guard<std::mutex> lock(g_mu);
-      mark_failed_locked(handle, "work still pending at destroy", true);
-      return;
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(200));
-  }
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    g_comms[handle]->state.store(kDestroyed);
-    for (auto it = g_pending.begin(); it != g_pending.end();) {
-      if (it->handle == handle) {
-        g_event_pool.push_back(it->ev);
-        it = g_pending.erase(it);
-      } else {
-        ++it;
-      }
-    }
-  }
+  if (!wd().valid(handle)) return;
+  if (!wd().drain_for_destroy(handle, std::chrono::seconds(30))) return;  // failed / aborted / pending
+  const auto cd = wd().comm_and_device(handle);
   int prev = 0;
   (void)hipGetDevice(&prev);
-  (void)hipSetDevice(device);
-  const ncclResult_t rc = api().comm_destroy(comm);
+  (void)hipSetDevice(cd.second);
+  const ncclResult_t rc = api().comm_destroy(cd.first);
   (void)hipSetDevice(prev);
   check(rc, "ncclCommDestroy");
 }
@@ -534,61 +258,11 @@ void rccl_comm_destroy(int64_t handle) {
 // Block the host until the newest tracked collective of `handle` completes, at most
 // timeout_ms.  false = deadline passed: the communicator is marked failed (observed, so no
 // teardown) and aborted in the background.
-bool rccl_wait(int64_t handle, int64_t timeout_ms) {
-  hipStream_t s_last = nullptr;
-  bool has_last = false;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    Comm& c = comm_ref(handle);
-    TORCH_CHECK(c.state.load() == kOk, "rccl_direct: communicator ", handle, " is unusable (", c.reason, ")");
-    s_last = c.last_stream;
-    has_last = c.has_last;
-  }
-  if (!has_last) return true;  // nothing was ever enqueued
-  // our own probe behind the newest collective: "the newest pending entry" is not enough - a
-  // counted collective's follow-up probe may still be on its way from the watchdog (that race
-  // let a held collective pass as complete)
-  const uint64_t seq = track(handle, s_last, true);
-  const auto deadline = Clock::now() + std::chrono::milliseconds(timeout_ms);
-  for (;;) {
-    {
-      std::lock_guard<std::mutex> lock(g_mu);
-      // still pending? (the watchdog retires completed entries; their events are reused)
-      hipEvent_t ev = nullptr;
-      for (const auto& p : g_pending)
-        if (p.seq == seq) ev = p.ev;
-      if (!ev) return g_comms[handle]->state.load() == kOk;
-      const hipError_t q = hipEventQuery(ev);
-      if (q == hipSuccess) return true;
-      if (q != hipErrorNotReady || Clock::now() > deadline) {
-        mark_failed_locked(handle,
-                           q != hipErrorNotReady ? std::string("completion query failed: ") + hipGetErrorString(q)
-                                                 : "a collective did not complete within " +
-                                                       std::to_string(timeout_ms) + " ms",
-                           true);
-        return false;
-      }
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(20));
-  }
-}
+bool rccl_wait(int64_t handle, int64_t timeout_ms) { return wd().wait(handle, timeout_ms); }
 
 // stop the watchdog (after draining the abort queue); called from Python's atexit hook so the
 // thread never outlives the HIP runtime
-void rccl_shutdown() {
-  std::thread* t = nullptr;
-  {
-    std::lock_guard<std::mutex> lock(g_mu);
-    t = g_watchdog;
-    g_watchdog = nullptr;
-    g_stop = true;
-    g_cv.notify_all();
-  }
-  if (t) {
-    t->join();
-    delete t;
-  }
-}
+void rccl_shutdown() { wd().shutdown(); }
 
 // dst [nranks * src.numel()] <- every rank's src, on the current stream of src's device
 void rccl_all_gather(int64_t handle, const at::Tensor& src, at::Tensor dst) {
@@ -648,7 +322,10 @@ struct Plan {
   int64_t src_end = 0, dst_end_per_rank = 0;
   std::vector<ViewSpec> views;
 };
+std::mutex& g_mu = *new std::mutex;  // the plan tables
 std::deque<Plan>& g_plans = *new std::deque<Plan>;  // under g_mu; immutable, stable addresses
+std::map<int64_t, std::vector<std::vector<int64_t>>>& g_plan_ops =
+    *new std::map<int64_t, std::vector<std::vector<int64_t>>>;  // under g_mu: each plan's spec
 
 // codes of torcheval_amd.parallel.state_buffer._DT_CODE
 bool nccl_dtype(int64_t code, ncclDataType_t* dt, int64_t* es) {
@@ -665,9 +342,61 @@ bool nccl_dtype(int64_t code, ncclDataType_t* dt, int64_t* es) {
   }
 }
 
-// ops: [kind, src_off, dst_off, count, dtype_code, op_code] each; returns a plan id
-int64_t rccl_plan_create(const std::vector<std::vector<int64_t>>& ops) {
+// Plans are immutable and communicator-agnostic, so identical specs share one id (interned by
+// ops + views): a metric rebuilt per evaluation epoch (load_state_dict / to() / a new
+// instance) finds its layout's plan again instead of growing the table without bound.
+std::map<std::vector<int64_t>, int64_t>& g_plan_ids = *new std::map<std::vector<int64_t>, int64_t>;  // under g_mu
+
+std::vector<int64_t> plan_key(const std::vector<std::vector<int64_t>>& ops, const std::vector<std::vector<int64_t>>& views) {
+  std::vector<int64_t> k;
+  for (const auto& o : ops) {
+    k.push_back(static_cast<int64_t>(o.size()));
+    k.insert(k.end(), o.begin(), o.end());
+  }
+  k.push_back(-1);  // ops / views separator
+  for (const auto& v : views) {
+    k.push_back(static_cast<int64_t>(v.size()));
+    k.insert(k.end(), v.begin(), v.end());
+  }
+  return k;
+}
+
+at::ScalarType scalar_of_code(int64_t code) {
+  switch (code) {
+    case 0: return at::kFloat;
+    case 1: return at::kHalf;
+    case 2: return at::kBFloat16;
+    case 3: return at::kDouble;
+    case 4: return at::kLong;
+    case 5: return at::kInt;
+    case 6: return at::kByte;
+    case 7: return at::kBool;
+    case 8: return at::kChar;
+    case 9: return at::kShort;
+    default: TORCH_CHECK(false, "rccl_plan_set_views: bad dtype code ", code);
+  }
+  return at::kByte;
+}
+
+std::vector<ViewSpec> parse_views(const std::vector<std::vector<int64_t>>& views) {
+  std::vector<ViewSpec> vs;
+  for (const auto& v : views) {
+    TORCH_CHECK(v.size() >= 2 && v[1] >= 0, "rccl_plan views: each view is [dtype, elem_off, *shape]");
+    vs.push_back({scalar_of_code(v[0]), v[1], std::vector<int64_t>(v.begin() + 2, v.end())});
+  }
+  return vs;
+}
+
+// ops: [kind, src_off, dst_off, count, dtype_code, op_code] each; views: [dtype_code, elem_off,
+// *shape] per synced state (may be empty: rccl_plan_set_views once, later); returns a plan id
+int64_t rccl_plan_create(const std::vector<std::vector<int64_t>>& ops, const std::vector<std::vector<int64_t>>& views) {
   TORCH_CHECK(!ops.empty(), "rccl_plan_create: empty plan");
+  const std::vector<int64_t> key = plan_key(ops, views);
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    auto it = g_plan_ids.find(key);
+    if (it != g_plan_ids.end()) return it->second;
+  }
   Plan p;
   for (const auto& o : ops) {
     TORCH_CHECK(o.size() == 6, "rccl_plan_create: each op is [kind, src_off, dst_off, count, dtype, op]");
@@ -692,9 +421,15 @@ int64_t rccl_plan_create(const std::vector<std::vector<int64_t>>& ops) {
     p.src_end = std::max(p.src_end, q.src_off + q.count * q.esize);
     p.ops.push_back(q);
   }
+  p.views = parse_views(views);
   std::lock_guard<std::mutex> lock(g_mu);
+  auto it = g_plan_ids.find(key);  // a concurrent caller interned it meanwhile
+  if (it != g_plan_ids.end()) return it->second;
   g_plans.push_back(std::move(p));
-  return static_cast<int64_t>(g_plans.size()) - 1;
+  const int64_t id = static_cast<int64_t>(g_plans.size()) - 1;
+  g_plan_ids.emplace(key, id);
+  g_plan_ops.emplace(id, ops);
+  return id;
 }
 
 void rccl_group_start() { check(api().group_start(), "ncclGroupStart"); }
@@ -748,33 +483,29 @@ void rccl_plan_run(int64_t handle, int64_t plan, const at::Tensor& src, const at
   if (!grouped) track(handle, s);
 }
 
-at::ScalarType scalar_of_code(int64_t code) {
-  switch (code) {
-    case 0: return at::kFloat;
-    case 1: return at::kHalf;
-    case 2: return at::kBFloat16;
-    case 3: return at::kDouble;
-    case 4: return at::kLong;
-    case 5: return at::kInt;
-    case 6: return at::kByte;
-    case 7: return at::kBool;
-    case 8: return at::kChar;
-    case 9: return at::kShort;
-    default: TORCH_CHECK(false, "rccl_plan_set_views: bad dtype code ", code);
-  }
-  return at::kByte;
-}
 
-// views: [dtype_code, elem_off, *shape] per state, in the order the caller assigns them
+// views: [dtype_code, elem_off, *shape] per state, in the order the caller assigns them.  Plans
+// are shared (interned): only a plan created without views may receive them (once); setting the
+// views it already has is a no-op.
 void rccl_plan_set_views(int64_t plan, const std::vector<std::vector<int64_t>>& views) {
-  std::vector<ViewSpec> vs;
-  for (const auto& v : views) {
-    TORCH_CHECK(v.size() >= 2 && v[1] >= 0, "rccl_plan_set_views: each view is [dtype, elem_off, *shape]");
-    vs.push_back({scalar_of_code(v[0]), v[1], std::vector<int64_t>(v.begin() + 2, v.end())});
-  }
+  std::vector<ViewSpec> vs = parse_views(views);
   std::lock_guard<std::mutex> lock(g_mu);
   TORCH_CHECK(plan >= 0 && plan < static_cast<int64_t>(g_plans.size()), "rccl_plan_set_views: invalid plan ", plan);
-  g_plans[plan].views = std::move(vs);
+  Plan& p = g_plans[plan];
+  auto same = [&]() {
+    if (p.views.size() != vs.size()) return false;
+    for (size_t i = 0; i < vs.size(); ++i)
+      if (p.views[i].dtype != vs[i].dtype || p.views[i].elem_off != vs[i].elem_off || p.views[i].shape != vs[i].shape)
+        return false;
+    return true;
+  };
+  if (same()) return;
+  TORCH_CHECK(p.views.empty(), "rccl_plan_set_views: plan ", plan, " already has other views (plans are immutable)");
+  p.views = std::move(vs);
+  // re-key the interned entry: (ops, no views) -> (ops, these views)
+  const auto& ops = g_plan_ops.at(plan);
+  g_plan_ids.erase(plan_key(ops, {}));
+  g_plan_ids.emplace(plan_key(ops, views), plan);
 }
 
 // The whole direct sync of one metric in one call: a fresh result buffer like `src`, the
@@ -862,6 +593,8 @@ void tea_register_rccl(pybind11::module_& m) {
   m.def("rccl_comm_reason", &rccl_comm_reason, "why a communicator failed", py::arg("handle"));
   m.def("rccl_wait_aborted", &rccl_wait_aborted, "wait for the background abort of a failed communicator",
         py::arg("handle"), py::arg("timeout_ms"), py::call_guard<py::gil_scoped_release>());
+  m.def("rccl_comm_abort", &rccl_comm_abort, "abort a healthy communicator whose peer failed (no teardown)",
+        py::arg("handle"));
   m.def("rccl_comm_destroy", &rccl_comm_destroy, "ncclCommDestroy of a handle (after its work drains)",
         py::arg("handle"), py::call_guard<py::gil_scoped_release>());
   m.def("rccl_wait", &rccl_wait, "host wait for the newest collective of a handle; false = deadline passed",
@@ -872,8 +605,9 @@ void tea_register_rccl(pybind11::module_& m) {
   m.def("rccl_all_reduce", &rccl_all_reduce,
         "ncclAllReduce on the current stream (op 0/1/2 = sum/max/min), in place or into out", py::arg("handle"),
         py::arg("t"), py::arg("op"), py::arg("out") = py::none());
-  m.def("rccl_plan_create", &rccl_plan_create, "register a sync plan: [[kind, src_off, dst_off, count, dtype, op]]",
-        py::arg("ops"));
+  m.def("rccl_plan_create", &rccl_plan_create,
+        "register (or find) a sync plan: [[kind, src_off, dst_off, count, dtype, op]] + [[dtype, elem_off, *shape]]",
+        py::arg("ops"), py::arg("views") = std::vector<std::vector<int64_t>>{});
   m.def("rccl_plan_run", &rccl_plan_run, "run a sync plan as one RCCL group (src -> dst, out of place)",
         py::arg("handle"), py::arg("plan"), py::arg("src"), py::arg("dst"), py::arg("nranks"),
         py::arg("grouped") = false);

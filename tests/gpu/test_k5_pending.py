@@ -98,3 +98,41 @@ def test_weighted_and_variable_batches():
         den += float(w.double().sum())
     torch.testing.assert_close(m.sum_squared_error.cpu().double(), num, rtol=1e-6, atol=1e-4)
     assert float(m.sum_weight) == pytest.approx(den, rel=1e-6)
+
+
+def test_sum_mean_deferred_long_rows():
+    from torcheval_amd.metrics import Mean, Sum
+
+    g = torch.Generator().manual_seed(9)
+    s, m = Sum(device=DEV), Mean(device=DEV)
+    ref_s, ref_w = 0.0, 0.0
+    batches = [(torch.randn(8192, 1001, generator=g), 0.5), (torch.randn(7, generator=g), 2.0),
+               (torch.randn(100_003, generator=g), 1.0), (torch.randn(3000, 40, generator=g), "t")]
+    for x, w in batches:
+        if w == "t":
+            wt = torch.rand(x.shape, generator=g)
+            s.update(x.to(DEV), weight=wt.to(DEV))
+            m.update(x.to(DEV), weight=wt.to(DEV))
+            ref_s += float((x.double() * wt.double()).sum())
+            ref_w += float(wt.double().sum())
+        else:
+            s.update(x.to(DEV), weight=w)
+            m.update(x.to(DEV), weight=w)
+            ref_s += float(x.double().sum()) * w
+            ref_w += w * x.numel()
+    assert s.__dict__["_pend_dirty"] and m.__dict__["_pend_dirty"]
+    assert float(s.compute()) == pytest.approx(ref_s, rel=1e-10, abs=1e-6)
+    assert float(m.compute()) == pytest.approx(ref_s / ref_w, rel=1e-10, abs=1e-10)
+    # reset drops pending sums; merge / state_dict / copies fold them
+    x = torch.randn(50_000, generator=g)
+    s.update(x.to(DEV))
+    c = copy.deepcopy(s)
+    assert float(c.weighted_sum) == pytest.approx(ref_s + float(x.double().sum()), rel=1e-10, abs=1e-6)
+    s.reset()
+    assert float(s.compute()) == 0.0
+    s.update(x.to(DEV))
+    s2 = Sum(device=DEV)
+    s2.update(x.to(DEV))
+    s.merge_state([s2])
+    assert float(s.weighted_sum) == pytest.approx(2 * float(x.double().sum()), rel=1e-10, abs=1e-6)
+    assert float(s.state_dict()["weighted_sum"]) == pytest.approx(2 * float(x.double().sum()), rel=1e-10, abs=1e-6)

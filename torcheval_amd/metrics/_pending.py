@@ -20,13 +20,24 @@ folded state is at least as accurate as the reference's per-update float32 ``+=`
 (mean_squared_error.py:82-97, r2_score.py:97-106).
 """
 
-from typing import Dict, Optional
+from typing import Dict, NamedTuple, Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops import native
+from torcheval_amd.ops import compiling, native
 
 PEND_SLOTS = 64  # csrc/include/tea_kernels.h kMomentsPendSlots
+ROWSUMS_PEND_STATS = 7  # kRowPendStats
+ROWSUMS_PEND_BLOCKS = 2048  # kRowPendBlocks
+ROWSUMS_PEND_MIN = 32768  # rowsums.hip kSingle: shorter rows are one block, folded in-launch
+
+
+class RowSumsSpec(NamedTuple):
+    """The K5b outputs a deferred update accumulates: state names, packed codes, rows."""
+
+    names: Tuple[str, ...]
+    codes: Tuple[int, ...]
+    rows: int
 
 
 def _prop(name: str) -> property:
@@ -68,8 +79,12 @@ class PendingMixin:
         """The state tensor without folding (for the update that adds to the pending sums)."""
         return self.__dict__["_pv_" + name]
 
-    def _pend_buffer(self, numel: int, device: torch.device) -> torch.Tensor:
+    def _pend_buffer(self, numel: int, device: torch.device, spec=None) -> torch.Tensor:
+        """The pending buffer for an update that will add ``spec``'s sums (pending sums of a
+        different spec are folded first)."""
         d = self.__dict__
+        if d.get("_pend_dirty") and spec is not None and d.get("_pend_spec") != spec:
+            self._fold_pending()
         buf: Optional[torch.Tensor] = d.get("_pend")
         if buf is None or buf.numel() < numel or buf.device != device or d.get("_pend_id") != id(self):
             if d.get("_pend_dirty"):
@@ -90,10 +105,27 @@ class PendingMixin:
         d = self.__dict__
         d["_pend_dirty"] = False  # first: the state reads below must not recurse
         spec = d.get("_pend_spec") or {}
-        st = {k: d["_pv_" + n] for k, n in spec.items()}
-        native().column_moments_fold(d["_pend"], d.get("_pend_r", 0), st.get("sse"), st.get("st"), st.get("stt"),
-                                     st.get("sx"), st.get("sw"))
+        if isinstance(spec, RowSumsSpec):  # K5b: outputs and codes of the deferred updates
+            native().row_sums_fold(d["_pend"], d.get("_pend_r", 0), [d["_pv_" + n] for n in spec.names],
+                                   list(spec.codes), spec.rows)
+        else:  # K5 column moments: {statistic: state name}
+            st = {k: d["_pv_" + n] for k, n in spec.items()}
+            native().column_moments_fold(d["_pend"], d.get("_pend_r", 0), st.get("sse"), st.get("st"),
+                                         st.get("stt"), st.get("sx"), st.get("sw"))
         d["_pend_r"] = 0
+
+    def _rowsums_deferred(self, x: torch.Tensor, w, w_scalar: float, spec: "RowSumsSpec") -> bool:
+        """K5b deferred update of ``spec``'s states from a long ROCm batch viewed as one row
+        (Sum / Mean): True when the launch ran (the states now have pending sums)."""
+        if not x.is_cuda or x.numel() <= ROWSUMS_PEND_MIN or compiling():
+            return False
+        pend = self._pend_buffer(spec.rows * ROWSUMS_PEND_STATS * ROWSUMS_PEND_BLOCKS, x.device, spec)
+        used = native().row_sums_pend(x, None, w, w_scalar, [self.__dict__["_pv_" + n] for n in spec.names],
+                                      list(spec.codes), spec.rows, pend)
+        if not used:
+            return False
+        self._pend_mark(used, spec)
+        return True
 
     def _drop_pending(self) -> None:
         d = self.__dict__

@@ -5,15 +5,19 @@ from typing import Iterable, Optional, Union
 import torch
 
 from torcheval_amd.metrics.functional.aggregation import _sum_update
+from torcheval_amd.metrics._pending import PendingMixin, RowSumsSpec, pending_states
 from torcheval_amd.metrics.metric import Metric
 from torcheval_amd.ops import rowsums as _rs
 
 __all__ = ["Sum"]
 
 _CODES = [_rs.code(_rs.WX, _rs.ADD)]
+# long ROCm batches add to device pending sums, folded into the state when it is read
+_SPEC = RowSumsSpec(("weighted_sum",), tuple(_CODES), 1)
 
 
-class Sum(Metric[torch.Tensor]):
+@pending_states("weighted_sum")
+class Sum(PendingMixin, Metric[torch.Tensor]):
     """Weighted sum of all inputs (float64 accumulator)."""
 
     def __init__(self, *, device: Optional[torch.device] = None) -> None:
@@ -21,9 +25,12 @@ class Sum(Metric[torch.Tensor]):
         self._add_state("weighted_sum", torch.tensor(0.0, device=self.device, dtype=torch.float64), merge="sum")
 
     def update(self, input: torch.Tensor, *, weight: Union[float, int, torch.Tensor] = 1.0) -> "Sum":
-        if _rs.fast_ok(input, weight, self.weighted_sum):  # K5b, one launch (host twin on CPU)
+        ws = self.__dict__["_pv_weighted_sum"]  # no fold: an update only adds
+        if _rs.fast_ok(input, weight, ws):  # K5b, one launch (host twin on CPU)
             tw = isinstance(weight, torch.Tensor)
-            _rs.update(input, None, weight if tw else None, 1.0 if tw else float(weight), [self.weighted_sum], _CODES)
+            wt, wsc = (weight, 1.0) if tw else (None, float(weight))
+            if not self._rowsums_deferred(input, wt, wsc, _SPEC):
+                _rs.update(input, None, wt, wsc, [ws], _CODES)
             return self
         return self._update_aten(input, weight)
 

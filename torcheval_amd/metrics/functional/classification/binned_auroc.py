@@ -13,7 +13,9 @@ from typing import List, Optional, Tuple, Union
 import torch
 
 from torcheval_amd.metrics.functional.tensor_utils import _threshold_check, _create_threshold_tensor
+from torcheval_amd.ops import native, use_native
 from torcheval_amd.ops.binned import binned_counts, binned_finalize, binned_finalize_supported
+from torcheval_amd.ops.hostread import read_int
 
 DEFAULT_NUM_THRESHOLD = 200
 
@@ -115,6 +117,23 @@ def multiclass_binned_auroc(
     return _multiclass_binned_auroc_compute(input, target, num_classes, threshold, average, one_vs_rest)
 
 
+def _native_per_sample(input: torch.Tensor, target: torch.Tensor, num_classes: int, threshold: torch.Tensor) -> bool:
+    return (
+        use_native(input)
+        and input.dim() == 2
+        and input.dtype == torch.float32
+        and input.shape[1] == num_classes
+        and input.shape[1] >= 1
+        and input.stride(1) == 1
+        and input.shape[0] > 0
+        and threshold.dtype == torch.float32
+        and threshold.numel() >= 1
+        and target.is_cuda
+        and target.dim() == 1
+        and not target.dtype.is_floating_point
+    )
+
+
 def _per_sample_binned_auroc(input: torch.Tensor, target: torch.Tensor, num_classes: int,
                              threshold: torch.Tensor) -> torch.Tensor:
     """float32 [N]: the reference's per-sample rows, without its [T, N, C] boolean tensor.
@@ -123,6 +142,16 @@ def _per_sample_binned_auroc(input: torch.Tensor, target: torch.Tensor, num_clas
     classes at or above thr_t is the suffix sum of a [T + 1] histogram of its bins; the true
     class contributes tp_t = [t < b_true] and the rest fp_t.  The trapezoid runs over the
     descending-threshold curve with a leading 0, as ``rot90`` + ``pad`` build it there."""
+    if _native_per_sample(input, target, num_classes, threshold):
+        # K4b (csrc/kernels/binned_auroc.hip): one streaming pass, one binary search per
+        # sample; the label range goes through a device flag read once (no min / max syncs)
+        out = torch.empty(input.shape[0], dtype=torch.float32, device=input.device)
+        err = torch.zeros(1, dtype=torch.int32, device=input.device)
+        t = target if target.dtype in (torch.int64, torch.int32) else target.long()
+        native().sample_binned_auroc(input, t, threshold.to(input.device).contiguous(), out, err)
+        if read_int(err):
+            raise RuntimeError("Class values must be smaller than num_classes.")  # F.one_hot's check
+        return out
     if target.numel() and (int(target.min()) < 0 or int(target.max()) >= num_classes):
         raise RuntimeError("Class values must be smaller than num_classes.")  # F.one_hot's check
     n, T = input.shape[0], threshold.numel()

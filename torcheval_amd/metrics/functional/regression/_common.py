@@ -76,7 +76,7 @@ def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w
             ns = 1 if need == 1 else 3 if need == 7 else 4  # tea_kernels.h moments_ns
             from torcheval_amd.metrics._pending import PEND_SLOTS
 
-            pend = metric._pend_buffer(PEND_SLOTS * (ns * d + 1), input.device)
+            pend = metric._pend_buffer(PEND_SLOTS * (ns * d + 1), input.device, spec)
             slots = native().column_moments_pend(input, target, w, kw["sse"], kw["st"], kw["stt"], None, kw["sw"], pend)
             if slots:
                 metric._pend_mark(slots, spec)

@@ -23,9 +23,22 @@ timeout):
   sync on the group builds a fresh one.
 
 Bootstrapping is collective: every rank of the group reaches ``comm_for`` at the same sync
-(the engine's plans are built at the same call on every rank).  ``TORCHEVAL_AMD_DIRECT_RCCL=0``
-keeps every collective on torch.distributed (e.g. when a program interleaves its own
-collectives on other streams with metric syncs in a rank-dependent order).
+(the engine's plans are built at the same call on every rank).
+
+Policy (``TORCHEVAL_AMD_DIRECT_RCCL``): ``auto`` (the default) uses the direct communicators
+only for 1-rank groups (the forced multi-rank engine of the tests and benchmarks), because no
+multi-GPU run has validated the multi-rank bootstrap yet; multi-rank groups keep
+torch.distributed's collectives and the rank-ordered gather + ``seg_reduce`` path.  ``1`` opts
+every group in, ``0`` keeps every collective on torch.distributed.
+
+Agreement: with ``TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING=0`` (no teardown on a failure) a
+communicator can fail on one rank only (its watchdog fired, its peers' collectives completed).
+Rebuilding on that rank's own view would pair its ``broadcast`` of a new id with its peers'
+next direct collective and hang, so in that mode every direct sync of a multi-rank group first
+votes on the group's health (one MIN all-reduce over torch.distributed): if any rank's
+communicator failed, EVERY rank drops it at the same sync and the group builds a fresh one (or
+falls back to torch.distributed, again by a collective vote).  With teardown on (the default)
+a failure ends the process, as c10d's does, so no rank can continue alone.
 """
 
 import atexit
@@ -42,14 +55,38 @@ GENERATION = [0]
 _ABORTING: List[int] = []  # failed handles whose background abort a new communicator waits for
 _OPS = {"sum": 0, "max": 1, "min": 2}
 _DEFAULT_TIMEOUT = timedelta(minutes=10)  # c10d's NCCL default when the group reports none
+# devices whose groups may get a direct communicator (tests/test_rccl_decisions.py adds "cpu" to
+# drive the decision logic over gloo ranks with a fake native layer)
+_DEVICE_TYPES = ("cuda",)
 
 
-def enabled() -> bool:
-    if os.environ.get("TORCHEVAL_AMD_DIRECT_RCCL", "1") == "0":
+def enabled(ws: int = 1) -> bool:
+    """Whether a group of ``ws`` ranks uses the direct communicators (see the module docstring)."""
+    mode = os.environ.get("TORCHEVAL_AMD_DIRECT_RCCL", "auto")
+    if mode == "0" or (mode != "1" and ws > 1):
         return False
     from torcheval_amd.ops import native, native_loaded
 
     return native_loaded() and bool(native().rccl_available())
+
+
+def teardown_on_failure() -> bool:
+    """c10d-style async error handling (the default): a failed communicator ends the process."""
+    return os.environ.get("TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING", "1") != "0"
+
+
+def agree(handle: Optional[int], group, ws: int, device: torch.device) -> Optional[int]:
+    """The handle to use for this sync of a multi-rank group, decided by ALL ranks together
+    when a failure can be local (no teardown): a MIN vote of every rank's communicator health.
+    A failed vote drops the communicator on every rank (``forget``) and rebuilds it collectively
+    (``comm_for``), so every rank enqueues the sync on the same path.  Returns the (possibly new)
+    handle or None (torch.distributed)."""
+    if handle is None or ws <= 1 or teardown_on_failure():
+        return handle
+    if _vote(state(handle) == 0, group, device):
+        return handle
+    forget(handle, abort=True)
+    return comm_for(group, ws, device)
 
 
 def group_timeout(group, device: torch.device) -> timedelta:
@@ -73,7 +110,7 @@ def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
 
     A communicator that failed (deadline or async error) is replaced by a fresh one here, after
     its background abort has finished."""
-    if device.type != "cuda" or not enabled():
+    if device.type not in _DEVICE_TYPES or not enabled(ws):
         return None
     from torcheval_amd.ops import native
 
@@ -102,20 +139,26 @@ def comm_for(group, ws: int, device: torch.device) -> Optional[int]:
             uid, ws, rank, device.index if device.index is not None else 0, _ms(group_timeout(group, device))))
     except RuntimeError:
         handle = None
-    if ws > 1 and handle is not None and not _self_check(handle, ws, rank, device):
-        native().rccl_comm_destroy(handle)
-        handle = None
     if ws > 1:
-        # every rank must take the same path: one failed init sends the whole group back to
-        # torch.distributed (a rank-dependent choice would pair a direct collective with a
-        # torch.distributed one and hang)
-        ok = torch.tensor([1 if handle is not None else 0], dtype=torch.int32, device=device)
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
-        if int(ok.item()) == 0 and handle is not None:
-            native().rccl_comm_destroy(handle)
+        # every rank must take the same path (a rank-dependent choice would pair a direct
+        # collective with a torch.distributed one and hang), so each step is voted on by the
+        # whole group: first every rank must hold a communicator - the self-check is itself a
+        # collective on it, which a rank without one would never join - then every rank's
+        # self-check must pass.  Any failed vote sends the whole group to torch.distributed.
+        if not _vote(handle is not None, group, device) or not _vote(_self_check(handle, ws, rank, device), group,
+                                                                    device):
+            if handle is not None:
+                native().rccl_comm_destroy(handle)
             handle = None
     _COMMS[id(group)] = (group, ws, handle)
     return handle
+
+
+def _vote(ok: bool, group, device: torch.device) -> bool:
+    """True iff ``ok`` holds on every rank of ``group`` (one MIN all-reduce)."""
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return int(t.item()) == 1
 
 
 def _self_check(handle: int, ws: int, rank: int, device: torch.device) -> bool:
@@ -143,11 +186,16 @@ def _self_check(handle: int, ws: int, rank: int, device: torch.device) -> bool:
     return ok
 
 
-def forget(handle: int) -> None:
-    """Drop a failed communicator from the cache (the next ``comm_for`` rebuilds)."""
+def forget(handle: int, abort: bool = False) -> None:
+    """Drop a communicator from the cache (the next ``comm_for`` rebuilds).  ``abort``: also
+    abort it if it is still healthy here (a peer's failed: its collectives may never complete)."""
     for k, (_, _, h) in list(_COMMS.items()):
         if h == handle:
             del _COMMS[k]
+    if abort and state(handle) == 0:
+        from torcheval_amd.ops import native
+
+        native().rccl_comm_abort(handle)
     _ABORTING.append(handle)
     GENERATION[0] += 1
 
@@ -170,12 +218,13 @@ def wait(handle: int, timeout: timedelta) -> None:
         raise TimeoutError(f"metric-state sync did not complete within {timeout} ({reason})")
 
 
-def plan_create(ops: Sequence[Sequence[int]]) -> int:
+def plan_create(ops: Sequence[Sequence[int]], views: Sequence[Sequence[int]] = ()) -> int:
     """Register a sync plan: ``[kind, src_off, dst_off, count, dtype_code, op_code]`` per operand
-    (kind 0 all-reduce of ``count`` elements, 1 all-gather of ``count`` bytes; byte offsets)."""
+    (kind 0 all-reduce of ``count`` elements, 1 all-gather of ``count`` bytes; byte offsets) and
+    its synced-state views (``plan_set_views``).  Identical specs share one plan id (interned)."""
     from torcheval_amd.ops import native
 
-    return int(native().rccl_plan_create([list(map(int, o)) for o in ops]))
+    return int(native().rccl_plan_create([list(map(int, o)) for o in ops], [list(map(int, v)) for v in views]))
 
 
 def plan_set_views(plan: int, views: Sequence[Sequence[int]]) -> None:

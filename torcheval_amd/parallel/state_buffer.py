@@ -385,10 +385,10 @@ class _Plan:
         spec = direct_plan_spec(sb, cls) if self.comm is not None else None
         if spec is not None:
             ops, self.dassign = spec
-            self.rplan = rccl_direct.plan_create(ops)
             # the synced states are built as views of the result buffer inside the same native
-            # call (rccl_plan_sync): one pybind round trip instead of a Python view per state
-            rccl_direct.plan_set_views(self.rplan, view_specs(self.dassign))
+            # call (rccl_plan_sync): one pybind round trip instead of a Python view per state;
+            # plans are interned by spec, so rebuilt buffers of one layout share one native plan
+            self.rplan = rccl_direct.plan_create(ops, view_specs(self.dassign))
             self.dnames = [(name, prop) for name, _, _, _, _, prop in self.dassign]
 
 
@@ -427,6 +427,11 @@ def _plan_for(sb: StateBuffer, group, ws: int, metric) -> _Plan:
     plan = sb.plans.get(key)
     if plan is None or plan.group is not group or (plan.comm is not None and plan.gen != rccl_direct.GENERATION[0]):
         plan = sb.plans[key] = _Plan(sb, group, ws, metric)
+    if plan.comm is not None and ws > 1 and not rccl_direct.teardown_on_failure():
+        # a failure may be local to one rank: the group votes before every direct sync, and a
+        # failed vote rebuilds (or leaves) the communicator on every rank at this same sync
+        if rccl_direct.agree(plan.comm, plan.pg, ws, sb.device) != plan.comm:
+            plan = sb.plans[key] = _Plan(sb, group, ws, metric)
     return plan
 
 
@@ -614,7 +619,8 @@ def _fast_issue(metrics, group, ws: int, side: bool) -> Optional[_FastIssue]:
     if nccl and collectives.current_sync_timeout() is None:
         from torch.distributed.distributed_c10d import _get_default_group
 
-        comm = rccl_direct.comm_for(group if group is not None else _get_default_group(), ws, dev)
+        pg = group if group is not None else _get_default_group()
+        comm = rccl_direct.agree(rccl_direct.comm_for(pg, ws, dev), pg, ws, dev)
     if side and comm is None:
         return None
     if comm is not None:
