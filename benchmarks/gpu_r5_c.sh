@@ -1,12 +1,9 @@
 #!/bin/bash
-# Round 5: K4b per-sample binned AUROC, K5 / K5b deferred mode, direct-RCCL engine tests, then
-# the K5b deferred A/B and the odd-width cliff benchmark.
+# Round 5: the whole GPU suite (K4b per-sample binned AUROC, K5 / K5b deferred mode, K1 unaligned
+# rows, direct-RCCL engine), then the K5b deferred A/B and the odd-width cliff benchmark.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread \
-  tests/gpu/test_k4b_sample_binned_auroc.py tests/gpu/test_k5_pending.py tests/gpu/test_k5b_rowsums.py \
-  tests/gpu/test_k5_v2_odd.py tests/gpu/test_rccl_direct.py tests/gpu/test_rccl_single_rank.py \
-  tests/gpu/test_sync_multirank_kernels.py tests/gpu/test_k3_k4_k6.py \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   > gpurun_out/r5_c_tests.log 2>&1 || { tail -40 gpurun_out/r5_c_tests.log; exit 1; }
 tail -1 gpurun_out/r5_c_tests.log
 timeout -k 10 120 python -u benchmarks/k5b_pend_ab.py > gpurun_out/r5_k5b_ab_vpt8.json 2>&1 || { tail -20 gpurun_out/r5_k5b_ab_vpt8.json; exit 1; }

@@ -266,4 +266,111 @@ void r2_sums(const S* x, int64_t xs0, int64_t xs1, const S* t, int64_t ts0, int6
     }
 }
 
+// FP64 column sums for the class-API regression updates: sse = sum w (t - x)^2, st = sum w t,
+// stt = sum w t^2 (null = not requested), sw = sum w (n without weights)
+template <typename S>
+void moment_sums(const S* x, int64_t xs0, int64_t xs1, const S* t, int64_t ts0, int64_t ts1, const S* w, int64_t ws0,
+                 int64_t n, int64_t d, double* sse, double* st, double* stt, double& sw) {
+  for (int64_t c = 0; c < d; ++c) {
+    if (sse) sse[c] = 0.0;
+    if (st) st[c] = 0.0;
+    if (stt) stt[c] = 0.0;
+  }
+  sw = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const double wi = w ? static_cast<double>(w[i * ws0]) : 1.0;
+    sw += wi;
+    for (int64_t c = 0; c < d; ++c) {
+      const double tv = static_cast<double>(t[i * ts0 + c * ts1]);
+      if (sse) {
+        const double e = tv - static_cast<double>(x[i * xs0 + c * xs1]);
+        sse[c] += wi * e * e;
+      }
+      if (st) st[c] += wi * tv;
+      if (stt) stt[c] += wi * tv * tv;
+    }
+  }
+}
+
+// torch.nan_to_num of a float32: NaN -> 0, +-inf -> +-FLT_MAX
+inline float nan_to_num(float v) {
+  if (std::isnan(v)) return 0.f;
+  if (std::isinf(v)) return v > 0 ? 3.4028234663852886e38f : -3.4028234663852886e38f;
+  return v;
+}
+
+// Macro / weighted class averages of float32 per-class counts [C], element-wise in float32 as the
+// reference's tensor expressions are (the final mean / weighted sum accumulates in FP64):
+//   kind 0 accuracy  (a correct, b total):      mean over total != 0 of a / b
+//   kind 1 F1        (a tp, b label, c pred):    over label | pred != 0, nan_to_num(2 p r / (p + r))
+//   kind 2 precision (a tp, b fp, c label):      over label | tp + fp != 0, nan_to_num(tp / (tp + fp))
+//   kind 3 recall    (a tp, b label, c pred):    over label | pred != 0, tp / label (NaNs -> 0)
+// avg 0 macro, 1 weighted (by label / sum(label) over all classes).  *label_zero: some class has
+// no label (the F1 warning); nan_idx: recall's NaN positions within the masked vector.
+inline float class_average(int kind, int avg, const float* a, const float* b, const float* c, int64_t C,
+                           bool* label_zero, std::vector<int64_t>* nan_idx) {
+  const float* label = kind == 2 ? c : b;
+  double lsum_d = 0.0;
+  for (int64_t i = 0; i < C; ++i) lsum_d += label[i];
+  const float lsum = static_cast<float>(lsum_d);
+  std::vector<float> vals, wts;
+  vals.reserve(C);
+  wts.reserve(C);
+  for (int64_t i = 0; i < C; ++i) {
+    float v;
+    if (kind == 0) {
+      if (b[i] == 0.f) continue;
+      v = a[i] / b[i];
+    } else if (kind == 1) {
+      if (b[i] == 0.f && label_zero) *label_zero = true;
+      if (b[i] == 0.f && c[i] == 0.f) continue;
+      const float p = a[i] / c[i], r = a[i] / b[i];
+      v = nan_to_num(2.f * p * r / (p + r));
+    } else if (kind == 2) {
+      if (c[i] == 0.f && a[i] + b[i] == 0.f) continue;
+      v = nan_to_num(a[i] / (a[i] + b[i]));
+    } else {
+      if (b[i] == 0.f && c[i] == 0.f) continue;
+      v = a[i] / b[i];
+    }
+    vals.push_back(v);
+    wts.push_back(label[i] / lsum);
+  }
+  if (kind == 3) {  // torch.nan_to_num only runs when some class is NaN
+    bool any = false;
+    for (size_t j = 0; j < vals.size(); ++j)
+      if (std::isnan(vals[j])) {
+        any = true;
+        if (nan_idx) nan_idx->push_back(static_cast<int64_t>(j));
+      }
+    if (any)
+      for (float& v : vals) v = nan_to_num(v);
+  }
+  double acc = 0.0;
+  if (avg == 0) {
+    for (float v : vals) acc += v;
+    return static_cast<float>(acc / static_cast<double>(vals.size()));  // empty: NaN, as mean([])
+  }
+  for (size_t j = 0; j < vals.size(); ++j) acc += static_cast<double>(vals[j] * wts[j]);
+  return static_cast<float>(acc);
+}
+
+// confusion matrix [C, C] (target, prediction) counts of a small batch: prediction = argmax of
+// scores [n, C] (row stride ld), a label, or (binary) score >= threshold.  False when some label is
+// outside [0, C) (the caller's checking path raises the reference's error).
+template <typename S>
+bool confusion_counts(const S* scores, int64_t ld, const Labels& pred_labels, bool binary, double threshold,
+                      const Labels& target, int64_t n, int64_t C, int64_t* cm) {
+  for (int64_t i = 0; i < n; ++i) {
+    const int64_t t = target.at(i);
+    int64_t p;
+    if (binary) p = scores[i * ld] < static_cast<S>(threshold) ? 0 : 1;  // torch.where(x < thr, 0, 1)
+    else if (scores) p = row_argmax(scores + i * ld, C);
+    else p = pred_labels.at(i);
+    if (t < 0 || t >= C || p < 0 || p >= C) return false;
+    cm[t * C + p] += 1;
+  }
+  return true;
+}
+
 }  // namespace tea_cpu

@@ -527,6 +527,162 @@ at::Tensor cpu_r2(const at::Tensor& x, const at::Tensor& t, int64_t mode, int64_
   return x.scalar_type() == at::kFloat ? r2_impl<float>(x, t, mode, k) : r2_impl<double>(x, t, mode, k);
 }
 
+// ---- class-API regression updates (small CPU batches) ----
+
+bool f32_state(const c10::optional<at::Tensor>& s, int64_t numel, int64_t dim, float** out) {
+  *out = nullptr;
+  if (!s.has_value()) return true;
+  if (s->is_cuda() || s->scalar_type() != at::kFloat || !s->is_contiguous() || s->numel() != numel || s->dim() != dim)
+    return false;
+  *out = s->data_ptr<float>();
+  return true;
+}
+
+// MeanSquaredError / R2Score.update: this batch's FP64 column sums (tea_cpu::moment_sums) rounded
+// to float32 and added into the states in place, as the reference's ``state += batch.sum(dim=0)``
+// does; sw += sum w, or += n (``count``, and without weights).  x, t: float32 [n] or [n, d];
+// the [d] states are 1-D for 2-D batches and 0-d for 1-D ones, sw is 0-d.  False (nothing
+// written) for anything else: the caller's general path runs.
+bool cpu_moments_update(const at::Tensor& x, const at::Tensor& t, const c10::optional<at::Tensor>& w,
+                        const c10::optional<at::Tensor>& sse, const c10::optional<at::Tensor>& st,
+                        const c10::optional<at::Tensor>& stt, const c10::optional<at::Tensor>& sw, bool count) {
+  if (x.is_cuda() || t.is_cuda() || x.sizes() != t.sizes() || (x.dim() != 1 && x.dim() != 2) ||
+      x.scalar_type() != at::kFloat || t.scalar_type() != at::kFloat || x.numel() == 0)
+    return false;
+  if (w.has_value() &&
+      (w->is_cuda() || w->dim() != 1 || w->size(0) != x.size(0) || w->scalar_type() != at::kFloat))
+    return false;
+  const int64_t n = x.size(0), d = x.dim() == 2 ? x.size(1) : 1, sdim = x.dim() == 2 ? 1 : 0;
+  float *psse, *pst, *pstt, *psw;
+  if (!f32_state(sse, d, sdim, &psse) || !f32_state(st, d, sdim, &pst) || !f32_state(stt, d, sdim, &pstt) ||
+      !f32_state(sw, 1, 0, &psw))
+    return false;
+  std::vector<double> buf(3 * d);
+  double wsum = 0.0;
+  tea_cpu::moment_sums(x.data_ptr<float>(), x.stride(0), x.dim() == 2 ? x.stride(1) : 0, t.data_ptr<float>(),
+                       t.stride(0), t.dim() == 2 ? t.stride(1) : 0, w.has_value() ? w->data_ptr<float>() : nullptr,
+                       w.has_value() ? w->stride(0) : 0, n, d, psse ? buf.data() : nullptr,
+                       pst ? buf.data() + d : nullptr, pstt ? buf.data() + 2 * d : nullptr, wsum);
+  for (int64_t c = 0; c < d; ++c) {
+    if (psse) psse[c] += static_cast<float>(buf[c]);
+    if (pst) pst[c] += static_cast<float>(buf[d + c]);
+    if (pstt) pstt[c] += static_cast<float>(buf[2 * d + c]);
+  }
+  if (psw) psw[0] += static_cast<float>(count || !w.has_value() ? static_cast<double>(n) : wsum);
+  return true;
+}
+
+// ---- macro / weighted averages of per-class counts (small CPU states) ----
+
+// -> (0-d float32 average, some class has no label, recall's NaN positions in the masked vector);
+// kinds and averages as tea_cpu::class_average
+std::tuple<at::Tensor, bool, std::vector<int64_t>> cpu_class_average(int64_t kind, int64_t avg, const at::Tensor& a,
+                                                                     const at::Tensor& b,
+                                                                     const c10::optional<at::Tensor>& c) {
+  TORCH_CHECK(kind >= 0 && kind <= 3 && (avg == 0 || (avg == 1 && kind != 0)) && (kind == 0 || c.has_value()),
+              "cpu_class_average: bad kind / average");
+  auto ok = [&](const at::Tensor& v) {
+    return !v.is_cuda() && v.scalar_type() == at::kFloat && v.dim() == 1 && v.is_contiguous() && v.numel() == a.numel();
+  };
+  TORCH_CHECK(ok(a) && ok(b) && (!c.has_value() || ok(*c)), "cpu_class_average: contiguous float32 [C] CPU counts");
+  bool label_zero = false;
+  std::vector<int64_t> nan_idx;
+  at::Tensor out = at::empty({}, at::TensorOptions().dtype(at::kFloat));
+  out.data_ptr<float>()[0] = tea_cpu::class_average(static_cast<int>(kind), static_cast<int>(avg), a.data_ptr<float>(),
+                                                    b.data_ptr<float>(), c.has_value() ? c->data_ptr<float>() : nullptr,
+                                                    a.numel(), &label_zero, &nan_idx);
+  return {out, label_zero, nan_idx};
+}
+
+// The macro / weighted multiclass functionals of a small CPU batch in one call: the class
+// histograms (tea_cpu::cls_counts into local float32 arrays) and then tea_cpu::class_average.
+// None when a label is out of range (the caller's ATen path raises the reference's error).
+c10::optional<std::tuple<at::Tensor, bool, std::vector<int64_t>>> cpu_class_metric(int64_t kind, int64_t avg,
+                                                                                   const at::Tensor& input,
+                                                                                   const at::Tensor& target, int64_t C,
+                                                                                   int64_t k) {
+  TORCH_CHECK(kind >= 0 && kind <= 3 && (avg == 0 || (avg == 1 && kind != 0)) && C > 0 && k >= 1 &&
+                  (k == 1 || kind == 0),
+              "cpu_class_metric: bad kind / average / k");
+  TORCH_CHECK(!input.is_cuda() && !target.is_cuda() && target.dim() == 1 && label_dtype(target),
+              "cpu_class_metric: CPU [N] int64 / int32 target");
+  const int64_t n = target.size(0);
+  const bool scores = input.dim() == 2;
+  if (scores) {
+    TORCH_CHECK(input.size(0) == n && input.size(1) == C && input.stride(1) == 1 &&
+                    (input.scalar_type() == at::kFloat || input.scalar_type() == at::kDouble),
+                "cpu_class_metric: scores [N, C] float32 / float64 with unit column stride");
+  } else {
+    TORCH_CHECK(input.dim() == 1 && input.size(0) == n && label_dtype(input) && k == 1,
+                "cpu_class_metric: labels [N] int64 / int32");
+  }
+  if (!cpu_labels_valid(input, target, C)) return c10::nullopt;
+  std::vector<float> cc(C, 0.f), cl(C, 0.f), cp(C, 0.f), cf(C, 0.f);
+  tea_cpu::ClsOut o;
+  o.cc = cc.data();
+  o.cl = cl.data();
+  if (k == 1) {
+    o.cp = cp.data();
+    o.cf = cf.data();
+  }
+  const tea_cpu::Labels tl = labels_of(target);
+  if (!scores)
+    tea_cpu::cls_counts<float>(nullptr, 0, labels_of(input), tl, n, C, k, o);
+  else if (input.scalar_type() == at::kFloat)
+    tea_cpu::cls_counts(input.data_ptr<float>(), input.stride(0), tea_cpu::Labels{}, tl, n, C, k, o);
+  else
+    tea_cpu::cls_counts(input.data_ptr<double>(), input.stride(0), tea_cpu::Labels{}, tl, n, C, k, o);
+  // (a, b, c) per kind, as cpu_class_average
+  const float* a = cc.data();
+  const float* b = kind == 2 ? cf.data() : cl.data();
+  const float* c = kind == 2 ? cl.data() : cp.data();
+  bool label_zero = false;
+  std::vector<int64_t> nan_idx;
+  at::Tensor out = at::empty({}, at::TensorOptions().dtype(at::kFloat));
+  out.data_ptr<float>()[0] = tea_cpu::class_average(static_cast<int>(kind), static_cast<int>(avg), a, b, c, C,
+                                                    &label_zero, &nan_idx);
+  return std::make_tuple(out, label_zero, nan_idx);
+}
+
+// ---- confusion matrices of small CPU batches ----
+
+// [C, C] counts in the target's dtype (the reference's ``ones_like(target)`` values), or None when
+// some label is out of range (the caller's checking path then raises the reference's error).
+// binary: input [N] float scores thresholded (torch.where(x < thr, 0, 1)); else argmax of [N, C]
+// float scores or [N] labels.
+c10::optional<at::Tensor> cpu_confusion(const at::Tensor& input, const at::Tensor& target, int64_t C,
+                                        double threshold, bool binary) {
+  TORCH_CHECK(!input.is_cuda() && !target.is_cuda() && target.dim() == 1 && label_dtype(target) &&
+                  input.size(0) == target.size(0) && C >= 2,
+              "cpu_confusion: CPU [N] int64 / int32 target");
+  const int64_t n = target.size(0);
+  const bool flt = input.scalar_type() == at::kFloat || input.scalar_type() == at::kDouble;
+  if (binary) {
+    TORCH_CHECK(input.dim() == 1 && flt && C == 2, "cpu_confusion: binary input [N] float32 / float64");
+  } else if (input.dim() == 2) {
+    TORCH_CHECK(flt && input.size(1) == C && input.stride(1) == 1, "cpu_confusion: scores [N, C] float32 / float64");
+  } else {
+    TORCH_CHECK(input.dim() == 1 && label_dtype(input), "cpu_confusion: labels [N] int64 / int32");
+  }
+  std::vector<int64_t> cm(C * C, 0);
+  const tea_cpu::Labels tl = labels_of(target);
+  bool ok;
+  if (!binary && input.dim() == 1)
+    ok = tea_cpu::confusion_counts<float>(nullptr, 0, labels_of(input), false, 0.0, tl, n, C, cm.data());
+  else if (input.scalar_type() == at::kFloat)
+    ok = tea_cpu::confusion_counts(input.data_ptr<float>(), input.stride(0), tea_cpu::Labels{},
+                                   binary, threshold, tl, n, C, cm.data());
+  else
+    ok = tea_cpu::confusion_counts(input.data_ptr<double>(), input.stride(0), tea_cpu::Labels{}, binary, threshold,
+                                   tl, n, C, cm.data());
+  if (!ok) return c10::nullopt;
+  at::Tensor out = at::empty({C, C}, at::TensorOptions().dtype(target.scalar_type()));
+  if (target.scalar_type() == at::kLong) std::copy(cm.begin(), cm.end(), out.data_ptr<int64_t>());
+  else
+    for (int64_t i = 0; i < C * C; ++i) out.data_ptr<int32_t>()[i] = static_cast<int32_t>(cm[i]);
+  return out;
+}
+
 }  // namespace
 
 void tea_register_cpu_metrics(pybind11::module_& m) {
@@ -555,6 +711,21 @@ void tea_register_cpu_metrics(pybind11::module_& m) {
         "host fast path of MulticlassAccuracy.update (micro): counts added into the states",
         pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("k"), pybind11::arg("correct"),
         pybind11::arg("total"));
+  m.def("cpu_moments_update", &cpu_moments_update,
+        "host fast path of MeanSquaredError / R2Score.update: FP64 batch sums added into float32 states",
+        pybind11::arg("x"), pybind11::arg("t"), pybind11::arg("w"), pybind11::arg("sse"), pybind11::arg("st"),
+        pybind11::arg("stt"), pybind11::arg("sw"), pybind11::arg("count"));
+  m.def("cpu_class_average", &cpu_class_average,
+        "macro / weighted accuracy, F1, precision, recall of float32 per-class counts (small CPU states)",
+        pybind11::arg("kind"), pybind11::arg("average"), pybind11::arg("a"), pybind11::arg("b"),
+        pybind11::arg("c") = pybind11::none());
+  m.def("cpu_class_metric", &cpu_class_metric,
+        "macro / weighted multiclass accuracy, F1, precision, recall of a small CPU batch in one call",
+        pybind11::arg("kind"), pybind11::arg("average"), pybind11::arg("input"), pybind11::arg("target"),
+        pybind11::arg("num_classes"), pybind11::arg("k") = 1);
+  m.def("cpu_confusion", &cpu_confusion, "host fast path of the confusion-matrix functionals for small CPU batches",
+        pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("num_classes"), pybind11::arg("threshold"),
+        pybind11::arg("binary"));
   m.def("cpu_micro_accuracy", &cpu_micro_accuracy,
         "host fast path: fused argmax / top-k test + micro accuracy for small CPU batches",
         pybind11::arg("input"), pybind11::arg("target"), pybind11::arg("k") = 1);

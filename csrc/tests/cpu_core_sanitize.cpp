@@ -3,6 +3,7 @@
 // rowsums_host.cpp), built with -fsanitize=address,undefined by tests/test_sanitizers.py and run
 // on randomized shapes (0, 1, odd, large), strides, NaN / inf values, weights and int / bool
 // targets, each result checked against a naive formula written independently here.
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
@@ -268,6 +269,112 @@ void test_regression() {
   }
 }
 
+// ---------------------------------------------------------------- class-API moment sums
+template <typename S>
+void test_moments() {
+  for (int it = 0; it < 300; ++it) {
+    const int64_t n = rsize(), d = rint(1, 9), pad = rint(0, 2);
+    const int64_t ld = d + pad;
+    std::vector<S> x = rvec<S>(n * ld + 1, 0.02), t = rvec<S>(n * ld + 1, 0.02), w = rvec<S>(n + 1);
+    const bool weighted = it % 2 == 0, want_st = it % 3 != 0;
+    std::vector<double> sse(d, -7), st(d, -7), stt(d, -7);  // overwritten, not accumulated
+    double sw = -7;
+    tea_cpu::moment_sums(x.data(), ld, 1, t.data(), ld, 1, weighted ? w.data() : nullptr, 1, n, d, sse.data(),
+                         want_st ? st.data() : nullptr, stt.data(), sw);
+    double wsw = 0;
+    for (int64_t i = 0; i < n; ++i) wsw += weighted ? static_cast<double>(w[i]) : 1.0;
+    CHECK(close(sw, wsw, 1e-12), "moments sw");
+    for (int64_t c = 0; c < d; ++c) {
+      double a = 0, b = 0, e2 = 0;
+      for (int64_t i = 0; i < n; ++i) {
+        const double wi = weighted ? static_cast<double>(w[i]) : 1.0;
+        const double tv = t[i * ld + c], e = tv - static_cast<double>(x[i * ld + c]);
+        a += wi * e * e;
+        b += wi * tv;
+        e2 += wi * tv * tv;
+      }
+      CHECK(close(sse[c], a, 1e-9) && close(stt[c], e2, 1e-9), "moments sse / stt c=%lld", (long long)c);
+      CHECK(want_st ? close(st[c], b, 1e-9) : st[c] == -7, "moments st c=%lld", (long long)c);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- class averages
+void test_class_average() {
+  for (int it = 0; it < 600; ++it) {
+    const int64_t C = rint(1, 40);
+    const int kind = static_cast<int>(rint(0, 3)), avg = kind == 0 ? 0 : static_cast<int>(rint(0, 1));
+    std::vector<float> a(C), b(C), c(C);
+    for (int64_t i = 0; i < C; ++i) {  // counts with zeros: absent classes, empty predictions
+      b[i] = static_cast<float>(rint(0, 3) == 0 ? 0 : rint(0, 20));
+      c[i] = static_cast<float>(rint(0, 3) == 0 ? 0 : rint(0, 20));
+      a[i] = static_cast<float>(rint(0, static_cast<int64_t>(std::min(b[i], c[i]))));
+    }
+    bool zero = false;
+    std::vector<int64_t> nan_idx;
+    const float got = tea_cpu::class_average(kind, avg, a.data(), b.data(), c.data(), C, &zero, &nan_idx);
+    // naive: the reference's masked expressions, element-wise in float32
+    const std::vector<float>& label = kind == 2 ? c : b;
+    double lsum = 0;
+    for (float v : label) lsum += v;
+    double num = 0;
+    int64_t cnt = 0;
+    bool any_zero = false;
+    std::vector<int64_t> want_nan;
+    for (int64_t i = 0; i < C; ++i) {
+      any_zero |= b[i] == 0;
+      bool keep;
+      float v;
+      if (kind == 0) { keep = b[i] != 0; v = a[i] / b[i]; }
+      else if (kind == 1) { keep = b[i] != 0 || c[i] != 0; const float p = a[i] / c[i], r = a[i] / b[i]; v = tea_cpu::nan_to_num(2.f * p * r / (p + r)); }
+      else if (kind == 2) { keep = c[i] != 0 || a[i] + b[i] != 0; v = tea_cpu::nan_to_num(a[i] / (a[i] + b[i])); }
+      else { keep = b[i] != 0 || c[i] != 0; v = a[i] / b[i]; if (keep && std::isnan(v)) { want_nan.push_back(cnt); v = 0; } }
+      if (!keep) continue;
+      num += avg == 0 ? static_cast<double>(v) : static_cast<double>(v * (label[i] / static_cast<float>(lsum)));
+      ++cnt;
+    }
+    const double want = avg == 0 ? num / static_cast<double>(cnt) : num;
+    CHECK(close(got, static_cast<float>(want), 1e-6), "class_average kind %d avg %d C %lld: %g vs %g", kind, avg,
+          (long long)C, static_cast<double>(got), want);
+    if (kind == 1) CHECK(zero == any_zero, "class_average label-zero flag");
+    if (kind == 3) CHECK(nan_idx == want_nan, "class_average recall NaN positions");
+  }
+}
+
+// ---------------------------------------------------------------- confusion counts
+template <typename S>
+void test_confusion() {
+  for (int it = 0; it < 300; ++it) {
+    const int64_t n = rsize(), C = rint(2, 12), ld = C + rint(0, 2);
+    const bool binary = it % 3 == 0, labels_in = !binary && it % 3 == 1;
+    const int64_t Ce = binary ? 2 : C;
+    std::vector<S> x = rvec<S>(n * ld + 1, 0.05, true);
+    std::vector<int64_t> t(n), p(n);
+    const bool bad = it % 11 == 0 && n > 0;
+    for (int64_t i = 0; i < n; ++i) {
+      t[i] = rint(0, Ce - 1);
+      p[i] = rint(0, Ce - 1);
+    }
+    if (bad) t[rint(0, n - 1)] = Ce;
+    tea_cpu::Labels tl{t.data(), true, 1}, pl{p.data(), true, 1};
+    std::vector<int64_t> cm(Ce * Ce, 0);
+    const bool ok = labels_in ? tea_cpu::confusion_counts<S>(nullptr, 0, pl, false, 0.0, tl, n, Ce, cm.data())
+                              : tea_cpu::confusion_counts(x.data(), binary ? 1 : ld, tea_cpu::Labels{}, binary, 0.25,
+                                                          tl, n, Ce, cm.data());
+    CHECK(ok == !bad, "confusion validity");
+    if (!ok) continue;
+    std::vector<int64_t> want(Ce * Ce, 0);
+    for (int64_t i = 0; i < n; ++i) {
+      int64_t q;
+      if (labels_in) q = p[i];
+      else if (binary) q = x[i] < static_cast<S>(0.25) ? 0 : 1;
+      else q = tea_cpu::row_argmax(x.data() + i * ld, C);
+      ++want[t[i] * Ce + q];
+    }
+    CHECK(cm == want, "confusion counts n=%lld C=%lld binary=%d", (long long)n, (long long)Ce, binary);
+  }
+}
+
 // ---------------------------------------------------------------- K5b host twin
 void test_rowsums() {
   using namespace tea;
@@ -359,6 +466,11 @@ int main() {
   test_binary();
   test_regression<float>();
   test_regression<double>();
+  test_moments<float>();
+  test_moments<double>();
+  test_class_average();
+  test_confusion<float>();
+  test_confusion<double>();
   test_rowsums();
   if (g_fail) {
     std::printf("cpu_core_sanitize: %d failures\n", g_fail);

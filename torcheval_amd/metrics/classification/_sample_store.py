@@ -29,11 +29,23 @@ class SampleStoreMetric(Metric[TComputeReturn]):
     def _check(self, input: torch.Tensor, target: torch.Tensor) -> None:
         pass
 
-    @inference_update
     def update(self: TSelf, input: torch.Tensor, target: torch.Tensor) -> TSelf:
         """Append a batch of scores and targets (kept on the metric's device)."""
-        input = input.to(self.device)
-        target = target.to(self.device)
+        dev = self._device
+        if input.device != dev or target.device != dev:
+            return self._update_moved(input, target)
+        # already on the metric's device: the reference's ``.to`` is a no-op that stores the
+        # caller's tensors themselves, so neither the copy nor the inference-mode context
+        # (~2-4 us, the whole cost of a small append) is needed
+        self._check(input, target)
+        self.inputs.append(input)
+        self.targets.append(target)
+        return self
+
+    @inference_update
+    def _update_moved(self: TSelf, input: torch.Tensor, target: torch.Tensor) -> TSelf:
+        input = input.to(self._device)
+        target = target.to(self._device)
         self._check(input, target)
         self.inputs.append(input)
         self.targets.append(target)

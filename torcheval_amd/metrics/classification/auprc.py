@@ -4,8 +4,6 @@ from typing import Optional
 
 import torch
 
-from torcheval_amd.metrics.metric import inference_update
-
 from torcheval_amd.metrics.classification._sample_store import SampleStoreMetric
 from torcheval_amd.metrics.functional.classification._curve import merged_areas, runs_mergeable, sort_run
 from torcheval_amd.metrics.functional.classification.auprc import (
@@ -35,10 +33,9 @@ class BinaryAUPRC(SampleStoreMetric[torch.Tensor]):
     def _check(self, input, target) -> None:
         _binary_auprc_update_input_check(input, target, self.num_tasks)
 
-    @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "BinaryAUPRC":
         self._sorted_runs = False
-        return super().update(input, target)
+        return SampleStoreMetric.update(self, input, target)
 
     @torch.inference_mode()
     def compute(self) -> torch.Tensor:

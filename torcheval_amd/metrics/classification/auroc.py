@@ -24,6 +24,19 @@ TAUROC = TypeVar("TAUROC")
 TMulticlassAUROC = TypeVar("TMulticlassAUROC")
 
 
+_NO_WEIGHT = {}
+
+
+def _no_weight(device: torch.device) -> torch.Tensor:
+    """The shared empty float64 placeholder of an unweighted batch (one per device, a normal
+    tensor even when first made inside inference mode): no allocation per append."""
+    t = _NO_WEIGHT.get(device)
+    if t is None:
+        with torch.inference_mode(False):
+            t = _NO_WEIGHT[device] = torch.empty(0, dtype=torch.float64, device=device)
+    return t
+
+
 def _cat_weights(inputs: List[torch.Tensor], weights: List[torch.Tensor]) -> Optional[torch.Tensor]:
     if all(w.numel() == 0 for w in weights):
         return None
@@ -55,7 +68,6 @@ class BinaryAUROC(Metric[torch.Tensor]):
         self._add_state("targets", [], merge="cat")
         self._add_state("weights", [], merge="cat")
 
-    @inference_update
     def update(
         self: TAUROC,
         input: torch.Tensor,
@@ -63,15 +75,29 @@ class BinaryAUROC(Metric[torch.Tensor]):
         weight: Optional[torch.Tensor] = None,
     ) -> TAUROC:
         """Append a batch of scores, {0,1} targets and optional weights."""
-        input = input.to(self.device)
-        target = target.to(self.device)
-        if weight is not None:
-            weight = weight.to(self.device)
+        dev = self._device
+        if input.device != dev or target.device != dev or (weight is not None and weight.device != dev):
+            return self._update_moved(input, target, weight)
+        # on the metric's device already: stored as they are (the reference's no-op ``.to``),
+        # with no inference-mode context (see SampleStoreMetric.update)
         _binary_auroc_update_input_check(input, target, self.num_tasks, weight)
         self._sorted_runs = False
         self.inputs.append(input)
         self.targets.append(target)
-        self.weights.append(weight if weight is not None else input.new_empty(0, dtype=torch.float64))
+        self.weights.append(weight if weight is not None else _no_weight(dev))
+        return self
+
+    @inference_update
+    def _update_moved(self: TAUROC, input, target, weight) -> TAUROC:
+        input = input.to(self._device)
+        target = target.to(self._device)
+        if weight is not None:
+            weight = weight.to(self._device)
+        _binary_auroc_update_input_check(input, target, self.num_tasks, weight)
+        self._sorted_runs = False
+        self.inputs.append(input)
+        self.targets.append(target)
+        self.weights.append(weight if weight is not None else _no_weight(self._device))
         return self
 
     @torch.inference_mode()

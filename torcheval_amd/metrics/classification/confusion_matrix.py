@@ -65,6 +65,9 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
         target = target.to(self.device)
         if native_cls(input, target, self.confusion_matrix, num_classes=self.num_classes) and input.shape[0] > 0:
             _confusion_matrix_shape_check(input, target, self.num_classes)
+            if not input.is_cuda:  # the host twin ran after a label-range check: nothing to flag
+                cls_counts(input, target, num_classes=self.num_classes, confusion=self.confusion_matrix.view(-1))
+                return self
             if self._err is None:
                 self._err = torch.zeros(3, dtype=torch.int32, device=input.device)
             self._err_dtypes = (target.dtype, input.dtype)
@@ -86,8 +89,15 @@ class MulticlassConfusionMatrix(Metric[torch.Tensor]):
             _raise_confusion_err(torch.tensor([code]), torch.tensor(max_p, dtype=self._err_dtypes[1]),
                                  torch.tensor(max_t, dtype=self._err_dtypes[0]), self.num_classes)
 
-    @torch.inference_mode()
     def compute(self: TMulticlassConfusionMatrix) -> torch.Tensor:
+        if self._err is None and self.normalize in (None, "none"):
+            # the raw counts: no tensor op, so no inference-mode context (~2-4 us on small states)
+            out = self.confusion_matrix
+            return out.clone() if self._tea_sb is not None else out
+        with torch.inference_mode():
+            return self._compute()
+
+    def _compute(self: TMulticlassConfusionMatrix) -> torch.Tensor:
         self._check_device_errors()
         out = _confusion_matrix_compute(self.confusion_matrix, normalize=self.normalize)
         # never hand out a state that lives in a state buffer: reset() restores it in place

@@ -19,6 +19,8 @@ from torcheval_amd.ops.classification import (
     binary_counts,
     cls_counts,
     cls_counts_supported,
+    cpu_class_average,
+    cpu_class_metric,
     multilabel_counts,
     native_cls,
     native_multilabel,
@@ -88,6 +90,12 @@ def multiclass_accuracy(
     ):
         # small CPU batches: one fused C++ call instead of six ATen dispatches
         return native().cpu_micro_accuracy(input, target, k)
+    if average == "macro" and type(k) == int and k >= 1:
+        _accuracy_param_check(average, num_classes, k)
+        _accuracy_update_input_check(input, target, num_classes, k)
+        fast = cpu_class_metric(0, average, input, target, num_classes, k)
+        if fast is not None:  # small CPU batch: one host call, no inference-mode context
+            return fast[0]
     return _multiclass_accuracy_impl(input, target, average=average, num_classes=num_classes, k=k)
 
 
@@ -212,6 +220,9 @@ def _accuracy_compute(
     average: Optional[str],
 ) -> torch.Tensor:
     if isinstance(average, str) and average == "macro":
+        fast = cpu_class_average(0, average, num_correct, num_total)
+        if fast is not None:  # small CPU states: one host call
+            return fast[0]
         mask = num_total != 0
         return (num_correct[mask] / num_total[mask]).mean()
     return num_correct / num_total

@@ -12,7 +12,7 @@ from typing import Optional
 import torch
 import torch.nn.functional as F
 
-from torcheval_amd.ops.classification import binary_counts, cls_counts, native_binary, native_cls
+from torcheval_amd.ops.classification import binary_counts, cls_counts, cpu_confusion, native_binary, native_cls
 from torcheval_amd.ops.hostread import read_int
 
 
@@ -27,6 +27,11 @@ def binary_confusion_matrix(
     """2x2 confusion matrix (rows: target, cols: prediction) of thresholded ``input``.
     ``normalize`` in None | "none" | "true" | "pred" | "all".  Class: ``BinaryConfusionMatrix``."""
     _confusion_matrix_param_check(2, normalize)
+    if normalize in (None, "none"):
+        _binary_confusion_matrix_update_input_check(input, target)
+        cm = cpu_confusion(input, target, 2, threshold, binary=True)
+        if cm is not None:  # small CPU batch: one host call
+            return cm
     matrix = _binary_confusion_matrix_update(input, target, threshold)
     return _functional_result(matrix, normalize)
 
@@ -42,6 +47,11 @@ def multiclass_confusion_matrix(
     """[C, C] confusion matrix (rows: target, cols: prediction).
     Class version: ``MulticlassConfusionMatrix``."""
     _confusion_matrix_param_check(num_classes, normalize)
+    if normalize in (None, "none"):
+        _confusion_matrix_shape_check(input, target, num_classes)
+        cm = cpu_confusion(input, target, num_classes)
+        if cm is not None:  # small CPU batch, labels in range: one host call
+            return cm
     cm = _confusion_matrix_update(input, target, num_classes)
     return _functional_result(cm, normalize)
 

@@ -6,7 +6,15 @@ from typing import Optional, Tuple
 import torch
 
 from torcheval_amd.ops import native
-from torcheval_amd.ops.classification import _cpu_prf_ok, binary_counts, cls_counts, native_binary, native_cls
+from torcheval_amd.ops.classification import (
+    _cpu_prf_ok,
+    binary_counts,
+    cls_counts,
+    cpu_class_average,
+    cpu_class_metric,
+    native_binary,
+    native_cls,
+)
 
 
 @torch.inference_mode()
@@ -24,7 +32,6 @@ def binary_f1_score(input: torch.Tensor, target: torch.Tensor, *, threshold: flo
     return _f1_score_compute(num_tp, num_label, num_prediction, "micro")
 
 
-@torch.inference_mode()
 def multiclass_f1_score(
     input: torch.Tensor,
     target: torch.Tensor,
@@ -35,6 +42,16 @@ def multiclass_f1_score(
     """F1 for ``[N]`` labels or ``[N, C]`` scores; ``average`` in micro | macro | weighted |
     None.  Class version: ``MulticlassF1Score``."""
     _f1_score_param_check(num_classes, average)
+    if average in ("macro", "weighted"):
+        _f1_score_update_input_check(input, target, num_classes)
+        fast = cpu_class_metric(1, average, input, target, num_classes)
+        if fast is not None:  # small CPU batch: one host call, no inference-mode context
+            return _f1_fast(fast)
+    return _multiclass_f1_score(input, target, num_classes, average)
+
+
+@torch.inference_mode()
+def _multiclass_f1_score(input, target, num_classes, average) -> torch.Tensor:
     num_tp, num_label, num_prediction = _f1_score_update(input, target, num_classes, average)
     return _f1_score_compute(num_tp, num_label, num_prediction, average)
 
@@ -106,6 +123,9 @@ def _f1_score_compute(
     num_prediction: torch.Tensor,
     average: Optional[str],
 ) -> torch.Tensor:
+    fast = cpu_class_average(1, average, num_tp, num_label, num_prediction)
+    if fast is not None:  # small CPU states: one host call
+        return _f1_fast(fast)
     num_label_is_zero = num_label == 0
     if num_label_is_zero.any():
         logging.warning(
@@ -124,6 +144,15 @@ def _f1_score_compute(
     if average == "weighted":
         return (f1 * (num_label / num_label.sum())).sum()
     return f1
+
+
+def _f1_fast(fast) -> torch.Tensor:
+    """The result of a host-call average (ops.classification.cpu_class_*), with the warning."""
+    if fast[1]:
+        logging.warning(
+            "Warning: Some classes do not exist in the target. F1 scores for these classes will be cast to zeros."
+        )
+    return fast[0]
 
 
 def _f1_score_param_check(num_classes: Optional[int], average: Optional[str]) -> None:

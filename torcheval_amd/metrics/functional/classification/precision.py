@@ -10,7 +10,15 @@ from typing import Optional, Tuple
 import torch
 
 from torcheval_amd.ops import native
-from torcheval_amd.ops.classification import _cpu_prf_ok, binary_counts, cls_counts, native_binary, native_cls
+from torcheval_amd.ops.classification import (
+    _cpu_prf_ok,
+    binary_counts,
+    cls_counts,
+    cpu_class_average,
+    cpu_class_metric,
+    native_binary,
+    native_cls,
+)
 
 
 @torch.inference_mode()
@@ -24,7 +32,6 @@ def binary_precision(input: torch.Tensor, target: torch.Tensor, *, threshold: fl
     return _precision_compute(num_tp, num_fp, num_label, "micro")
 
 
-@torch.inference_mode()
 def multiclass_precision(
     input: torch.Tensor,
     target: torch.Tensor,
@@ -35,6 +42,16 @@ def multiclass_precision(
     """Precision for ``[N]`` labels or ``[N, C]`` scores; ``average`` in micro | macro |
     weighted | None.  Class version: ``torcheval_amd.metrics.MulticlassPrecision``."""
     _precision_param_check(num_classes, average)
+    if average in ("macro", "weighted"):
+        _precision_update_input_check(input, target, num_classes)
+        fast = cpu_class_metric(2, average, input, target, num_classes)
+        if fast is not None:  # small CPU batch: one host call, no inference-mode context
+            return fast[0]
+    return _multiclass_precision(input, target, num_classes, average)
+
+
+@torch.inference_mode()
+def _multiclass_precision(input, target, num_classes, average) -> torch.Tensor:
     num_tp, num_fp, num_label = _precision_update(input, target, num_classes, average)
     return _precision_compute(num_tp, num_fp, num_label, average)
 
@@ -74,6 +91,9 @@ def _precision_compute(
     num_label: torch.Tensor,
     average: Optional[str],
 ) -> torch.Tensor:
+    fast = cpu_class_average(2, average, num_tp, num_fp, num_label)
+    if fast is not None:  # small CPU states: one host call
+        return fast[0]
     if average in ("macro", "weighted"):
         mask = (num_label != 0) | (num_tp + num_fp != 0)
         num_tp, num_fp = num_tp[mask], num_fp[mask]

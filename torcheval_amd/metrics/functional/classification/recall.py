@@ -11,7 +11,15 @@ from typing import Optional, Tuple
 import torch
 
 from torcheval_amd.ops import native
-from torcheval_amd.ops.classification import _cpu_prf_ok, binary_counts, cls_counts, native_binary, native_cls
+from torcheval_amd.ops.classification import (
+    _cpu_prf_ok,
+    binary_counts,
+    cls_counts,
+    cpu_class_average,
+    cpu_class_metric,
+    native_binary,
+    native_cls,
+)
 
 
 @torch.inference_mode()
@@ -60,7 +68,6 @@ def _binary_recall_update_input_check(input: torch.Tensor, target: torch.Tensor)
         raise ValueError(f"target should be a one-dimensional tensor, got shape {target.shape}.")
 
 
-@torch.inference_mode()
 def multiclass_recall(
     input: torch.Tensor,
     target: torch.Tensor,
@@ -71,6 +78,16 @@ def multiclass_recall(
     """Recall for ``[N]`` labels or ``[N, C]`` scores; ``average`` in micro | macro |
     weighted | None.  Class version: ``MulticlassRecall``."""
     _recall_param_check(num_classes, average)
+    if average in ("macro", "weighted"):
+        _recall_update_input_check(input, target, num_classes)
+        fast = cpu_class_metric(3, average, input, target, num_classes)
+        if fast is not None:  # small CPU batch: one host call, no inference-mode context
+            return _recall_fast(fast)
+    return _multiclass_recall(input, target, num_classes, average)
+
+
+@torch.inference_mode()
+def _multiclass_recall(input, target, num_classes, average) -> torch.Tensor:
     num_tp, num_labels, num_predictions = _recall_update(input, target, num_classes, average)
     return _recall_compute(num_tp, num_labels, num_predictions, average)
 
@@ -111,6 +128,9 @@ def _recall_compute(
     num_predictions: torch.Tensor,
     average: Optional[str],
 ) -> torch.Tensor:
+    fast = cpu_class_average(3, average, num_tp, num_labels, num_predictions)
+    if fast is not None:  # small CPU states: one host call
+        return _recall_fast(fast)
     if average in ("macro", "weighted"):
         mask = (num_labels != 0) | (num_predictions != 0)
         num_tp = num_tp[mask]
@@ -132,6 +152,15 @@ def _recall_compute(
     if average == "weighted":
         return (recall * (num_labels[mask] / num_labels.sum())).sum()
     return recall
+
+
+def _recall_fast(fast) -> torch.Tensor:
+    """The result of a host-call average (ops.classification.cpu_class_*), with the warning."""
+    if fast[2]:
+        logging.warning(
+            f"One or more NaNs identified, as no ground-truth instances of {fast[2]} have been seen. These have been converted to zero."
+        )
+    return fast[0]
 
 
 def _recall_param_check(num_classes: Optional[int], average: Optional[str]) -> None:

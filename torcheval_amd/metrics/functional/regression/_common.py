@@ -4,7 +4,11 @@ from typing import Optional, Tuple
 
 import torch
 
-from torcheval_amd.ops import compiling, native, use_native
+from torcheval_amd.ops import _C, compiling, native, use_native
+from torcheval_amd.ops import rowsums as _rs
+
+# K5b statistic -> cpu_moments_update destination (sse, st, stt, sw)
+_CPU_SLOT = {_rs.WSSE: 0, _rs.SSE: 0, _rs.WT: 1, _rs.WTT: 2, _rs.W: 3, _rs.COUNT: 3}
 
 
 def _native(input: torch.Tensor, target: torch.Tensor, w: Optional[torch.Tensor] = None) -> bool:
@@ -43,6 +47,25 @@ def _promote_lazy(metric, names, input: torch.Tensor) -> bool:
     return all(s.numel() == d and s.ndim == (1 if input.ndim == 2 else 0) for s in states)
 
 
+def _cpu_update(metric, input: torch.Tensor, target: torch.Tensor, w: Optional[torch.Tensor], sums, scalars) -> bool:
+    """Small CPU batch: one host call (csrc/runtime/cpu_metrics.cpp cpu_moments_update) adds
+    the FP64 batch sums into the f32 states; it declines (False) any dtype / shape / state
+    layout it does not take, so the checks stay in C++."""
+    n = input.numel()
+    if n == 0 or n > _rs.HOST_MAX or _C is None or compiling():
+        return False
+    if input.ndim == 2 and not _promote_lazy(metric, [s for s, _ in sums], input):
+        return False
+    kw = [None, None, None, None]  # sse, st, stt, sw
+    count = False
+    for name, stat in sums:
+        kw[_CPU_SLOT[stat]] = _state(metric, name)
+    for name, stat in scalars:
+        kw[_CPU_SLOT[stat]] = _state(metric, name)
+        count = count or stat == _rs.COUNT
+    return _C.cpu_moments_update(input, target, w, kw[0], kw[1], kw[2], kw[3], count)
+
+
 def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w: Optional[torch.Tensor],
                             sums, scalars) -> bool:
     """One-call update of per-column regression sums straight into ``metric``'s f32 states.
@@ -50,9 +73,10 @@ def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w
     ``sums``: (state name, K5b stat) of the [d] states; ``scalars``: (state name, stat) of the
     0-d ones (a count or a weight total).  ROCm [n, d] batches run K5 column moments
     (coalesced over d) accumulating into the states; ROCm [n] batches and small CPU batches
-    run K5b (``ops/rowsums.py``) over the transposed view.  False: take the ATen path."""
-    from torcheval_amd.ops import rowsums as _rs
-
+    run K5b (``ops/rowsums.py``) over the transposed view; small CPU batches one host call
+    (csrc/runtime/cpu_metrics.cpp cpu_moments_update).  False: take the ATen path."""
+    if not input.is_cuda and _cpu_update(metric, input, target, w, sums, scalars):
+        return True
     if input.dtype != torch.float32 or target.dtype != torch.float32:
         return False
     if w is not None and (w.dtype != torch.float32 or w.ndim != 1):

@@ -86,6 +86,69 @@ def _cpu_prf_ok(input: torch.Tensor, target: torch.Tensor) -> bool:
     )
 
 
+_AVERAGES = {"macro": 0, "weighted": 1}
+
+
+def cpu_class_average(kind: int, average, a: torch.Tensor, b: torch.Tensor, c: Optional[torch.Tensor] = None):
+    """Macro / weighted averages of small CPU float32 per-class count vectors in one host call
+    (csrc/runtime/cpu_metrics.cpp cpu_class_average) instead of the ~10-op ATen mask / divide /
+    nan_to_num / mean chain.  kind: 0 accuracy (correct, total), 1 F1 (tp, label, pred),
+    2 precision (tp, fp, label), 3 recall (tp, label, pred).  Returns (0-d float32 value, some
+    class has no label, recall's NaN class positions) or None (take the ATen path)."""
+    if average not in _AVERAGES or (kind == 0 and average != "macro"):
+        return None
+    if compiling() or _ops.DISABLE_HIP or not native_loaded() or a.numel() > _CPU_MAX:
+        return None
+    for v in (a, b) if c is None else (a, b, c):
+        if (v.device.type != "cpu" or v.dtype != torch.float32 or v.dim() != 1 or not v.is_contiguous()
+                or v.numel() != a.numel() or v.requires_grad):
+            return None
+    return native().cpu_class_average(kind, _AVERAGES[average], a, b, c)
+
+
+def cpu_class_metric(kind: int, average, input: torch.Tensor, target: torch.Tensor,
+                     num_classes: Optional[int], k: int = 1):
+    """A whole macro / weighted multiclass functional (kinds as ``cpu_class_average``) of a small
+    CPU batch in one host call: class histograms and the average.  Returns the
+    ``cpu_class_average`` triple, or None (other shapes / dtypes / devices, or a label out of
+    range: the caller's ATen path then runs and raises the reference's errors)."""
+    if average not in _AVERAGES or (kind == 0 and average != "macro"):
+        return None
+    if compiling() or _ops.DISABLE_HIP or input.is_cuda or target.is_cuda or not native_loaded():
+        return None
+    if type(num_classes) is not int or num_classes <= 0 or input.numel() > _CPU_MAX or input.requires_grad:
+        return None
+    if target.dim() != 1 or target.dtype not in (torch.int64, torch.int32) or input.shape[0] != target.shape[0]:
+        return None
+    if input.dim() == 2:
+        if input.dtype not in (torch.float32, torch.float64) or input.shape[1] != num_classes or input.stride(1) != 1:
+            return None
+    elif input.dim() != 1 or input.dtype not in (torch.int64, torch.int32) or k != 1:
+        return None
+    return native().cpu_class_metric(kind, _AVERAGES[average], input, target, num_classes, k)
+
+
+def cpu_confusion(input: torch.Tensor, target: torch.Tensor, num_classes: int, threshold: float = 0.5,
+                  binary: bool = False) -> Optional[torch.Tensor]:
+    """[C, C] confusion counts of a small CPU batch in one host call (the target's integer dtype,
+    as the reference's ``ones_like(target)`` sparse sum), or None: out-of-range labels, other
+    dtypes / devices (the caller's checking path then runs)."""
+    if compiling() or _ops.DISABLE_HIP or input.is_cuda or target.is_cuda or not native_loaded():
+        return None
+    if target.dim() != 1 or target.dtype not in (torch.int64, torch.int32) or input.numel() > _CPU_MAX:
+        return None
+    if input.shape[0] != target.shape[0] or input.shape[0] == 0 or input.requires_grad:
+        return None  # (an empty batch takes the checking path: the reference's torch.max raises)
+    if binary or input.dim() == 2:
+        if input.dtype not in (torch.float32, torch.float64) or input.dim() != (1 if binary else 2):
+            return None
+        if not binary and (input.shape[1] != num_classes or input.stride(1) != 1):
+            return None
+    elif input.dim() != 1 or input.dtype not in (torch.int64, torch.int32):
+        return None
+    return native().cpu_confusion(input, target, int(num_classes), float(threshold), bool(binary))
+
+
 def _f32_scalars(*states: torch.Tensor) -> bool:
     """0-d float32 CPU states (the host twins' in-place contract)."""
     return all(s.dim() == 0 and s.dtype == torch.float32 and s.device.type == "cpu" for s in states)
