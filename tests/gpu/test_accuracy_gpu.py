@@ -237,3 +237,28 @@ def test_graphed_update_rejects_rebinding_metric():
         step(x, t)
         eager_m.update(x, t)
     torch.testing.assert_close(graphed_m.compute(), eager_m.compute())
+
+
+@pytest.mark.gpu
+def test_graphed_update_reports_its_measured_cost():
+    """GraphedUpdate times direct updates against replays at construction and warns when the
+    replay is slower (one-kernel updates on this runtime); the timing updates leave no trace."""
+    import warnings
+
+    from torcheval_amd.utils.graphs import GraphedUpdate
+
+    x = torch.randn(8, 6, device="cuda")
+    y = torch.randint(0, 6, (8,), device="cuda")
+    m = MulticlassAccuracy(device="cuda")
+    with warnings.catch_warnings(record=True) as rec:
+        warnings.simplefilter("always")
+        step = GraphedUpdate(m, x, y)
+    assert step.direct_us > 0 and step.replay_us > 0
+    slower = [w for w in rec if "graph replay costs" in str(w.message)]
+    assert bool(slower) == (step.replay_us > step.direct_us)
+    assert float(m.compute().nan_to_num(-1)) == -1  # no samples counted by the timing runs
+    step(x, y)
+    ref = MulticlassAccuracy(device="cuda")
+    ref.update(x, y)
+    torch.testing.assert_close(m.compute(), ref.compute())
+    print(f"GraphedUpdate bs=8: direct {step.direct_us:.1f} us, replay {step.replay_us:.1f} us")

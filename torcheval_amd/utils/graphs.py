@@ -1,10 +1,15 @@
 """HIP-graph capture of metric ``update`` calls.
 
-A metric update on the native path is a handful of launches (often one: K1, K2, K5, K7 write
-straight into the state tensors), so for small batches the step is launch- and Python-bound
-rather than HBM-bound.  ``GraphedUpdate`` records ``metric.update(*static_inputs)`` once into a
-HIP graph (``torch.cuda.CUDAGraph`` on ROCm) and then replays it: per call, the new inputs are
-copied into the static input buffers and the whole update is one graph launch.
+``GraphedUpdate`` records ``metric.update(*static_inputs)`` once into a HIP graph
+(``torch.cuda.CUDAGraph`` on ROCm) and then replays it: per call, the new inputs are copied into
+the static input buffers and the captured launches run as one graph launch.
+
+Measured cost, not a free speed-up: on this runtime (ROCm 7 / MI355X) a graph launch costs
+~27 us of wall time, while a direct one-kernel update (K1, K2, K5, K7 write straight into the
+states) costs ~5 us (``profiles/bench_suite_r4b.json``: the "HIP-graph replay" rows, 27.3 vs
+5.0 us at bs=8).  So a graph pays only for a step that chains many launches (a user's forward
+plus several metric updates, or an ATen-path update of ~10 ops), never for a one-kernel update.
+The constructor times both (``check_speed=True``) and warns when the replay is the slower one.
 
 Requirements (checked): the update must write its states in place (the native kernels do;
 an update that rebinds a state attribute, e.g. ``self.x = self.x + y``, would replay against
@@ -17,6 +22,8 @@ graph writes.  Anything else that rebinds a state after capture (``load_state_di
 ``to()``) is caught at the next replay, which raises instead of writing into freed memory.
 """
 
+import time
+import warnings
 from typing import Any, Dict, List, Tuple
 
 import torch
@@ -51,7 +58,7 @@ class GraphedUpdate:
         acc.compute()
     """
 
-    def __init__(self, metric: Metric, *example_args: torch.Tensor, warmup: int = 2) -> None:
+    def __init__(self, metric: Metric, *example_args: torch.Tensor, warmup: int = 2, check_speed: bool = True) -> None:
         if not all(isinstance(a, torch.Tensor) and a.is_cuda for a in example_args):
             raise ValueError("GraphedUpdate needs ROCm-device tensor inputs")
         self.metric = metric
@@ -83,7 +90,19 @@ class GraphedUpdate:
             raise RuntimeError(
                 f"{type(metric).__name__}.update rebinds its states; it cannot be replayed from a graph"
             )
-        # undo the warm-up updates in place (the graph holds these exact tensors)
+        torch.cuda.current_stream().wait_stream(stream)
+        self.direct_us = self.replay_us = None
+        if check_speed:
+            self.direct_us, self.replay_us = self._time(metric)
+            if self.replay_us > self.direct_us:
+                warnings.warn(
+                    f"GraphedUpdate({type(metric).__name__}): a graph replay costs {self.replay_us:.1f} us against "
+                    f"{self.direct_us:.1f} us for the direct update on this runtime; call metric.update directly "
+                    "(graphs pay only for steps that chain many launches)",
+                    RuntimeWarning,
+                    stacklevel=2,
+                )
+        # undo the warm-up / timing updates in place (the graph holds these exact tensors)
         with torch.no_grad():
             for name, v in before.items():
                 cur = getattr(metric, name)
@@ -94,6 +113,25 @@ class GraphedUpdate:
         torch.cuda.current_stream().wait_stream(stream)
         self._names = tuple(n for n, p in ptrs.items() if isinstance(p, int))
         self._ptrs = tuple(ptrs[n] for n in self._names)
+
+    def _time(self, metric: Metric, n: int = 10) -> Tuple[float, float]:
+        """Wall time per call (us) of ``n`` direct updates and of ``n`` replays, each run to
+        completion: what the caller's loop pays per step either way."""
+        out = []
+        for replay in (False, True):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(n):
+                if replay:
+                    self.graph.replay()
+                else:
+                    metric.update(*self._static)
+            torch.cuda.synchronize()
+            out.append((time.perf_counter() - t0) / n * 1e6)
+        mark = getattr(metric, "_mark_updated", None)
+        if mark is not None:  # replays added into deferred folds: let the restore see them
+            mark()
+        return out[0], out[1]
 
     @property
     def static_inputs(self) -> Tuple[torch.Tensor, ...]:
