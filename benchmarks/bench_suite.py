@@ -155,6 +155,11 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         x, y = rand(N100k, C100), randint(C100, N100k)
         return lambda: F.multiclass_auprc(x, y, num_classes=C100)
 
+    def mc_binned_auroc():
+        # the reference-default (per-sample) multiclass binned AUROC: K4b
+        x, y = rand(N100k, C100), randint(C100, N100k)
+        return lambda: F.multiclass_binned_auroc(x, y, num_classes=C100, threshold=200)
+
     def mc_binned_auprc_cls():
         x, y = rand(N100k, C100), randint(C100, N100k)
         m = M.MulticlassBinnedAUPRC(num_classes=C100, threshold=100, device=dev)
@@ -306,6 +311,7 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "multiclass_auroc N=100k C=100": mc_auroc,
         "multiclass_auprc N=100k C=100": mc_auprc,
         "MulticlassBinnedAUPRC(C=100,T=100).update N=100k": mc_binned_auprc_cls,
+        "multiclass_binned_auroc N=100k C=100 T=200 (K4b)": mc_binned_auroc,
         "MultilabelAccuracy(hamming).update 8192x1000": ml_hamming,
         "topk_multilabel_accuracy 8192x1000": topk_ml,
         "reciprocal_rank 8192x1000 k=10 (K10)": rr,

@@ -7,6 +7,7 @@
 #include <torch/extension.h>
 
 #include <cstdlib>
+#include <array>
 #include <mutex>
 #include <unordered_map>
 
@@ -117,6 +118,15 @@ void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, i
     else it->second = ws;
   }
   return it->second.data_ptr();
+}
+
+// K3 look-back kernels: tile ids from a counter ticket (TORCHEVAL_AMD_K3_DYNID=1) instead of blockIdx
+bool k3_dynid() {
+  static const bool v = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K3_DYNID");
+    return e != nullptr && e[0] == '1';
+  }();
+  return v;
 }
 
 void check_launch(int rc, const char* what) {
@@ -423,6 +433,17 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
   }
   Tensor ws = at::empty({tea::auc_scan_workspace_bytes(rows, n)},
                         at::TensorOptions().dtype(at::kByte).device(sorted.device()));
+  // opt-in: measured slower at 1M (tile_area 20.8 us against 11.7 + 5.0 for tile_area +
+  // tile_sums: every block reads its prefix through agent-scope loads; profiles/k3_onesweep_r5.json)
+  static const bool lb = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K3_LB");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (lb && payload_kind != 0 && rows <= 4) {  // tile totals published inside tile_area (sortscan.hip)
+    const int64_t words = 16 + rows * tea::auc_scan_tiles(n);
+    a.lb_hdr = static_cast<uint32_t*>(zeroed_workspace(sorted, stream_for(sorted), words * 4, 13));
+    a.lb_dyn = k3_dynid() ? 1 : 0;
+  }
   check_launch(tea::launch_auc_scan(a, ws.data_ptr(), stream_for(sorted)), "auc_scan");
 }
 
@@ -721,7 +742,7 @@ void row_sums(const Tensor& x_in, const optional<Tensor>& t_in, const optional<T
   if (a.blocks > 1) {  // stream-ordered scratch, fully rewritten by every call: cached, no allocation
     a.ws = static_cast<double*>(zeroed_workspace(x, stream_for(x), a.rows * a.blocks * tea::kRowRaw * 8, 3));
     if (mode != 0) {  // self-cleaning arrival tickets
-      a.ticket = static_cast<unsigned*>(zeroed_workspace(x, stream_for(x), a.rows * 4, 4));
+      a.ticket = static_cast<unsigned*>(zeroed_workspace(x, stream_for(x), a.rows * 4, 9));
       a.wt = mode == 2;
     }
   }
@@ -1272,6 +1293,44 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   a.region = (cap / 4 - 4) / 4;  // fixed per buffer, so the next call finds region 3 at the same place
   a.out_sorted = out_sorted.data_ptr<float>();
   a.out_order = out_order.data_ptr<int32_t>();
+  static const bool onesweep = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K3_ONESWEEP");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (onesweep && tea::radix_onesweep_ok(a.rows, a.n)) {
+    // self-cleaning onesweep state (tea_kernels.h RadixArgs): header + digit totals, the status
+    // planes and the group planes in three zeroed workspaces whose plane strides depend only on
+    // their capacity; if any of them is (re)allocated, all three restart from zero together
+    hipStream_t st = stream_for(x);
+    int64_t scap = 0, gcap = 0;
+    auto* hdr = static_cast<uint32_t*>(zeroed_workspace(x, st, (16 + a.rows * 8 * 4 * 256) * 4, 10));
+    auto* sws = static_cast<uint32_t*>(
+        zeroed_workspace(x, st, 2 * tea::radix_onesweep_status_words(a.rows, a.n) * 4, 11, &scap));
+    auto* gws = static_cast<unsigned long long*>(
+        zeroed_workspace(x, st, 2 * tea::radix_onesweep_group_words(a.rows, a.n) * 8, 12, &gcap));
+    {
+      static std::mutex mu;
+      static auto& seen = *new std::unordered_map<uint64_t, std::array<const void*, 3>>();
+      const uint64_t key = (static_cast<uint64_t>(x.device().index()) << 56) ^ reinterpret_cast<uint64_t>(st);
+      std::lock_guard<std::mutex> lock(mu);
+      const std::array<const void*, 3> now{hdr, sws, gws};
+      auto it = seen.find(key);
+      if (it != seen.end() && it->second != now) {
+        // one buffer is new (zero) while the others may hold another layout's dirty words
+        TORCH_CHECK(hipMemsetAsync(hdr, 0, (16 + a.rows * 8 * 4 * 256) * 4, st) == hipSuccess &&
+                        hipMemsetAsync(sws, 0, scap, st) == hipSuccess && hipMemsetAsync(gws, 0, gcap, st) == hipSuccess,
+                    "sort_desc: workspace reset failed");
+      }
+      seen[key] = now;
+    }
+    a.os_hdr = hdr;
+    a.os_g = hdr + 16;
+    a.os_status = sws;
+    a.os_splane = scap / 8;  // two u32 planes
+    a.os_gacc = gws;
+    a.os_gplane = gcap / 16;  // two u64 planes
+    a.os_dyn = k3_dynid() ? 1 : 0;
+  }
   Tensor pl;
   if (payload.has_value() && payload_kind != 0) {
     TORCH_CHECK(payload_kind == 1 || payload_kind == 2, "sort_desc: payload_kind must be 0, 1 or 2");

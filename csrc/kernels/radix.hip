@@ -21,6 +21,8 @@
 //     probabilities, whose top byte is nearly constant);
 //   * rows are independent segments: histogram/scan/offsets are per row, so a [C, n]
 //     one-vs-rest score matrix is sorted in the same 12 launches.
+#include <algorithm>
+
 #include "tea_common.h"
 #include "tea_kernels.h"
 
@@ -342,6 +344,310 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
   }
 }
 
+// ---------------------------------------------------------------- onesweep
+// The same sort in 5 launches instead of 8: ONE histogram kernel reads every key once and
+// counts all four digits (the row totals each pass needs for its digit starts), then each pass
+// ranks its tile exactly as the downsweep above and gets its tiles-before prefix in the same
+// launch (decoupled look-back, Merrill & Garland / Adinets & Merrill "onesweep"), so the four
+// upsweep launches and their second read of the keys are gone.
+//   * tiles take dynamic ids from a counter (launch order), so every tile a block waits on has
+//     started: no deadlock whatever the residency;
+//   * look-back without chained prefixes: each tile publishes its per-digit count (the data is
+//     the flag: bit 31 = ready) and adds it, with an arrival count, into its group's word (32
+//     tiles per group); a tile's prefix is the sum of the complete groups before its own plus
+//     the counts of the tiles before it in its group - <= 2 x 16 independent agent-scope loads
+//     per digit at <= 1024 tiles a row, every round trip in flight together (a chained
+//     inclusive-prefix look-back serialises hops when all tiles start at once, as they do here);
+//   * every hand-off word is an agent-scope (write-through) store / atomic and an agent-scope
+//     load (the XCDs' L2s are not coherent), relaxed: the words carry the data themselves;
+//   * self-cleaning: the status and group planes alternate between passes and each pass clears
+//     the plane the previous pass used, up to the extent recorded for it (so a later sort of
+//     another shape never reads stale flags); the last tile of each row in pass 3 clears the
+//     row's digit totals once every tile of the row has consumed them (its look-back saw all
+//     of them publish, and each publishes only after its digit-start scan); the histogram
+//     kernel resets the tile counters.  Every spin is bounded (a timeout sets hdr[8]).
+constexpr int kOSMaxTiles = 1024;
+constexpr uint32_t kReady = 0x80000000u;
+constexpr int kSpinLimit = 1 << 22;
+constexpr int kHistKeys = 16;  // keys per thread per round of the histogram kernel
+constexpr int kGCopies = 8;    // copies of the digit totals (histogram block % 8): 8x fewer
+                               // same-address device atomics (256 blocks on one address: ~5 us)
+
+typedef __attribute__((address_space(1))) unsigned os_u32;
+typedef __attribute__((address_space(1))) unsigned long long os_u64;
+
+__device__ __forceinline__ void os_put(uint32_t* p, uint32_t v) {
+  __hip_atomic_store((os_u32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t os_get(const uint32_t* p) {
+  return __hip_atomic_load((os_u32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long os_get64(const unsigned long long* p) {
+  return __hip_atomic_load((os_u64*)(const_cast<unsigned long long*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void os_add64(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_fetch_add((os_u64*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// all four digit histograms of the row's keys, one read: LDS counts (kC copies per digit, one
+// per lane % kC, against same-bin contention on the near-constant top byte), then one device
+// atomic per non-zero (digit, bin) into copy (block % kGCopies) of the row totals
+__global__ __launch_bounds__(kRT) void onesweep_hist_kernel(RadixArgs a, int64_t per_block) {
+  constexpr int kC = 8;
+  __shared__ uint32_t h[4][kC][kBins + 1];
+  for (int q = threadIdx.x; q < 4 * kC * (kBins + 1); q += kRT) (&h[0][0][0])[q] = 0u;
+  __syncthreads();
+  const int64_t row = blockIdx.y;
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * per_block;
+  const int64_t hi = lo + per_block < a.n ? lo + per_block : a.n;
+  const int c = threadIdx.x % kC;
+  const float* in = a.in + row * a.in_row_stride;
+  for (int64_t i0 = lo; i0 < hi; i0 += kRT * kHistKeys) {
+    uint32_t k[kHistKeys];
+#pragma unroll
+    for (int j = 0; j < kHistKeys; ++j) {  // clamped loads, all in flight; the tail masked below
+      const int64_t i = i0 + j * kRT + threadIdx.x;
+      k[j] = f2key_desc(in[i < hi ? i : hi - 1]);
+    }
+#pragma unroll
+    for (int j = 0; j < kHistKeys; ++j) {
+      if (i0 + j * kRT + threadIdx.x < hi) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p) atomicAdd(&h[p][c][(k[j] >> (8 * p)) & 0xffu], 1u);
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < kC; ++q) v += h[p][q][threadIdx.x];
+    if (v) atomicAdd(&a.os_g[((row * kGCopies + blockIdx.x % kGCopies) * 4 + p) * kBins + threadIdx.x], v);
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) a.os_hdr[threadIdx.x] = 0u;  // tile counters
+}
+
+// one pass: load + rank as radix_downsweep_kernel, then publish / look back, then scatter
+template <int kRounds, int VMODE, typename PT = uint32_t, int KIND = 0>
+__global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const uint32_t* keys_in,
+                                                            const uint32_t* vals_in, uint32_t* keys_out,
+                                                            uint32_t* vals_out, int pass) {
+  constexpr int kRTile = kRT * kRounds;
+  constexpr int kSub = kRTile / kRWaves;
+  __shared__ uint32_t base[kBins];
+  __shared__ uint32_t tstart[kBins];
+  __shared__ uint32_t wc[kRWaves][kBins];
+  __shared__ uint32_t wsum[kRWaves];
+  __shared__ uint32_t sk[kRTile], sv[kRTile];
+  // tile id: blockIdx (workgroups are dispatched in order per XCD, so the lowest unfinished
+  // tile only ever waits on finished ones), or (os_dyn) a counter ticket
+  __shared__ uint32_t s_id;
+  if (a.os_dyn) {
+    if (threadIdx.x == 0)
+      s_id = __hip_atomic_fetch_add((os_u32*)(a.os_hdr + pass), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+  }
+  const int64_t id = a.os_dyn ? static_cast<int64_t>(s_id) : static_cast<int64_t>(blockIdx.x);
+  const int64_t row = id / a.tiles;
+  const int tile = static_cast<int>(id - row * a.tiles);
+  const int shift = 8 * pass;
+  const bool last = pass == 3;
+  const int lane = lane_id();
+  const int w = threadIdx.x >> 6;
+  const int64_t tbase = static_cast<int64_t>(tile) * kRTile;
+  const int64_t wbase = tbase + static_cast<int64_t>(w) * kSub;
+  uint32_t k[kRounds], v[kRounds], r[kRounds];
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const int64_t i = wbase + j * 64 + lane;
+    const int64_t ic = i < a.n ? i : a.n - 1;
+    k[j] = load_key(a, keys_in, pass, row, ic);
+    if constexpr (VMODE == 0) v[j] = vals_in[row * a.n + ic];
+    else if constexpr (VMODE == 1) v[j] = static_cast<uint32_t>(i);
+    else v[j] = first_payload<PT, KIND>(a, row, ic);
+  }
+  // the row's digit totals (histogram kernel) -> exclusive scan over the digits
+  uint32_t gtot = 0;
+#pragma unroll
+  for (int c = 0; c < kGCopies; ++c) gtot += a.os_g[((row * kGCopies + c) * 4 + pass) * kBins + threadIdx.x];
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const bool ok = wbase + j * 64 + lane < a.n;
+    k[j] = ok ? k[j] : 0u;
+    v[j] = ok ? v[j] : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < kBins / 64; ++q) wc[w][lane + 64 * q] = 0;
+  uint32_t gb;
+  {
+    uint32_t inc = gtot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if (lane >= o) inc += u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+#pragma unroll
+    for (int q = 0; q < kRWaves; ++q)
+      if (q < w) off += wsum[q];
+    gb = off + inc - gtot;
+  }
+  // wave-local stable ranks (as radix_downsweep_kernel)
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const bool valid = wbase + j * 64 + lane < a.n;
+    const uint64_t active = __ballot(valid);
+    const uint32_t d = (k[j] >> shift) & 0xffu;
+    const uint64_t peers = match_digit(d, active);
+    const uint64_t pb = peers & below;
+    r[j] = wc[w][d] + static_cast<uint32_t>(__popcll(pb));
+    if (valid && pb == 0ull) wc[w][d] += static_cast<uint32_t>(__popcll(peers));
+  }
+  __syncthreads();
+  const int P = pass & 1;
+  {  // thread t owns digit t
+    const int t = threadIdx.x;
+    uint32_t o = 0;
+#pragma unroll
+    for (int q = 0; q < kRWaves; ++q) {
+      const uint32_t c = wc[q][t];
+      wc[q][t] = o;
+      o += c;
+    }
+    // publish this tile's count (ready-flagged) and add it to the group's word
+    const int ngroups = static_cast<int>(a.ngroups);
+    uint32_t* st = a.os_status + P * a.os_splane + row * a.tiles * kBins;
+    unsigned long long* ga = a.os_gacc + P * a.os_gplane + row * static_cast<int64_t>(ngroups) * kBins;
+    const int g = tile / kGroup;
+    os_put(st + static_cast<int64_t>(tile) * kBins + t, kReady | o);
+    os_add64(ga + static_cast<int64_t>(g) * kBins + t, (1ull << 32) | o);
+    uint32_t inc = o;
+#pragma unroll
+    for (int s2 = 1; s2 < 64; s2 <<= 1) {
+      const uint32_t u = __shfl_up(inc, s2, 64);
+      if (lane >= s2) inc += u;
+    }
+    // clear the planes the previous pass used (the next pass uses them), up to their extents
+    {
+      const int64_t nthr = static_cast<int64_t>(gridDim.x) * kRT;
+      const int64_t me = id * kRT + t;
+      uint32_t* so = a.os_status + (P ^ 1) * a.os_splane;
+      const int64_t se = a.os_hdr[4 + (P ^ 1)];
+      for (int64_t q = me; q < se; q += nthr) so[q] = 0u;
+      unsigned long long* go = a.os_gacc + (P ^ 1) * a.os_gplane;
+      const int64_t ge = a.os_hdr[6 + (P ^ 1)];
+      for (int64_t q = me; q < ge; q += nthr) go[q] = 0ull;
+    }
+    // tiles-before prefix: whole groups before this tile's group, then the group's earlier tiles
+    uint32_t pre = 0;
+    int spins = 0;
+    for (int g0 = 0; g0 < g; g0 += 16) {
+      unsigned long long gv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) gv[q] = os_get64(ga + static_cast<int64_t>(min(g0 + q, g - 1)) * kBins + t);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (g0 + q < g) {
+          while ((gv[q] >> 32) < static_cast<unsigned long long>(kGroup) && spins < kSpinLimit) {
+            ++spins;
+            gv[q] = os_get64(ga + static_cast<int64_t>(g0 + q) * kBins + t);
+          }
+          pre += static_cast<uint32_t>(gv[q]);
+        }
+      }
+    }
+    for (int j0 = g * kGroup; j0 < tile; j0 += 16) {
+      uint32_t sv2[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sv2[q] = os_get(st + static_cast<int64_t>(min(j0 + q, tile - 1)) * kBins + t);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        if (j0 + q < tile) {
+          while (!(sv2[q] & kReady) && spins < kSpinLimit) {
+            ++spins;
+            sv2[q] = os_get(st + static_cast<int64_t>(j0 + q) * kBins + t);
+          }
+          pre += sv2[q] & ~kReady;
+        }
+      }
+    }
+    if (spins >= kSpinLimit) a.os_hdr[8] = 1u;
+    base[t] = gb + pre;
+    // the last tile of the row: every tile of the row has consumed the digit totals
+    if (last && tile == a.tiles - 1) {
+#pragma unroll
+      for (int q = 0; q < kGCopies * 4; ++q) a.os_g[(row * kGCopies * 4 + q) * kBins + t] = 0u;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+#pragma unroll
+    for (int q = 0; q < kRWaves; ++q)
+      if (q < w) off += wsum[q];
+    tstart[t] = off + inc - o;
+  }
+  if (id == 0 && threadIdx.x == 0) {  // this pass's extents: the next pass clears them
+    a.os_hdr[4 + P] = static_cast<uint32_t>(a.rows * a.tiles * kBins);
+    a.os_hdr[6 + P] = static_cast<uint32_t>(a.rows * a.ngroups * kBins);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    if (wbase + j * 64 + lane < a.n) {
+      const uint32_t d = (k[j] >> shift) & 0xffu;
+      const uint32_t p = tstart[d] + wc[w][d] + r[j];
+      sk[p] = k[j];
+      sv[p] = v[j];
+    }
+  }
+  __syncthreads();
+  const int64_t tn64 = a.n - tbase;
+  const int tn = static_cast<int>(tn64 < kRTile ? tn64 : kRTile);
+  if (tn == kRTile) {
+    uint32_t kk[kRounds], vv[kRounds];
+    int32_t pb[kRounds];
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      kk[j] = sk[threadIdx.x + j * kRT];
+      vv[j] = sv[threadIdx.x + j * kRT];
+    }
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      const uint32_t d = (kk[j] >> shift) & 0xffu;
+      pb[j] = static_cast<int32_t>(base[d]) - static_cast<int32_t>(tstart[d]);
+    }
+#pragma unroll
+    for (int j = 0; j < kRounds; ++j) {
+      const int64_t pos = row * a.n + static_cast<int64_t>(pb[j]) + (threadIdx.x + j * kRT);
+      if (last) {
+        a.out_sorted[pos] = key2f_desc(kk[j]);
+        a.out_order[pos] = static_cast<int32_t>(vv[j]);
+      } else {
+        keys_out[pos] = kk[j];
+        vals_out[pos] = vv[j];
+      }
+    }
+    return;
+  }
+  for (int p = threadIdx.x; p < tn; p += kRT) {
+    const uint32_t key = sk[p];
+    const uint32_t d = (key >> shift) & 0xffu;
+    const int64_t pos = row * a.n + base[d] + (p - tstart[d]);
+    if (last) {
+      a.out_sorted[pos] = key2f_desc(key);
+      a.out_order[pos] = static_cast<int32_t>(sv[p]);
+    } else {
+      keys_out[pos] = key;
+      vals_out[pos] = sv[p];
+    }
+  }
+}
+
 // [n, C] row-major -> [C, n] (LDS-tiled 64 x 64 transpose; coalesced both ways)
 __global__ __launch_bounds__(kRT) void transpose_kernel(const float* in, int64_t n, int64_t c, int64_t ld_in,
                                                         float* out) {
@@ -451,11 +757,69 @@ int radix_passes(const RadixArgs& a, hipStream_t stream) {
   return static_cast<int>(hipGetLastError());
 }
 
+template <int R>
+int radix_onesweep(const RadixArgs& a, hipStream_t stream) {
+  // histogram: ~512 blocks over all rows, whole 4096-key rounds per block
+  const int64_t round = static_cast<int64_t>(kRT) * kHistKeys;
+  const int64_t want = std::max<int64_t>(1, 256 / a.rows);
+  int64_t per = (a.n + want - 1) / want;
+  per = std::max<int64_t>(round, (per + round - 1) / round * round);
+  const dim3 hgrid(static_cast<unsigned>((a.n + per - 1) / per), static_cast<unsigned>(a.rows));
+  hipLaunchKernelGGL(onesweep_hist_kernel, hgrid, dim3(kRT), 0, stream, a, per);
+  const dim3 grid(static_cast<unsigned>(a.rows * a.tiles));
+  const uint32_t* kin[4] = {nullptr, a.keys0, a.keys1, a.keys0};
+  const uint32_t* vin[4] = {nullptr, a.vals0, a.vals1, a.vals0};
+  uint32_t* kout[4] = {a.keys0, a.keys1, a.keys0, nullptr};
+  uint32_t* vout[4] = {a.vals0, a.vals1, a.vals0, nullptr};
+  for (int p = 0; p < 4; ++p) {
+#define TEA_PASS(...) \
+  hipLaunchKernelGGL((onesweep_pass_kernel<R, __VA_ARGS__>), grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p)
+    if (p > 0) {
+      TEA_PASS(0);
+    } else if (a.payload_kind == 0) {
+      TEA_PASS(1);
+    } else if (a.payload_kind == 1) {
+      switch (a.payload_dt) {
+        case DType::f32: TEA_PASS(2, float, 1); break;
+        case DType::i64: TEA_PASS(2, int64_t, 1); break;
+        case DType::i32: TEA_PASS(2, int32_t, 1); break;
+        case DType::u8: case DType::b8: TEA_PASS(2, uint8_t, 1); break;
+        default: return -2;
+      }
+    } else {
+      switch (a.payload_dt) {
+        case DType::i64: TEA_PASS(2, int64_t, 2); break;
+        case DType::i32: TEA_PASS(2, int32_t, 2); break;
+        default: return -2;
+      }
+    }
+#undef TEA_PASS
+  }
+  return static_cast<int>(hipGetLastError());
+}
+
 }  // namespace
+
+bool radix_onesweep_ok(int64_t rows, int64_t n) {
+  const int64_t tiles = radix_sort_tiles(rows, n);
+  return rows > 0 && n > 0 && tiles <= kOSMaxTiles && rows * tiles * kBins < (int64_t{1} << 31);
+}
+
+int64_t radix_onesweep_status_words(int64_t rows, int64_t n) { return rows * radix_sort_tiles(rows, n) * kBins; }
+
+int64_t radix_onesweep_group_words(int64_t rows, int64_t n) {
+  return rows * radix_sort_groups(radix_sort_tiles(rows, n)) * kBins;
+}
 
 int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
   if (a.n <= 0 || a.rows <= 0) return 0;
   if (a.tiles != radix_sort_tiles(a.rows, a.n)) return -2;  // workspace sized for another tiling
+  if (a.os_hdr != nullptr) {
+    if (!radix_onesweep_ok(a.rows, a.n) || a.os_splane < radix_onesweep_status_words(a.rows, a.n) ||
+        a.os_gplane < radix_onesweep_group_words(a.rows, a.n))
+      return -2;
+    return radix_sort_rounds(a.rows, a.n) == 16 ? radix_onesweep<16>(a, stream) : radix_onesweep<8>(a, stream);
+  }
   return radix_sort_rounds(a.rows, a.n) == 16 ? radix_passes<16>(a, stream) : radix_passes<8>(a, stream);
 }
 

@@ -475,9 +475,13 @@ int launch_need(const RowSumsArgs& a, bool vec, hipStream_t stream) {
     if (a.pend) {  // deferred: no combine launch; 8 x 16-B loads per operand in flight per thread
       static const int vpt = [] {
         const char* e = std::getenv("TORCHEVAL_AMD_K5B_PEND_VPT");
-        return (e != nullptr && std::atoi(e) == 4) ? 4 : 8;
+        const int v = e != nullptr ? std::atoi(e) : 8;
+        return v == 4 || v == 16 ? v : 8;
       }();
-      if (vpt == 8) {
+      if (vpt == 16) {
+        if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true, 16>), grid, dim3(kB), 0, stream, a, span);
+        else hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, false, 16>), grid, dim3(kB), 0, stream, a, span);
+      } else if (vpt == 8) {
         if (vec) hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, true, 8>), grid, dim3(kB), 0, stream, a, span);
         else hipLaunchKernelGGL((row_sums_grid_kernel<NEED, HAS_W, false, 8>), grid, dim3(kB), 0, stream, a, span);
       } else {

@@ -34,17 +34,21 @@ def _state(metric, name: str) -> torch.Tensor:
     return v if v is not None else getattr(metric, name)
 
 
-def _promote_lazy(metric, names, input: torch.Tensor) -> bool:
+def _promote_lazy(metric, names, input: torch.Tensor):
     """The reference's lazy shape promotion of 0-d states to [d] on the first 2-D update
-    (done here up front so the fused kernels can accumulate in place).  False when the states
-    and the batch disagree in shape (the ATen path then reproduces the reference's broadcast)."""
+    (done here up front so the fused kernels can accumulate in place).  Returns the states by
+    name (the promoted tensors themselves: under torch.compile a re-read of the instance dict
+    can see the pre-promotion value), or None when the states and the batch disagree in shape
+    (the ATen path then reproduces the reference's broadcast)."""
     d = input.shape[1] if input.ndim == 2 else 1
-    states = [_state(metric, n) for n in names]
-    if input.ndim == 2 and all(s.ndim == 0 for s in states):
-        for n, s in zip(names, states):
-            setattr(metric, n, torch.zeros(d, dtype=s.dtype, device=s.device) + s)
-        return True
-    return all(s.numel() == d and s.ndim == (1 if input.ndim == 2 else 0) for s in states)
+    states = {n: _state(metric, n) for n in names}
+    if input.ndim == 2 and all(s.ndim == 0 for s in states.values()):
+        for n, s in list(states.items()):
+            states[n] = torch.zeros(d, dtype=s.dtype, device=s.device) + s
+            setattr(metric, n, states[n])
+        return states
+    ok = all(s.numel() == d and s.ndim == (1 if input.ndim == 2 else 0) for s in states.values())
+    return states if ok else None
 
 
 def _cpu_update(metric, input: torch.Tensor, target: torch.Tensor, w: Optional[torch.Tensor], sums, scalars) -> bool:
@@ -54,12 +58,13 @@ def _cpu_update(metric, input: torch.Tensor, target: torch.Tensor, w: Optional[t
     n = input.numel()
     if n == 0 or n > _rs.HOST_MAX or _C is None or compiling():
         return False
-    if input.ndim == 2 and not _promote_lazy(metric, [s for s, _ in sums], input):
+    states = _promote_lazy(metric, [s for s, _ in sums], input) if input.ndim == 2 else None
+    if input.ndim == 2 and states is None:
         return False
     kw = [None, None, None, None]  # sse, st, stt, sw
     count = False
     for name, stat in sums:
-        kw[_CPU_SLOT[stat]] = _state(metric, name)
+        kw[_CPU_SLOT[stat]] = states[name] if states is not None else _state(metric, name)
     for name, stat in scalars:
         kw[_CPU_SLOT[stat]] = _state(metric, name)
         count = count or stat == _rs.COUNT
@@ -85,13 +90,16 @@ def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w
     if not all(_state(metric, n).dtype == torch.float32 and _state(metric, n).device == input.device for n in names):
         return False
     if input.is_cuda and input.ndim == 2:
-        if not _native(input, target, w) or not _promote_lazy(metric, [n for n, _ in sums], input):
+        if not _native(input, target, w):
+            return False
+        states = _promote_lazy(metric, [n for n, _ in sums], input)
+        if states is None:
             return False
         key = {_rs.WSSE: "sse", _rs.SSE: "sse", _rs.WT: "st", _rs.WTT: "stt", _rs.W: "sw", _rs.COUNT: "sw"}
         spec = {key[stat]: n for n, stat in list(sums) + list(scalars)}
         kw = {"sse": None, "st": None, "stt": None, "sw": None}
         for k, n in spec.items():
-            kw[k] = _state(metric, n)
+            kw[k] = states[n] if n in states else _state(metric, n)
         if getattr(metric, "_pend_states", ()) and not compiling():
             # deferred mode (metrics/_pending.py): the launch only adds FP64 partials to the
             # metric's pending slots; the states fold them in when read
@@ -111,7 +119,7 @@ def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w
         return True
     if not _rs.supported(input, target, w) or input.numel() == 0:
         return False
-    if not _promote_lazy(metric, [n for n, _ in sums], input):
+    if _promote_lazy(metric, [n for n, _ in sums], input) is None:
         return False
     rows = input.shape[1] if input.ndim == 2 else 1
     x2 = input.t() if input.ndim == 2 else input.reshape(1, -1)
