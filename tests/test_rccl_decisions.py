@@ -172,3 +172,12 @@ def test_default_policy_keeps_multi_rank_groups_on_torch_distributed(monkeypatch
     assert not rd.enabled(2) and not rd.enabled(8)
     monkeypatch.setenv("TORCHEVAL_AMD_DIRECT_RCCL", "0")
     assert not rd.enabled(1)
+
+
+def test_deterministic_flag_keeps_multi_rank_groups_rank_ordered(monkeypatch):
+    from torcheval_amd.config import flags
+    from torcheval_amd.parallel import rccl_direct as rd
+
+    monkeypatch.setenv("TORCHEVAL_AMD_DIRECT_RCCL", "1")
+    with flags(deterministic=True):
+        assert not rd.enabled(2) and not rd.enabled(8)

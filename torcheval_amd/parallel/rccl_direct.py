@@ -29,7 +29,8 @@ Policy (``TORCHEVAL_AMD_DIRECT_RCCL``): ``auto`` (the default) uses the direct c
 only for 1-rank groups (the forced multi-rank engine of the tests and benchmarks), because no
 multi-GPU run has validated the multi-rank bootstrap yet; multi-rank groups keep
 torch.distributed's collectives and the rank-ordered gather + ``seg_reduce`` path.  ``1`` opts
-every group in, ``0`` keeps every collective on torch.distributed.
+every group in (except under ``config.deterministic``, which keeps the rank-ordered float
+sums), ``0`` keeps every collective on torch.distributed.
 
 Agreement: with ``TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING=0`` (no teardown on a failure) a
 communicator can fail on one rank only (its watchdog fired, its peers' collectives completed).
@@ -61,10 +62,20 @@ _DEVICE_TYPES = ("cuda",)
 
 
 def enabled(ws: int = 1) -> bool:
-    """Whether a group of ``ws`` ranks uses the direct communicators (see the module docstring)."""
+    """Whether a group of ``ws`` ranks uses the direct communicators (see the module docstring).
+
+    ``torcheval_amd.config.deterministic`` keeps multi-rank groups on the rank-ordered gather +
+    ``seg_reduce`` path even when opted in: a direct plan all-reduces float sums in RCCL's
+    order, which can differ in the last bits from the reference's sequential ``merge_state``.
+    Like every collective setting, the flag must be the same on all ranks."""
     mode = os.environ.get("TORCHEVAL_AMD_DIRECT_RCCL", "auto")
     if mode == "0" or (mode != "1" and ws > 1):
         return False
+    if ws > 1:
+        from torcheval_amd.config import config
+
+        if config.deterministic:
+            return False
     from torcheval_amd.ops import native, native_loaded
 
     return native_loaded() and bool(native().rccl_available())
