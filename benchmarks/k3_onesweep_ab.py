@@ -1,7 +1,8 @@
-"""binary_auroc at N=1M (BASELINE config 3): wall time per call for the K3 variants - the
-onesweep sort (TORCHEVAL_AMD_K3_ONESWEEP) and tile_sums folded into tile_area
-(TORCHEVAL_AMD_K3_LB), each against its legacy form.  The variables are read once per process,
-so each mode runs in its own child process; one JSON line per mode."""
+"""binary_auroc at N=1M (BASELINE config 3): wall time per call, onesweep sort vs the legacy
+upsweep / downsweep sort (TORCHEVAL_AMD_K3_ONESWEEP=0).  The variable is read once per process,
+so each mode runs in its own child process; one JSON line per mode.  (Round 5 also measured a
+tile_sums fold into tile_area and counter-ticket tile ids - both slower and removed:
+profiles/k3_onesweep_r5.json.)"""
 import json
 import os
 import subprocess
@@ -32,21 +33,35 @@ for name, fn in (("binary_auroc", binary_auroc), ("binary_auprc", binary_auprc))
         reps.append(s.elapsed_time(e) / 50 * 1e3)
     reps.sort()
     res[name] = {"median_us": round(reps[3], 2), "min_us": round(reps[0], 2)}
+xm = torch.rand(100_000, 100, device=dev, generator=g)
+ym = torch.randint(0, 100, (100_000,), device=dev, generator=g)
+from torcheval_amd.metrics.functional import multiclass_auroc
+for _ in range(5):
+    multiclass_auroc(xm, ym, num_classes=100)
+reps = []
+for _ in range(7):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(10):
+        multiclass_auroc(xm, ym, num_classes=100)
+    e.record()
+    torch.cuda.synchronize()
+    reps.append(s.elapsed_time(e) / 10 * 1e3)
+reps.sort()
+res["multiclass_auroc_100k_x100"] = {"median_us": round(reps[3], 2), "min_us": round(reps[0], 2)}
 res["auroc_abs_err_vs_cpu"] = abs(float(binary_auroc(x, t).cpu()) - float(binary_auroc(x.cpu().double(), t.cpu())))
 res["auprc_abs_err_vs_cpu"] = abs(float(binary_auprc(x, t).cpu()) - float(binary_auprc(x.cpu().double(), t.cpu())))
 print(json.dumps(res))
 '''
 
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for mode, lb, dyn in (("1", "0", "0"), ("1", "1", "0"), ("0", "0", "0")):
-    env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, TORCHEVAL_AMD_K3_LB=lb, TORCHEVAL_AMD_K3_DYNID=dyn, REPO=repo)
+for mode in ("1", "0"):
+    env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, REPO=repo)
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     if out.returncode != 0:
         print(out.stdout[-2000:], out.stderr[-4000:])
         sys.exit(out.returncode)
     line = json.loads(out.stdout.strip().splitlines()[-1])
     line["onesweep"] = mode == "1"
-    line["tile_sums_folded"] = lb == "1"
-    line["tile_ids"] = "counter" if dyn == "1" else "blockIdx"
     line["n"] = int(os.environ.get("AUROC_N", "1000000"))
     print(json.dumps(line), flush=True)

@@ -120,15 +120,6 @@ void* scratch_workspace(const Tensor& like, hipStream_t stream, int64_t bytes, i
   return it->second.data_ptr();
 }
 
-// K3 look-back kernels: tile ids from a counter ticket (TORCHEVAL_AMD_K3_DYNID=1) instead of blockIdx
-bool k3_dynid() {
-  static const bool v = [] {
-    const char* e = std::getenv("TORCHEVAL_AMD_K3_DYNID");
-    return e != nullptr && e[0] == '1';
-  }();
-  return v;
-}
-
 void check_launch(int rc, const char* what) {
   TORCH_CHECK(rc == 0, "torcheval_amd._C: ", what, " launch failed (code ", rc, ")");
 }
@@ -433,17 +424,6 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
   }
   Tensor ws = at::empty({tea::auc_scan_workspace_bytes(rows, n)},
                         at::TensorOptions().dtype(at::kByte).device(sorted.device()));
-  // opt-in: measured slower at 1M (tile_area 20.8 us against 11.7 + 5.0 for tile_area +
-  // tile_sums: every block reads its prefix through agent-scope loads; profiles/k3_onesweep_r5.json)
-  static const bool lb = [] {
-    const char* e = std::getenv("TORCHEVAL_AMD_K3_LB");
-    return e != nullptr && e[0] == '1';
-  }();
-  if (lb && payload_kind != 0 && rows <= 4) {  // tile totals published inside tile_area (sortscan.hip)
-    const int64_t words = 16 + rows * tea::auc_scan_tiles(n);
-    a.lb_hdr = static_cast<uint32_t*>(zeroed_workspace(sorted, stream_for(sorted), words * 4, 13));
-    a.lb_dyn = k3_dynid() ? 1 : 0;
-  }
   check_launch(tea::launch_auc_scan(a, ws.data_ptr(), stream_for(sorted)), "auc_scan");
 }
 
@@ -1329,7 +1309,6 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
     a.os_splane = scap / 8;  // two u32 planes
     a.os_gacc = gws;
     a.os_gplane = gcap / 16;  // two u64 planes
-    a.os_dyn = k3_dynid() ? 1 : 0;
   }
   Tensor pl;
   if (payload.has_value() && payload_kind != 0) {

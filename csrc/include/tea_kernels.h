@@ -113,11 +113,6 @@ struct AucScanArgs {
   void* tstart = nullptr;
   void* tarea = nullptr;
   void* totals = nullptr;
-  // tile_sums folded into tile_area (payload sorts, <= 4 rows of <= 1536 tiles): zeroed,
-  // self-cleaning [16 + rows * ntiles] words: [0] call tag (advanced by finalize), [1] dynamic tile
-  // counter, [2] look-back timeout flag, [16 ..] per-tile tags.  Null: the tile_sums launch.
-  uint32_t* lb_hdr = nullptr;
-  int lb_dyn = 0;  // tile ids from a counter ticket instead of blockIdx
   // K3c curve emission (PR curves / recall at fixed precision)
   int32_t* tcnt = nullptr;    // [rows, ntiles] tie-group tails per tile
   int32_t* cstart = nullptr;  // [rows, ntiles] exclusive scan of tcnt
@@ -136,7 +131,6 @@ struct AucScanArgs {
 };
 int64_t auc_scan_workspace_bytes(int64_t rows, int64_t n);
 int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream);
-int64_t auc_scan_tiles(int64_t n);
 // K3c: workspace for the curve passes; count (tile sums + tie-group tails, per-row scan, G_r
 // into a.sizes), emit (the compact ascending curves; a.row_off from the host after reading
 // sizes) and the sync-free recall-at-fixed-precision chain (count + emit + search + finalize).
@@ -466,14 +460,13 @@ struct RadixArgs {
   // onesweep mode (radix_onesweep_ok): one histogram launch for all four digits, then four
   // passes that each rank, look back and scatter in ONE launch (no upsweeps).  Self-cleaning,
   // zero-initialised workspaces:
-  uint32_t* os_hdr = nullptr;     // [16]: dynamic tile counters [4], dirty extents of the status /
-                                  // group planes [2] + [2], look-back timeout flag
+  uint32_t* os_hdr = nullptr;     // [16]: [4..7] dirty extents of the status / group planes,
+                                  // [8] look-back timeout flag
   uint32_t* os_g = nullptr;       // [rows, 8 copies, 4, 256] digit totals (hist kernel; cleared by pass 3)
   uint32_t* os_status = nullptr;  // 2 planes of [rows * tiles, 256] ready-flagged tile counts
   int64_t os_splane = 0;          // words per status plane
   unsigned long long* os_gacc = nullptr;  // 2 planes of [rows * ngroups, 256] (arrivals << 32 | sum)
   int64_t os_gplane = 0;          // words per group plane
-  int os_dyn = 0;                 // tile ids from a counter ticket instead of blockIdx
 };
 bool radix_onesweep_ok(int64_t rows, int64_t n);  // the tiling the onesweep passes take
 int64_t radix_onesweep_status_words(int64_t rows, int64_t n);

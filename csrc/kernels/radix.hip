@@ -350,8 +350,8 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
 // ranks its tile exactly as the downsweep above and gets its tiles-before prefix in the same
 // launch (decoupled look-back, Merrill & Garland / Adinets & Merrill "onesweep"), so the four
 // upsweep launches and their second read of the keys are gone.
-//   * tiles take dynamic ids from a counter (launch order), so every tile a block waits on has
-//     started: no deadlock whatever the residency;
+//   * a tile waits only on lower-numbered tiles of its row, and workgroups are dispatched in
+//     blockIdx order per XCD, so the lowest unfinished tile never waits on an undispatched one;
 //   * look-back without chained prefixes: each tile publishes its per-digit count (the data is
 //     the flag: bit 31 = ready) and adds it, with an arrival count, into its group's word (32
 //     tiles per group); a tile's prefix is the sum of the complete groups before its own plus
@@ -364,8 +364,8 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
 //     the plane the previous pass used, up to the extent recorded for it (so a later sort of
 //     another shape never reads stale flags); the last tile of each row in pass 3 clears the
 //     row's digit totals once every tile of the row has consumed them (its look-back saw all
-//     of them publish, and each publishes only after its digit-start scan); the histogram
-//     kernel resets the tile counters.  Every spin is bounded (a timeout sets hdr[8]).
+//     of them publish, and each publishes only after its digit-start scan).  Every spin is
+//     bounded (a timeout sets hdr[8]).
 constexpr int kOSMaxTiles = 1024;
 constexpr uint32_t kReady = 0x80000000u;
 constexpr int kSpinLimit = 1 << 22;
@@ -426,7 +426,6 @@ __global__ __launch_bounds__(kRT) void onesweep_hist_kernel(RadixArgs a, int64_t
     for (int q = 0; q < kC; ++q) v += h[p][q][threadIdx.x];
     if (v) atomicAdd(&a.os_g[((row * kGCopies + blockIdx.x % kGCopies) * 4 + p) * kBins + threadIdx.x], v);
   }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 4) a.os_hdr[threadIdx.x] = 0u;  // tile counters
 }
 
 // one pass: load + rank as radix_downsweep_kernel, then publish / look back, then scatter
@@ -441,15 +440,11 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   __shared__ uint32_t wc[kRWaves][kBins];
   __shared__ uint32_t wsum[kRWaves];
   __shared__ uint32_t sk[kRTile], sv[kRTile];
-  // tile id: blockIdx (workgroups are dispatched in order per XCD, so the lowest unfinished
-  // tile only ever waits on finished ones), or (os_dyn) a counter ticket
-  __shared__ uint32_t s_id;
-  if (a.os_dyn) {
-    if (threadIdx.x == 0)
-      s_id = __hip_atomic_fetch_add((os_u32*)(a.os_hdr + pass), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-  }
-  const int64_t id = a.os_dyn ? static_cast<int64_t>(s_id) : static_cast<int64_t>(blockIdx.x);
+  // tile id = blockIdx: workgroups are dispatched in order per XCD, so the lowest unfinished
+  // tile only ever waits on finished ones.  (Ids from a counter ticket, the textbook guard,
+  // cost 512 serialised same-address atomics per launch: 18.9 vs 13.2 us per pass at 1M,
+  // profiles/k3_onesweep_r5.json.)
+  const int64_t id = blockIdx.x;
   const int64_t row = id / a.tiles;
   const int tile = static_cast<int>(id - row * a.tiles);
   const int shift = 8 * pass;

@@ -443,330 +443,15 @@ __global__ __launch_bounds__(kT) void tile_area_kernel(AucScanArgs a) {
     reinterpret_cast<D2*>(a.tarea)[static_cast<int64_t>(r) * ntiles + blockIdx.x] = area;
 }
 
-// ---------------------------------------------------------------- tile_sums folded in (LB)
-// tile_area_lb_kernel: the tile totals are no longer a launch of their own.  Each block takes a
-// dynamic tile id (launch order), sums its tile, publishes the totals (two write-through FP64
-// stores, drained, then a tag word = this call's tag), and forms its tiles-before prefix from
-// the published totals of the tiles before it (polled until tagged; fixed per-thread
-// assignment + block scan, so the sum order never depends on timing: deterministic).  Only
-// BACKWARD waits exist, so no residency assumption:
-//   * a tie group entering from earlier tiles is resolved as before (window / binary search +
-//     the prefix of an earlier tile);
-//   * a tie group leaving the tile and reaching >= kWin samples past its end is NOT credited
-//     here (its TP / FP at the tail would need later tiles' totals): the tile holding the
-//     group's tail credits the skipped part at once from prefix differences,
-//       roc += (FP(S-) - FP(head-)) * (TP(head-) + TP(tail)) / 2
-//       pr  += (TP(S-) - TP(head-)) * TP(tail) / (TP(tail) + FP(tail)),
-//     where [head, S) are the samples of the group in the skipping tiles.
-// The tag / counter header lives in a zeroed workspace: finalize advances the tag and resets
-// the counter for the next call.
-typedef __attribute__((address_space(1))) unsigned lb_u32;
-constexpr int kLBSpin = 1 << 22;
-
-__device__ __forceinline__ void lb_put(uint32_t* p, uint32_t v) {
-  __hip_atomic_store((lb_u32*)(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t lb_get(const uint32_t* p) {
-  return __hip_atomic_load((lb_u32*)(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// init + the published totals of tiles [0, upto) of row r (block-cooperative)
-__device__ D2 lb_prefix(const AucScanArgs& a, int r, int upto, int ntiles, uint32_t tag, D2* lds) {
-  const D2* ts = reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles;
-  const uint32_t* tags = a.lb_hdr + 16 + static_cast<int64_t>(r) * ntiles;
-  uint32_t tg[kFusePer];
-#pragma unroll
-  for (int u = 0; u < kFusePer; ++u) {
-    const int t = u * kT + static_cast<int>(threadIdx.x);
-    tg[u] = lb_get(tags + (t < upto ? t : 0));
-  }
-  int spins = 0;
-  double pa = 0.0, pb = 0.0;
-#pragma unroll
-  for (int u = 0; u < kFusePer; ++u) {
-    const int t = u * kT + static_cast<int>(threadIdx.x);
-    if (t < upto) {
-      while (tg[u] != tag && spins < kLBSpin) {
-        ++spins;
-        tg[u] = lb_get(tags + t);
-      }
-    }
-  }
-  double qa[kFusePer], qb[kFusePer];
-#pragma unroll
-  for (int u = 0; u < kFusePer; ++u) {
-    const int t = u * kT + static_cast<int>(threadIdx.x);
-    const int tc = t < upto ? t : 0;
-    qa[u] = wt_load(&ts[tc].x);
-    qb[u] = wt_load(&ts[tc].y);
-  }
-#pragma unroll
-  for (int u = 0; u < kFusePer; ++u) {
-    const bool ok = u * kT + static_cast<int>(threadIdx.x) < upto;
-    pa += ok ? qa[u] : 0.0;
-    pb += ok ? qb[u] : 0.0;
-  }
-  if (spins >= kLBSpin) a.lb_hdr[2] = 1u;
-  D2 tot;
-  block_excl_scan(D2{pa, pb}, lds, tot);
-  if (a.init) tot = d2add(tot, D2{a.init[2 * r], a.init[2 * r + 1]});
-  return tot;
-}
-
-template <typename K>
-__global__ __launch_bounds__(kT) void tile_area_lb_kernel(AucScanArgs a, int ntiles) {
-  // tile id: blockIdx (in-order dispatch per XCD: the lowest unfinished tile only waits on
-  // finished ones), or (lb_dyn) a counter ticket
-  __shared__ uint32_t s_id;
-  if (a.lb_dyn) {
-    if (threadIdx.x == 0)
-      s_id = __hip_atomic_fetch_add((lb_u32*)(a.lb_hdr + 1), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-  }
-  const uint32_t id = a.lb_dyn ? s_id : blockIdx.x;
-  const int r = static_cast<int>(id / static_cast<uint32_t>(ntiles));
-  const int tile = static_cast<int>(id - static_cast<uint32_t>(r) * ntiles);
-  const uint32_t tag = a.lb_hdr[0] + 1u;
-  const int64_t base = static_cast<int64_t>(tile) * kTile;
-  const int tile_n = static_cast<int>(min(static_cast<int64_t>(kTile), a.n - base));
-  const float2* ab = nullptr;
-
-  __shared__ double s_tpx[kTile];
-  __shared__ double s_fpi[kTile];
-  __shared__ D2 lds[kT / 64];
-  __shared__ double s_bound[5];  // TP / FP before the entering group (0, 3); TP, FP at the leaving group's tail (1, 2)
-  __shared__ int s_flags[2];
-  __shared__ int s_fb[2];
-  __shared__ int s_hmax[kT / 64], s_tmin[kT / 64];
-  __shared__ int64_t s_pos;
-
-  const int j0 = threadIdx.x * kPer;
-  const int64_t i0 = base + j0;
-  K key[kPer];
-  float2 v[kPer];
-  const int64_t ilast = base + tile_n - 1;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int64_t i = i0 + k < ilast ? i0 + k : ilast;
-    key[k] = key_at<K>(a, r, i);
-    v[k] = load_ab<true>(a, ab, r, i);
-  }
-  const bool live = j0 < tile_n;
-  K pk0 = key_at<K>(a, r, i0 > 0 ? (i0 - 1 < ilast ? i0 - 1 : ilast) : 0);
-  K nk_last = key_at<K>(a, r, i0 + kPer < a.n ? i0 + kPer : a.n - 1);
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const bool ok = j0 + k < tile_n;
-    key[k] = ok ? key[k] : K(0);
-    v[k] = ok ? v[k] : make_float2(0.f, 0.f);
-  }
-  pk0 = (live && i0 > 0) ? pk0 : K(0);
-  nk_last = (live && i0 + kPer < a.n) ? nk_last : K(0);
-  double la = 0.0, lb = 0.0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    la += v[k].x;
-    lb += v[k].y;
-  }
-  if (threadIdx.x == 0) {
-    s_flags[0] = (base > 0 && key[0] == pk0) ? 1 : 0;
-    s_bound[0] = s_bound[1] = s_bound[2] = s_bound[3] = 0.0;
-  }
-  if (j0 + kPer == tile_n) s_flags[1] = (base + tile_n < a.n && key[kPer - 1] == nk_last) ? 1 : 0;
-  if (j0 < tile_n && tile_n < j0 + kPer) s_flags[1] = 0;
-  D2 tot;
-  const D2 ex = block_excl_scan(D2{la, lb}, lds, tot);
-  if (threadIdx.x == 0) {  // publish: the totals, drained, then the tag
-    D2* ts = reinterpret_cast<D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles + tile;
-    wt_store(&ts->x, tot.x);
-    wt_store(&ts->y, tot.y);
-    wt_drain();
-    lb_put(a.lb_hdr + 16 + static_cast<int64_t>(r) * ntiles + tile, tag);
-  }
-  const D2 t0 = lb_prefix(a, r, tile, ntiles, tag, lds);
-
-  bool headf[kPer], tailf[kPer];
-  int my_head = -1, my_tail = kTile;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int j = j0 + k;
-    const int64_t i = base + j;
-    bool h = false, tl = false;
-    if (j < tile_n) {
-      const K pk = (k > 0) ? key[k - 1] : pk0;
-      const K nk = (k + 1 < kPer) ? key[k + 1] : nk_last;
-      h = (i == 0) || !(pk == key[k]);
-      tl = (i == a.n - 1) || !(nk == key[k]);
-    }
-    headf[k] = h;
-    tailf[k] = tl;
-    if (h) my_head = j;
-  }
-#pragma unroll
-  for (int k = kPer - 1; k >= 0; --k)
-    if (tailf[k]) my_tail = j0 + k;
-  {
-    double ca = t0.x + ex.x, cb = t0.y + ex.y;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int j = j0 + k;
-      s_tpx[j] = ca;
-      ca += v[k].x;
-      cb += v[k].y;
-      s_fpi[j] = cb;
-    }
-  }
-  const int w = threadIdx.x >> 6;
-  const int hin = wave_incl_max(my_head);
-  const int tin = wave_incl_min_rev(my_tail);
-  if (lane_id() == 63) s_hmax[w] = hin;
-  if (lane_id() == 0) s_tmin[w] = tin;
-  __syncthreads();
-  int hmax_before = -1, tmin_after = kTile;
-  for (int k = 0; k < w; ++k) hmax_before = max(hmax_before, s_hmax[k]);
-  for (int k = w + 1; k < kT / 64; ++k) tmin_after = min(tmin_after, s_tmin[k]);
-  int h_excl = __shfl_up(hin, 1, 64);
-  if (lane_id() == 0) h_excl = -1;
-  h_excl = max(h_excl, hmax_before);
-  int t_excl = __shfl_down(tin, 1, 64);
-  if (lane_id() == 63) t_excl = kTile;
-  t_excl = min(t_excl, tmin_after);
-
-  constexpr int kWin = 64;
-  if (threadIdx.x == 0) s_fb[0] = s_fb[1] = 0;
-  __syncthreads();
-  if (s_flags[0] && w == 0) {
-    const K v0 = __shfl(key[0], 0, 64);
-    const int64_t i = base - kWin + lane_id();
-    const K kk = key_at<K>(a, r, i);
-    const float2 ab_i = load_ab<true>(a, ab, r, i);
-    const bool eq = kk == v0;
-    const unsigned long long m = __ballot(eq);
-    const double sa = wave_sum(eq ? static_cast<double>(ab_i.x) : 0.0);
-    const double sb = wave_sum(eq ? static_cast<double>(ab_i.y) : 0.0);
-    if (lane_id() == 0) {
-      if (m & 1ull) {
-        s_fb[0] = 1;
-      } else {
-        s_bound[0] = t0.x - sa;
-        s_bound[3] = t0.y - sb;
-        s_pos = base - __popcll(m);  // the group's head
-      }
-    }
-  }
-  if (s_flags[1] && w == 1) {
-    const K v1 = key_at<K>(a, r, base + tile_n - 1);
-    const int64_t i = base + tile_n + lane_id();
-    const bool valid = i < a.n;
-    const K kk = key_at<K>(a, r, valid ? i : a.n - 1);
-    const float2 ab_i = load_ab<true>(a, ab, r, valid ? i : a.n - 1);
-    const bool eq = valid && kk == v1;
-    const unsigned long long m = __ballot(eq);
-    const double sa = wave_sum(eq ? static_cast<double>(ab_i.x) : 0.0);
-    const double sb = wave_sum(eq ? static_cast<double>(ab_i.y) : 0.0);
-    if (lane_id() == 0) {
-      if (m >> 63) s_fb[1] = 1;  // reaches >= kWin past the tile: its tail tile credits it
-      else {
-        s_bound[1] = t0.x + tot.x + sa;
-        s_bound[2] = t0.y + tot.y + sb;
-      }
-    }
-  }
-  __syncthreads();
-  if (s_fb[0]) {
-    if (threadIdx.x == 0) s_pos = first_equal<K>(a, r, 0, base, key_at<K>(a, r, base));
-    __syncthreads();
-    const int64_t hpos = s_pos;
-    const int64_t ht = hpos / kTile;
-    const D2 part = block_range_sum<true>(a, ab, r, ht * kTile, hpos - 1, lds);
-    const D2 hs = lb_prefix(a, r, static_cast<int>(ht), ntiles, tag, lds);
-    if (threadIdx.x == 0) {
-      s_bound[0] = hs.x + part.x;
-      s_bound[3] = hs.y + part.y;
-    }
-    __syncthreads();
-  }
-
-  int ntail[kPer];
-  {
-    int nt = t_excl;
-#pragma unroll
-    for (int k = kPer - 1; k >= 0; --k) {
-      if (tailf[k]) nt = j0 + k;
-      ntail[k] = nt;
-    }
-  }
-  const double tile_tp_end = t0.x + tot.x;
-  const bool skip_leaving = s_fb[1] != 0;
-  double roc = 0.0, pr = 0.0;
-  int cur_head = h_excl;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int j = j0 + k;
-    if (headf[k]) cur_head = j;
-    if (j < tile_n) {
-      const int tail = ntail[k];
-      if (tail >= tile_n && skip_leaving) continue;  // credited by the group's tail tile
-      const double tps = (cur_head >= 0) ? s_tpx[cur_head] : s_bound[0];
-      double tpe, fpe;
-      if (tail < tile_n) {
-        tpe = (tail + 1 < tile_n) ? s_tpx[tail + 1] : tile_tp_end;
-        fpe = s_fpi[tail];
-      } else {
-        tpe = s_bound[1];
-        fpe = s_bound[2];
-      }
-      roc += static_cast<double>(v[k].y) * 0.5 * (tps + tpe);
-      const double den = tpe + fpe;
-      if (v[k].x != 0.f && den != 0.0) pr += static_cast<double>(v[k].x) * (tpe / den);
-    }
-  }
-  // the tail tile of an entering group credits the group's samples that earlier tiles skipped
-  if (threadIdx.x == 0 && s_flags[0]) {
-    int jt = kTile;
-    for (int q = 0; q < kT / 64; ++q) jt = min(jt, s_tmin[q]);
-    if (jt < tile_n) {
-      const int64_t hpos = s_pos;
-      // tile - 1 skipped iff the group reached >= kWin - 1 samples into this tile
-      const bool prev_skipped = jt >= kWin - 1;
-      const int64_t S = prev_skipped ? base : base - kTile;
-      if (hpos < S) {
-        double tps_x = t0.x, tps_y = t0.y;  // prefix before S
-        if (!prev_skipped) {
-          const D2* ts = reinterpret_cast<const D2*>(a.tsum) + static_cast<int64_t>(r) * ntiles + (tile - 1);
-          tps_x -= wt_load(&ts->x);  // tile - 1's totals: published before this block's prefix completed
-          tps_y -= wt_load(&ts->y);
-        }
-        const double sa = tps_x - s_bound[0], sb = tps_y - s_bound[3];
-        const double tpe = (jt + 1 < tile_n) ? s_tpx[jt + 1] : tile_tp_end;
-        const double fpe = s_fpi[jt];
-        roc += sb * 0.5 * (s_bound[0] + tpe);
-        const double den = tpe + fpe;
-        if (sa != 0.0 && den != 0.0) pr += sa * (tpe / den);
-      }
-    }
-  }
-  D2 area;
-  block_excl_scan(D2{roc, pr}, lds, area);
-  if (threadIdx.x == 0)
-    reinterpret_cast<D2*>(a.tarea)[static_cast<int64_t>(r) * ntiles + tile] = area;
-}
-
 // one block per row.  (A "last block finalises" fold inside tile_area was measured: the
 // agent-scope release / acquire fences it needs per block - the XCDs' L2s are not coherent -
 // doubled tile_area, 16 -> 34 us at 1M samples; a separate launch costs ~4 us.)
 __global__ __launch_bounds__(kT) void finalize_kernel(AucScanArgs a, int ntiles, int fused) {
   __shared__ D2 lds[kT / 64];
   finalize_row(a, blockIdx.x, ntiles, fused != 0, lds);
-  if (a.lb_hdr != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {  // the next call's tag, counter
-    a.lb_hdr[0] += 1u;
-    a.lb_hdr[1] = 0u;
-  }
 }
 
 }  // namespace
-
-int64_t auc_scan_tiles(int64_t n) { return (n + kTile - 1) / kTile; }
 
 int64_t auc_scan_workspace_bytes(int64_t rows, int64_t n) {
   const int64_t ntiles = (n + kTile - 1) / kTile;
@@ -792,14 +477,6 @@ int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream) {
   // block reduction before the scan), which 100 rows x 98 tiles paid for with +12 us per call
   const bool direct = a.payload_kind != 0, fused = ntiles <= kFuseTiles && a.rows <= 4;
   const bool f64 = a.key_dt == DType::f64;
-  if (a.lb_hdr != nullptr && direct && fused) {  // tile_sums folded into tile_area (2 launches)
-    const dim3 g1(static_cast<unsigned>(ntiles * a.rows));
-    if (f64) hipLaunchKernelGGL(tile_area_lb_kernel<double>, g1, dim3(kT), 0, stream, a, ntiles);
-    else hipLaunchKernelGGL(tile_area_lb_kernel<float>, g1, dim3(kT), 0, stream, a, ntiles);
-    hipLaunchKernelGGL(finalize_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles, 1);
-    return static_cast<int>(hipGetLastError());
-  }
-  a.lb_hdr = nullptr;
   if (direct) hipLaunchKernelGGL(tile_sums_kernel<true>, grid, dim3(kT), 0, stream, a);
   else hipLaunchKernelGGL(tile_sums_kernel<false>, grid, dim3(kT), 0, stream, a);
   if (!fused) hipLaunchKernelGGL(tile_scan_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles);

@@ -87,9 +87,9 @@ def test_binary_auroc_1m_matches_cpu_across_repeats():
 @pytest.mark.parametrize("group_len,offset", [(40, 1000), (64, 990), (100, 1000), (1100, 1000), (3000, 500),
                                               (2048, 1024), (70, 1023), (63, 961), (5000, 0)])
 def test_tie_groups_across_tiles(group_len, offset):
-    """Long tie groups straddling 1024-sample tiles at every offset class: the tile holding a
-    group's tail credits the parts earlier tiles skipped (tile_area_lb_kernel); weighted inputs
-    take the legacy scan, so both are held to the CPU oracle."""
+    """Long tie groups straddling 1024-sample tiles at every offset class (short groups resolved
+    from the edge window, long ones by the binary search), weighted and unweighted, one and
+    three rows, against the CPU oracle."""
     from torcheval_amd.metrics.functional import binary_auprc, binary_auroc
 
     g = torch.Generator().manual_seed(group_len + offset)

@@ -15,7 +15,13 @@ vectors, confusion matrices, covariance sums) keeps them as views into ONE devic
 
 ``sync_and_compute(MulticlassAccuracy)`` is therefore one collective on the live buffer (no
 packing ``cat``, no per-state loops: the plan is cached on the buffer) plus, at ws > 1, one
-reduction launch.  Update kernels keep writing the same views (the K1 fast path passes
+reduction launch.
+
+Groups that take the engine's own RCCL communicators (``parallel/rccl_direct.py``: 1-rank
+groups by default, multi-rank groups only when opted in with ``TORCHEVAL_AMD_DIRECT_RCCL=1``)
+sync with ONE grouped out-of-place all-reduce plan instead; its float sums follow RCCL's
+reduction order, so for multi-rank groups the rank-ordered bit-identical guarantee above holds
+on the torch.distributed path, which ``config.deterministic`` always selects.  Update kernels keep writing the same views (the K1 fast path passes
 ``num_correct`` / ``num_total`` pointers into the buffer).
 
 The buffer is built lazily (first sync or reset of an eligible metric).  Any rebinding of a
