@@ -754,11 +754,9 @@ int radix_passes(const RadixArgs& a, hipStream_t stream) {
 
 template <int R>
 int radix_onesweep(const RadixArgs& a, hipStream_t stream) {
-  // histogram: ~512 blocks over all rows, whole 4096-key rounds per block
-  const int64_t round = static_cast<int64_t>(kRT) * kHistKeys;
-  const int64_t want = std::max<int64_t>(1, 256 / a.rows);
-  int64_t per = (a.n + want - 1) / want;
-  per = std::max<int64_t>(round, (per + round - 1) / round * round);
+  // histogram: one 4096-key round per block (245 blocks at 1M keys; many-row sorts get their
+  // parallelism from the rows: 2 blocks per 100k-key row ran 13 serial rounds each)
+  const int64_t per = static_cast<int64_t>(kRT) * kHistKeys;
   const dim3 hgrid(static_cast<unsigned>((a.n + per - 1) / per), static_cast<unsigned>(a.rows));
   hipLaunchKernelGGL(onesweep_hist_kernel, hgrid, dim3(kRT), 0, stream, a, per);
   const dim3 grid(static_cast<unsigned>(a.rows * a.tiles));
@@ -796,8 +794,10 @@ int radix_onesweep(const RadixArgs& a, hipStream_t stream) {
 }  // namespace
 
 bool radix_onesweep_ok(int64_t rows, int64_t n) {
+  // few long rows only: at 100 rows x 100k the legacy sort stays ahead (361 vs 370 us for
+  // multiclass_auroc, profiles/k3_onesweep_r5.json): short rows leave the look-back little to save
   const int64_t tiles = radix_sort_tiles(rows, n);
-  return rows > 0 && n > 0 && tiles <= kOSMaxTiles && rows * tiles * kBins < (int64_t{1} << 31);
+  return rows > 0 && rows <= 8 && n > 0 && tiles <= kOSMaxTiles && rows * tiles * kBins < (int64_t{1} << 31);
 }
 
 int64_t radix_onesweep_status_words(int64_t rows, int64_t n) { return rows * radix_sort_tiles(rows, n) * kBins; }
