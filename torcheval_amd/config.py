@@ -15,6 +15,33 @@
 =============================  ========================================================
 
 Use ``torcheval_amd.config.flags(validate=True)`` as a context manager for a scoped change.
+``deterministic`` also keeps multi-rank syncs on the rank-ordered gather + ``seg_reduce`` path
+(``parallel/rccl_direct.py``).
+
+Engine policies (read once per process; not flags):
+
+=============================================  ==============================================
+``TORCHEVAL_AMD_DIRECT_RCCL``                  ``auto`` (default): the engine's own RCCL
+                                               communicators for 1-rank groups only; ``1``:
+                                               every group; ``0``: always torch.distributed
+``TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING``    1 (default): a failed direct communicator ends
+                                               the process (c10d's default); 0: the next sync
+                                               votes group-wide and rebuilds
+``TORCHEVAL_AMD_ASYNC_DIRECT_RCCL``            1: async syncs ride the direct path on a side
+                                               stream (default: torch.distributed async)
+``TORCHEVAL_AMD_RCCL_WATCHDOG``                0: no completion watchdog (A/B only)
+``TORCHEVAL_AMD_HOST_POLL_US``                 bound of the pinned-memory host spin of device
+                                               flag reads (``ops/hostread.py``)
+=============================================  ==============================================
+
+Kernel A/B knobs (benchmarks only; defaults are the measured winners, ``profiles/README.md``):
+``TORCHEVAL_AMD_K1_MICRO`` / ``_K1_WPB`` (K1 micro kernel, waves per workgroup),
+``_K3_ONESWEEP`` (0: the upsweep / downsweep sort), ``_K5_V2`` / ``_K5_CG`` / ``_K5_MAXR`` /
+``_K5_BLOCKS`` / ``_K5_PIPE`` / ``_K5_AB_SKIP_FOLD`` (K5 geometry; read per call only with
+``_AB_DYNAMIC``), ``_K5B_MODE`` / ``_K5B_GRID`` / ``_K5B_PEND_VPT`` (K5b launch shape),
+``_K8_MODE`` / ``_K8_SPLIT`` / ``_K8_EXACT`` / ``_FID_STAGE_ROWS`` (FID covariance),
+``_PPL_U2`` / ``_PPL_MAXGRID`` (K7), ``_SYMEIG_COOP`` (K9b cooperative launch),
+``_MAX_BLOCKS`` (grid cap), ``_ARCH`` (build target, default gfx950).
 """
 
 import contextlib
