@@ -48,8 +48,11 @@ def _keys(rows: int, n: int, seed: int, levels: int) -> torch.Tensor:
 
 def test_shape_sequence_keeps_the_workspace_clean():
     g = torch.Generator().manual_seed(5)
+    # (1, 2_097_152) is exactly 1024 tiles (the onesweep limit), one key more takes the legacy
+    # sort; (8, 500_000) crosses to 16-round tiles; 9 and 100 rows take the legacy sort
     shapes = [(1, 1_000_000), (1, 3), (3, 70_000), (1, 2_100_000), (1, 4096), (100, 1000), (1, 1_000_000),
-              (2, 5_000_000 // 2 + 17), (1, 2049), (8, 131_072), (1, 999_999), (1, 1)]
+              (2, 5_000_000 // 2 + 17), (1, 2049), (8, 131_072), (1, 999_999), (1, 1), (1, 2_097_152),
+              (1, 2_097_153), (8, 500_000), (9, 50_000)]
     for step, (rows, n) in enumerate(shapes * 2):
         levels = int(torch.randint(0, 3, (1,), generator=g)) * 7
         _check(_keys(rows, n, 100 + step, levels))
