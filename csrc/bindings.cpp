@@ -1338,6 +1338,21 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
 }
 
 
+// test hook: the onesweep look-back timeout word of `x`'s device / stream (0 = every spin of every
+// sort on it completed), optionally cleared; one device-to-host read
+int64_t sort_desc_timeouts(const Tensor& x, bool clear) {
+  check_gpu(x, "x");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  hipStream_t st = stream_for(x);
+  auto* hdr = static_cast<uint32_t*>(zeroed_workspace(x, st, 16 * 4, 10));
+  uint32_t v = 0;
+  TORCH_CHECK(hipMemcpyAsync(&v, hdr + 8, 4, hipMemcpyDeviceToHost, st) == hipSuccess &&
+                  hipStreamSynchronize(st) == hipSuccess,
+              "sort_desc_timeouts: read failed");
+  if (clear && v != 0) TORCH_CHECK(hipMemsetAsync(hdr + 8, 0, 4, st) == hipSuccess, "sort_desc_timeouts: clear failed");
+  return v;
+}
+
 // binned AUROC / AUPRC from [T, rows] float32 counts in one launch
 void binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tensor>& fn,
                      const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc,
@@ -1538,6 +1553,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("num_correct"), py::arg("num_total") = py::none(), py::arg("total") = 0.0);
   m.def("transpose_f32", &transpose_f32, "LDS-tiled [n, c] -> [c, n] float32 transpose", py::arg("x"),
         py::arg("out"));
+  m.def("sort_desc_timeouts", &sort_desc_timeouts, "test hook: onesweep look-back timeout word (0 = none)",
+        pybind11::arg("x"), pybind11::arg("clear") = true);
   m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
         py::arg("x"), py::arg("out_sorted"), py::arg("out_order"), py::arg("payload") = py::none(),
         py::arg("payload_kind") = 0);

@@ -53,9 +53,13 @@ def test_shape_sequence_keeps_the_workspace_clean():
     shapes = [(1, 1_000_000), (1, 3), (3, 70_000), (1, 2_100_000), (1, 4096), (100, 1000), (1, 1_000_000),
               (2, 5_000_000 // 2 + 17), (1, 2049), (8, 131_072), (1, 999_999), (1, 1), (1, 2_097_152),
               (1, 2_097_153), (8, 500_000), (9, 50_000)]
+    from torcheval_amd.ops import native
+
     for step, (rows, n) in enumerate(shapes * 2):
         levels = int(torch.randint(0, 3, (1,), generator=g)) * 7
         _check(_keys(rows, n, 100 + step, levels))
+    # no look-back spin of any of these sorts hit its bound
+    assert native().sort_desc_timeouts(torch.empty(1, device=DEV)) == 0
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.int64, torch.uint8, torch.bool])
