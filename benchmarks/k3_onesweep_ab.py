@@ -55,13 +55,14 @@ print(json.dumps(res))
 '''
 
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for mode in ("1", "0"):
-    env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, REPO=repo)
+for mode, rounds in (("1", ""), ("1", "16"), ("0", ""), ("0", "16")):
+    env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, TORCHEVAL_AMD_K3_ROUNDS=rounds, REPO=repo)
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     if out.returncode != 0:
         print(out.stdout[-2000:], out.stderr[-4000:])
         sys.exit(out.returncode)
     line = json.loads(out.stdout.strip().splitlines()[-1])
     line["onesweep"] = mode == "1"
+    line["rounds"] = rounds or "default"
     line["n"] = int(os.environ.get("AUROC_N", "1000000"))
     print(json.dumps(line), flush=True)

@@ -22,6 +22,7 @@
 //   * rows are independent segments: histogram/scan/offsets are per row, so a [C, n]
 //     one-vs-rest score matrix is sorted in the same 12 launches.
 #include <algorithm>
+#include <cstdlib>
 
 #include "tea_common.h"
 #include "tea_kernels.h"
@@ -695,7 +696,16 @@ __global__ __launch_bounds__(kRT) void transpose4_kernel(const float* in, int64_
 
 }  // namespace
 
-int radix_sort_rounds(int64_t rows, int64_t n) { return rows * n >= kBigSort ? 16 : 8; }
+int radix_sort_rounds(int64_t rows, int64_t n) {
+  // TORCHEVAL_AMD_K3_ROUNDS=8|16 forces the tiling (A/B); default: 16 from kBigSort keys
+  static const int forced = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K3_ROUNDS");
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v == 8 || v == 16 ? v : 0;
+  }();
+  if (forced) return forced;
+  return rows * n >= kBigSort ? 16 : 8;
+}
 
 int64_t radix_sort_tiles(int64_t rows, int64_t n) {
   const int64_t tile = static_cast<int64_t>(kRT) * radix_sort_rounds(rows, n);
