@@ -76,3 +76,13 @@ def test_bad_labels_raise_and_class_metric():
     m.update(x[200:].to(DEV), y[200:].to(DEV))
     ref = _per_sample_binned_auroc(x, y, 10, thr).mean()
     assert float(m.compute()[0]) == pytest.approx(float(ref), abs=1e-6)
+
+
+@pytest.mark.parametrize("t,c", [(5000, 7), (4096, 3), (4097, 64), (1, 5)])
+def test_threshold_counts_past_the_lds_stage(t, c):
+    """T > 4096 searches the thresholds in global memory instead of LDS; T = 1 and T = 4096 are
+    the edges of the staged path."""
+    x, y, thr = _case(1500, c, t, t + c)
+    ref = _per_sample_binned_auroc(x, y, c, thr)
+    got, _ = multiclass_binned_auroc(x.to(DEV), y.to(DEV), num_classes=c, threshold=thr.to(DEV), average=None)
+    torch.testing.assert_close(got.cpu(), ref, rtol=0, atol=1e-6)
