@@ -42,11 +42,13 @@ int main() {
   CK(hipMalloc(&gran, gbytes));
   CK(hipMalloc(&ctl, 2048));
   CK(hipMalloc(&trace, 2 * 16 * 8 * 8));
+  int* grid = nullptr;  // Sturm-count grid of the eigenvalue search (round 3 on)
+  CK(hipMalloc(&grid, tea::symeig_grid_bytes()));
   CK(hipMemset(gran, 0, gbytes));
   CK(hipMemset(trace, 0, 2 * 16 * 8 * 8));
   CK(hipMemcpy(dA, h.data(), (size_t)n * n * 8, hipMemcpyHostToDevice));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(tea::g_symeig_trace), &trace, sizeof(trace)));
-  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.slots = gran; a.ctl = ctl;
+  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.slots = gran; a.ctl = ctl; a.grid = grid;
   for (int it = 0; it < 3; ++it) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
