@@ -403,6 +403,254 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
   }
 }
 
+// ---------------------------------------------------------------- K9b v2: rows per WAVE
+// The same one-launch Householder reduction with a different ownership: each WAVE holds kRW
+// whole rows (lane l: columns l + 64 s, s < C), so every reduction of a column step is a
+// wave reduction (DPP inside 16-lane rows + 4 readlanes) instead of a block reduction with an
+// LDS round trip and a barrier.  The per-column phase trace of tridiag_kernel
+// (csrc/bench/k9b_trace.hip, round 5) spent ~8.9k of ~15.7k cycles per column in its three
+// block reductions, the reflector and the pass; the hand-off wait was the other ~6.8k.  Per
+// column here: the workgroup stages the handed-off p_j and row j+1 in LDS (one barrier,
+// double-buffered by column parity), then each wave redundantly forms w_j, updates row j+1,
+// derives reflector j+1 and applies step j to its rows while accumulating p_{j+1} - no further
+// barrier.  Hand-off slots, sentinel protocol, abort word and outputs are tridiag_kernel's.
+// Measured (round 5, profiles/symeig_wave_ab_r5.json): exact (the K9b tests pass with it), but
+// 18.5 ms at D = 2048 against tridiag_kernel's 14.7 ms - every wave redoes the column-length
+// work (R1, the row j+1 update, the reflector: 32 elements per lane instead of 8) and at one
+// wave per SIMD nothing hides the dependent DPP / readlane chains - so it is opt-in.
+constexpr int kRW = 2;                // rows per wave
+constexpr int kWRows = kRW * kWaves;  // rows per workgroup
+
+__device__ __forceinline__ double readlane_d(double x, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(x), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(x), l);
+  return __hiloint2double(hi, lo);
+}
+
+// the wave's total in every lane, fixed order (deterministic)
+__device__ __forceinline__ double wave_sum_d(double x) {
+  x = row16_sum(x);
+  return (readlane_d(x, 15) + readlane_d(x, 31)) + (readlane_d(x, 47) + readlane_d(x, 63));
+}
+
+// LAPACK dlarfg on x = a[jj+1 .. n) with the diagonal a[jj]; `alpha`, `diag` broadcast by the
+// caller; returns tau / beta / scale (v[jj+1] = 1, v[k] = a[k] * scale beyond)
+__device__ __forceinline__ Reflector reflector_of(double alpha, double sigma, double diag) {
+  Reflector h;
+  h.diag = diag;
+  if (sigma == 0.0) {
+    h.tau = 0.0;
+    h.beta = alpha;
+    h.scale = 0.0;
+  } else {
+    const double mu = sqrt(alpha * alpha + sigma);
+    h.beta = alpha >= 0.0 ? -mu : mu;
+    h.tau = (h.beta - alpha) / h.beta;
+    h.scale = 1.0 / (alpha - h.beta);
+  }
+  return h;
+}
+
+template <int C>
+__global__ __launch_bounds__(kThreads, 1) void tridiag_wave_kernel(const double* __restrict__ A, int n, int64_t ld,
+                                                                    double* d_out, double* e_out,
+                                                                    unsigned long long* slots, unsigned* ctl) {
+  constexpr int kCols = C * 64;
+  constexpr int kQ = kCols / kThreads;  // staged slots per thread per plane
+  __shared__ double sp[2][kCols];       // p_j, by column parity
+  __shared__ double sr[2][kCols];       // row j+1 (updated through step j-1)
+  const int64_t plane = (int64_t)(n - 2) * ld;
+  unsigned long long* const gp0 = slots;
+  unsigned long long* const gr0 = slots + plane;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int row0 = blockIdx.x * kWRows + wv * kRW;  // this wave's first row
+  // registers: the wave's rows, v_j and a (row j+1, turned into v_{j+1} in place); w_j is
+  // re-formed from the staged p_j where it is needed (register pressure: 4 x C doubles)
+  double rw[kRW][C];
+#pragma unroll
+  for (int r = 0; r < kRW; ++r)
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int k = lane + 64 * s, row = row0 + r;
+      rw[r][s] = (row < n && k < n) ? A[(int64_t)row * n + k] : 0.0;
+    }
+  double v[C], a[C];
+
+  // ---- phase 0: reflector 0 from row 0, p_0 of the wave's rows, row 1 published as is
+  Reflector h;
+  {
+    double s2 = 0.0, alpha = 0.0, diag = 0.0;
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int k = lane + 64 * s;
+      a[s] = k < n ? A[k] : 0.0;
+      s2 += k >= 2 ? a[s] * a[s] : 0.0;
+      alpha = k == 1 ? a[s] : alpha;
+      diag = k == 0 ? a[s] : diag;
+    }
+    h = reflector_of(readlane_d(alpha, 1), wave_sum_d(s2), readlane_d(diag, 0));
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int k = lane + 64 * s;
+      v[s] = k == 1 ? 1.0 : (k >= 2 ? a[s] * h.scale : 0.0);
+    }
+    if (blockIdx.x == 0 && t == 0) {
+      d_out[0] = h.diag;
+      e_out[0] = h.beta;
+    }
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) {
+      double acc = 0.0;
+#pragma unroll
+      for (int s = 0; s < C; ++s) acc += rw[r][s] * v[s];
+      acc = wave_sum_d(acc);
+      const int row = row0 + r;
+      if (lane == 0 && row < n && row >= 1) put(gp0, row, h.tau * acc);
+    }
+    if (row0 <= 1 && 1 < row0 + kRW) {
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const int k = lane + 64 * s;
+        if (k >= 1 && k < n) put(gr0, k, row0 == 1 ? rw[0][s] : rw[1][s]);
+      }
+    }
+  }
+
+  for (int j = 0; j <= n - 3; ++j) {
+    // ---- stage p_j and row j+1 in LDS (dead / padded columns as zeros); bounded spin
+    unsigned long long* const gp = gp0 + (int64_t)j * ld;
+    unsigned long long* const gr = gr0 + (int64_t)j * ld;
+    double* const P = sp[j & 1];
+    double* const R = sr[j & 1];
+    bool aborted = false;
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) {
+        const int k = t + kThreads * q;
+        if (k >= j + 1 && k < n) {
+          const unsigned long long x0 = get(gp + k), y0 = get(gr + k);
+          ok = ok && x0 != kSentBits && y0 != kSentBits;
+          P[k] = as_double(x0);
+          R[k] = as_double(y0);
+        } else {
+          P[k] = 0.0;
+          R[k] = 0.0;
+        }
+      }
+      if (ok) break;
+      if (__hip_atomic_load((gu32*)&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        aborted = true;
+        break;
+      }
+      if (spins > kSpinLimit) {
+        __hip_atomic_store((gu32*)&ctl[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        aborted = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (__syncthreads_or(aborted)) return;
+
+    // ---- w_j = p_j - c v_j, row j+1 <- row j+1 - v_j[j+1] w_j - w_j[j+1] v_j (every wave)
+    double r1 = 0.0;
+#pragma unroll
+    for (int s = 0; s < C; ++s) r1 += P[lane + 64 * s] * v[s];
+    r1 = wave_sum_d(r1);
+    const double c = 0.5 * h.tau * r1;
+    const double wj1 = P[j + 1] - c;  // v_j[j+1] = 1
+    double vi0 = 0.0, vi1 = 0.0, a1 = 0.0, a2 = 0.0, s2 = 0.0;
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int k = lane + 64 * s;
+      const double ws = P[k] - c * v[s];
+      a[s] = R[k] - (ws + wj1 * v[s]);
+      vi0 = k == row0 ? v[s] : vi0;
+      vi1 = k == row0 + 1 ? v[s] : vi1;
+      a1 = k == j + 1 ? a[s] : a1;
+      a2 = k == j + 2 ? a[s] : a2;
+      s2 += k >= j + 3 ? a[s] * a[s] : 0.0;
+    }
+    // the wave's rows' v_j[i] (lane i & 63 holds them), w_j[i] from the staged p_j
+    double vi[kRW], wi[kRW];
+    vi[0] = row0 < n ? readlane_d(vi0, row0 & 63) : 0.0;
+    vi[1] = row0 + 1 < n ? readlane_d(vi1, (row0 + 1) & 63) : 0.0;
+    wi[0] = row0 < n ? P[row0] - c * vi[0] : 0.0;
+    wi[1] = row0 + 1 < n ? P[row0 + 1] - c * vi[1] : 0.0;
+    a1 = readlane_d(a1, (j + 1) & 63);
+
+    if (j == n - 3) {
+      // last step: row n-2 is final; the owner of row n-1 finishes its diagonal
+      if (blockIdx.x == 0 && wv == 0) {
+#pragma unroll
+        for (int s = 0; s < C; ++s) {
+          const int k = lane + 64 * s;
+          if (k == n - 2) d_out[n - 2] = a[s];
+          if (k == n - 1) e_out[n - 2] = a[s];
+        }
+      }
+      const int r = (n - 1) - row0;
+      if (r >= 0 && r < kRW) {
+#pragma unroll
+        for (int s = 0; s < C; ++s) {
+          const int k = lane + 64 * s;
+          if (k == n - 1) d_out[n - 1] = (r == 0 ? rw[0][s] : rw[1][s]) - 2.0 * vi[r] * wi[r];
+        }
+      }
+      break;
+    }
+
+    // ---- reflector j+1 (redundant in every wave); a becomes v_{j+1}
+    a2 = readlane_d(a2, (j + 2) & 63);
+    const Reflector hn = reflector_of(a2, wave_sum_d(s2), a1);
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const int k = lane + 64 * s;
+      a[s] = k == j + 2 ? 1.0 : (k >= j + 3 ? a[s] * hn.scale : 0.0);
+    }
+    if (blockIdx.x == 0 && t == 0) {
+      d_out[j + 1] = hn.diag;
+      e_out[j + 1] = hn.beta;
+    }
+
+    // ---- one register pass: step j on the wave's rows, p_{j+1} accumulated
+    double acc[kRW] = {0.0, 0.0};
+    const bool live0 = row0 < n && row0 >= j + 1, live1 = row0 + 1 < n && row0 + 1 >= j + 1;  // wave-uniform
+#pragma unroll
+    for (int s = 0; s < C; ++s) {
+      const double ws = P[lane + 64 * s] - c * v[s];
+      if (live0) {
+        const double x = rw[0][s] - (vi[0] * ws + wi[0] * v[s]);
+        rw[0][s] = x;
+        acc[0] += x * a[s];
+      }
+      if (live1) {
+        const double x = rw[1][s] - (vi[1] * ws + wi[1] * v[s]);
+        rw[1][s] = x;
+        acc[1] += x * a[s];
+      }
+    }
+    // the owner of row j+2 publishes the row before the p reduction
+    const int ro = (j + 2) - row0;
+    if (ro >= 0 && ro < kRW) {
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const int k = lane + 64 * s;
+        if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, k, ro == 0 ? rw[0][s] : rw[1][s]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRW; ++r) {
+      const double pt = wave_sum_d(acc[r]);
+      const int row = row0 + r;
+      if (lane == 0 && row < n && row >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, row, hn.tau * pt);
+    }
+#pragma unroll
+    for (int s = 0; s < C; ++s) v[s] = a[s];
+    h = hn;
+  }
+}
+
 // # eigenvalues of the tridiagonal (d, e2 = e^2) below x (LAPACK dstebz's Sturm count).
 // (A v_rcp_f64 + Newton reciprocal with two interleaved chains per lane measured 13% slower
 // than this plain division at D = 2048: 2.15 vs 1.9 ms.)
@@ -568,6 +816,28 @@ int64_t symeig_slot_bytes(int64_t n) { return 2 * (n - 2) * symeig_slot_stride(n
 int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   int G = 0, R = 0;
   if (symeig_plan(a.n, &G, &R) != 0) return 1;
+  // K9b v2 (rows per wave) only on TORCHEVAL_AMD_SYMEIG_WAVE=1, and only when the grid of
+  // n / 8 workgroups fits the device's CUs and the row fits 32 columns per lane (n <= 2048):
+  // measured slower than tridiag_kernel (18.5 vs 14.7 ms at D = 2048,
+  // profiles/symeig_wave_ab_r5.json), kept as the A/B arm
+  static const bool wave_mode = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_WAVE");
+    return e && e[0] == '1';
+  }();
+  const void* wkern = nullptr;
+  int GW = 0;
+  if (wave_mode && a.n <= 2048) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+        (a.n + kWRows - 1) / kWRows <= cus) {
+      GW = (int)((a.n + kWRows - 1) / kWRows);
+      wkern = a.n <= 512    ? reinterpret_cast<const void*>(&tridiag_wave_kernel<8>)
+              : a.n <= 1024 ? reinterpret_cast<const void*>(&tridiag_wave_kernel<16>)
+              : a.n <= 1536 ? reinterpret_cast<const void*>(&tridiag_wave_kernel<24>)
+                            : reinterpret_cast<const void*>(&tridiag_wave_kernel<32>);
+    }
+  }
   // the smallest instance holding ceil(n / 256) columns and R rows per thread: every register
   // slot is live (the pass has no per-element column test), e.g. 8 x 8 for the FID's D = 2048
   const int need = (int)max((a.n + kThreads - 1) / kThreads, (int64_t)R);
@@ -586,6 +856,7 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   unsigned long long* slots = a.slots;
   unsigned* ctl = a.ctl;
   void* args[] = {&A, &n, &R, &ld, &d, &e, &slots, &ctl};
+  void* wargs[] = {&A, &n, &ld, &d, &e, &slots, &ctl};
   // TORCHEVAL_AMD_SYMEIG_COOP=0: a plain launch of the same grid (A/B of the cooperative
   // launch's process-exit behaviour under rocprofv3; G <= #CUs workgroups are co-resident in
   // practice and the bounded hand-off spins abort to the library fallback if they are not)
@@ -593,8 +864,11 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
     const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_COOP");
     return !(e && e[0] == '0');
   }();
-  const hipError_t lrc = coop ? hipLaunchCooperativeKernel(kern, dim3(G), dim3(kThreads), args, 0, stream)
-                              : hipLaunchKernel(kern, dim3(G), dim3(kThreads), args, 0, stream);
+  const void* lk = wkern ? wkern : kern;
+  void** la = wkern ? wargs : args;
+  const int lg = wkern ? GW : G;
+  const hipError_t lrc = coop ? hipLaunchCooperativeKernel(lk, dim3(lg), dim3(kThreads), la, 0, stream)
+                              : hipLaunchKernel(lk, dim3(lg), dim3(kThreads), la, 0, stream);
   if (lrc != hipSuccess) return 3;
   sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
   if (n >= 1536)

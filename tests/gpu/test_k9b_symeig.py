@@ -148,3 +148,35 @@ def test_nan_entries_do_not_stall_the_hand_off(payload):
     assert native().sym_eigvals(m.to(DEV), lam, status) == 0
     assert int(status.item()) == 0
     assert torch.isnan(lam.cpu()).all()
+
+
+_WAVE_CHILD = r"""
+import torch
+from torcheval_amd.ops import native
+out = []
+for n in (3, 5, 64, 257, 1000, 2048):
+    g = torch.Generator().manual_seed(n)
+    x = torch.randn(n, n + 7, generator=g, dtype=torch.float64)
+    m = x @ x.T / x.shape[1]
+    lam = torch.empty(n, dtype=torch.float64, device="cuda")
+    st = torch.zeros(1, dtype=torch.int32, device="cuda")
+    assert native().sym_eigvals(m.cuda(), lam, st) == 0 and int(st.item()) == 0
+    ref = torch.linalg.eigvalsh(m)
+    out.append(float((lam.cpu() - ref).abs().max() / ref.abs().max()))
+print(max(out))
+"""
+
+
+def test_wave_kernel_arm_matches_cpu():
+    """The opt-in rows-per-wave reduction (TORCHEVAL_AMD_SYMEIG_WAVE=1, read once per process,
+    hence the child process) against CPU eigvalsh."""
+    import os
+    import subprocess
+    import sys
+
+    env = dict(os.environ, TORCHEVAL_AMD_SYMEIG_WAVE="1")
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    r = subprocess.run([sys.executable, "-c", _WAVE_CHILD], env=env, cwd=root, capture_output=True,
+                       text=True, timeout=100)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert float(r.stdout.strip().splitlines()[-1]) < 1e-12
