@@ -64,6 +64,11 @@ def main() -> None:
     wts = torch.rand(64, 128000, device=dev, generator=g)
     mctr = M.ClickThroughRate(num_tasks=64, device=dev)
     work.append(("K5b ctr 64x128000", lambda: mctr.update(clicks, wts)))
+    work.append(("K4b multiclass binned auroc 100k x 100 T=200",
+                 lambda: F.multiclass_binned_auroc(xm, ym, num_classes=100, threshold=200)))
+    xo = torch.rand(8192, 1001, device=dev, generator=g)
+    yo = torch.rand(8192, 1001, device=dev, generator=g)
+    work.append(("K5 mse 8192x1001", lambda: F.mean_squared_error(xo, yo)))
     only = os.environ.get("PMC_ONLY")
     if only:
         work = [w for w in work if only in w[0]]
