@@ -1,6 +1,8 @@
 """binary_auroc at N=1M (BASELINE config 3): wall time per call, onesweep sort vs the legacy
 upsweep / downsweep sort (TORCHEVAL_AMD_K3_ONESWEEP=0).  The variable is read once per process,
-so each mode runs in its own child process; one JSON line per mode.  (Round 5 also measured a
+so each mode runs in its own child process; one JSON line per mode.  TORCHEVAL_AMD_K3_FOLD=1
+turns on the tile-sum fold into the last onesweep pass (no tile_sums launch); K3_AB_FOLD_PROBE=1
+splits its cost (TORCHEVAL_AMD_K3_FOLD_PROBE: 1 = no atomics, 2 = no fold work).  (Round 5 also measured a
 tile_sums fold into tile_area and counter-ticket tile ids - both slower and removed:
 profiles/k3_onesweep_r5.json.)"""
 import json
@@ -55,8 +57,14 @@ print(json.dumps(res))
 '''
 
 repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-for mode, rounds in (("1", ""), ("1", "16"), ("0", ""), ("0", "16")):
-    env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, TORCHEVAL_AMD_K3_ROUNDS=rounds, REPO=repo)
+MODES = [("1", "", "1"), ("1", "", "0"), ("0", "", "1")]
+if os.environ.get("K3_AB_FOLD_PROBE") == "1":  # fold cost split: no atomics / no fold work at all
+    MODES = [("1", "", "1"), ("1", "", "1p1"), ("1", "", "1p2"), ("1", "", "0")]
+if os.environ.get("K3_AB_ROUNDS") == "1":
+    MODES += [("1", "16", "1"), ("0", "16", "1")]
+for mode, rounds, fold in MODES:
+    env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, TORCHEVAL_AMD_K3_ROUNDS=rounds,
+               TORCHEVAL_AMD_K3_FOLD=fold[0], TORCHEVAL_AMD_K3_FOLD_PROBE=fold[2:], REPO=repo)
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     if out.returncode != 0:
         print(out.stdout[-2000:], out.stderr[-4000:])
@@ -64,5 +72,7 @@ for mode, rounds in (("1", ""), ("1", "16"), ("0", ""), ("0", "16")):
     line = json.loads(out.stdout.strip().splitlines()[-1])
     line["onesweep"] = mode == "1"
     line["rounds"] = rounds or "default"
+    line["tile_sums_fold"] = fold[0] == "1" and mode == "1"
+    line["fold_probe"] = fold[2:] or None
     line["n"] = int(os.environ.get("AUROC_N", "1000000"))
     print(json.dumps(line), flush=True)

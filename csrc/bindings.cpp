@@ -398,11 +398,17 @@ static tea::AucScanArgs scan_args(const Tensor& sorted, const Tensor& order, con
 void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
               const optional<Tensor>& weight, bool class_mode, const optional<Tensor>& out_auroc,
               const optional<Tensor>& out_auprc, const optional<Tensor>& init,
-              const optional<Tensor>& out_raw, int64_t payload_kind) {
+              const optional<Tensor>& out_raw, int64_t payload_kind, const optional<Tensor>& tsum) {
   c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sorted.device());
   Tensor tg, w;
   tea::AucScanArgs a = scan_args(sorted, order, target, weight, class_mode, payload_kind, tg, w, "auc_scan");
   const int64_t rows = a.rows, n = a.n;
+  if (tsum.has_value()) {  // tile totals folded by sort_desc (payload kinds 1 / 2 only)
+    TORCH_CHECK(payload_kind != 0 && tsum->scalar_type() == at::kDouble && tsum->is_contiguous() &&
+                    tsum->device() == sorted.device() && tsum->numel() == rows * ((n + 1023) / 1024) * 2,
+                "auc_scan: tsum must be sort_desc's float64 [rows, ceil(n / 1024), 2] fold of a payload sort");
+    a.tsum_ext = tsum->data_ptr<double>();
+  }
   auto f64_out = [&](const optional<Tensor>& t, const char* name) -> double* {
     if (!t.has_value()) return nullptr;
     TORCH_CHECK(t->scalar_type() == at::kDouble && t->is_contiguous() && t->numel() == rows &&
@@ -1237,8 +1243,12 @@ void transpose_f32(const Tensor& x, const Tensor& out) {
 }
 
 // K3a: segmented descending radix sort of f32 rows -> (sorted scores, int32 permutation)
-void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_order,
-               const optional<Tensor>& payload, int64_t payload_kind) {
+// `fold` (optional, float64 [rows, ceil(n / 1024), 2]): with a target / label payload on the
+// onesweep path, the last pass also writes the K3 scan's 1024-sample tile totals there
+// (RadixArgs::fold_ab) and the call returns true; pass it to auc_scan as `tsum`.  False: not
+// folded (legacy sort, no payload), auc_scan must run its own tile_sums.
+bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_order,
+               const optional<Tensor>& payload, int64_t payload_kind, const optional<Tensor>& fold) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kFloat && x.stride(1) == 1,
               "sort_desc: x must be float32 [rows, n] with contiguous rows");
@@ -1253,7 +1263,7 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   a.in_row_stride = x.stride(0);
   a.rows = x.size(0);
   a.n = x.size(1);
-  if (a.rows == 0 || a.n == 0) return;
+  if (a.rows == 0 || a.n == 0) return false;
   a.tiles = tea::radix_sort_tiles(a.rows, a.n);
   const int64_t m = a.rows * a.n;
   Tensor ws = at::empty({4 * m + a.rows * 256 * a.tiles}, x.options().dtype(at::kInt));
@@ -1334,7 +1344,23 @@ void sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
     a.payload = pl.data_ptr();
     a.payload_dt = dt_of(pl);
   }
+  const int64_t otiles = (a.n + 1023) / 1024;
+  if (fold.has_value()) {
+    TORCH_CHECK(fold->scalar_type() == at::kDouble && fold->is_contiguous() && fold->device() == x.device() &&
+                    fold->numel() == a.rows * otiles * 2,
+                "sort_desc: fold must be contiguous float64 [rows, ceil(n / 1024), 2] on the device of x");
+    if (a.os_hdr != nullptr && a.payload_kind != 0) {
+      a.fold_ab = fold->data_ptr<double>();
+      a.fold_otiles = otiles;
+      static const int probe = [] {
+        const char* e = std::getenv("TORCHEVAL_AMD_K3_FOLD_PROBE");
+        return e ? std::atoi(e) : 0;
+      }();
+      a.fold_probe = probe;
+    }
+  }
   check_launch(tea::launch_radix_sort_desc(a, stream_for(x)), "sort_desc");
+  return a.fold_ab != nullptr;
 }
 
 
@@ -1498,7 +1524,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("auc_scan", &auc_scan, "K3 tie-aware scan -> AUROC / AUPRC per row", py::arg("sorted"),
         py::arg("order"), py::arg("target"), py::arg("weight"), py::arg("class_mode"),
         py::arg("out_auroc"), py::arg("out_auprc"), py::arg("init") = py::none(),
-        py::arg("out_raw") = py::none(), py::arg("payload_kind") = 0);
+        py::arg("out_raw") = py::none(), py::arg("payload_kind") = 0, py::arg("tsum") = py::none());
   m.def("curve_workspace_bytes", &curve_workspace_bytes, "K3c workspace bytes", py::arg("rows"), py::arg("n"),
         py::arg("rafp"));
   m.def("curve_count", &curve_count, "K3c tile totals + tie-group tails + per-row scans (G_r -> sizes)",
@@ -1557,7 +1583,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         pybind11::arg("x"), pybind11::arg("clear") = true);
   m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
         py::arg("x"), py::arg("out_sorted"), py::arg("out_order"), py::arg("payload") = py::none(),
-        py::arg("payload_kind") = 0);
+        py::arg("payload_kind") = 0, py::arg("fold") = py::none());
   m.def("binned_finalize", &binned_finalize, "binned AUROC / AUPRC / PR-curve points from counts",
         py::arg("tp"), py::arg("fp"), py::arg("fn") = py::none(), py::arg("out_auroc") = py::none(),
         py::arg("out_auprc") = py::none(), py::arg("out_prec") = py::none(),
@@ -1588,12 +1614,12 @@ void op_row_sums(const Tensor& x, const optional<Tensor>& t, const optional<Tens
   row_sums(x, t, w, w_scalar, outs.vec(), codes.vec(), rows);
 }
 void op_sort_desc(const Tensor& x, const Tensor& s, const Tensor& o, const optional<Tensor>& p, int64_t kind) {
-  sort_desc(x, s, o, p, kind);
+  sort_desc(x, s, o, p, kind, c10::nullopt);
 }
 void op_auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target, const optional<Tensor>& weight,
                  bool class_mode, const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc,
                  const optional<Tensor>& init, const optional<Tensor>& out_raw, int64_t payload_kind) {
-  auc_scan(sorted, order, target, weight, class_mode, out_auroc, out_auprc, init, out_raw, payload_kind);
+  auc_scan(sorted, order, target, weight, class_mode, out_auroc, out_auprc, init, out_raw, payload_kind, c10::nullopt);
 }
 void op_rafp(const Tensor& sorted, const Tensor& order, const Tensor& target, bool class_mode, int64_t kind,
              double p, const Tensor& out_rec, const Tensor& out_thr) {

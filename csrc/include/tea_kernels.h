@@ -110,6 +110,7 @@ struct AucScanArgs {
   // workspace carve-up (set by the launcher)
   void* ab = nullptr;
   void* tsum = nullptr;
+  const void* tsum_ext = nullptr;  // [rows, ntiles] D2 tile totals already folded by the sort
   void* tstart = nullptr;
   void* tarea = nullptr;
   void* totals = nullptr;
@@ -467,6 +468,12 @@ struct RadixArgs {
   int64_t os_splane = 0;          // words per status plane
   unsigned long long* os_gacc = nullptr;  // 2 planes of [rows * ngroups, 256] (arrivals << 32 | sum)
   int64_t os_gplane = 0;          // words per group plane
+  // optional K3 tile-sum fold (onesweep, payload kinds 1 / 2): the last pass adds each
+  // 1024-sample output tile's (sum a, sum b) of the sorted payload (a = t, b = 1 - t; kind 2:
+  // t = [label == row]) into fold_ab, which pass 0 zeroes; auc_scan then skips tile_sums
+  double* fold_ab = nullptr;      // [rows, fold_otiles, 2]
+  int64_t fold_otiles = 0;        // ceil(n / 1024)
+  int fold_probe = 0;             // A/B probe (TORCHEVAL_AMD_K3_FOLD_PROBE): 1 no atomics, 2 no fold work
 };
 bool radix_onesweep_ok(int64_t rows, int64_t n);  // the tiling the onesweep passes take
 int64_t radix_onesweep_status_words(int64_t rows, int64_t n);

@@ -429,8 +429,83 @@ __global__ __launch_bounds__(kRT) void onesweep_hist_kernel(RadixArgs a, int64_t
   }
 }
 
+// K3 tile-sum fold (RadixArgs::fold_ab), run by the last pass once its sorted tile is staged in
+// LDS: positions rise monotonically through the staged tile (digit runs in digit order, each
+// run contiguous in the row), so each digit's run splits into <= 2 + run / 1024 pieces by
+// 1024-sample output tile.  Prefix sums of (a, b) over the staged tile (thread-contiguous chunks,
+// one block scan) give every piece's sums; thread d adds its run's pieces with device atomics
+// (a few per block for probability scores, whose top byte takes a handful of values).
+constexpr int kFoldShift = 10;  // k3::kTile = 1024-sample tiles of the scan
+
+template <int kRounds>
+__device__ __forceinline__ void fold_tile_sums(const RadixArgs& a, int64_t row, const uint32_t* sv, int tn,
+                                               const uint32_t* tstart, const uint32_t* base, uint32_t cnt,
+                                               double* fa, double* fb, double (*fw)[kRWaves]) {
+  const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
+  float va[kRounds];
+  double ca = 0.0, cb = 0.0;
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const int p = t * kRounds + j;
+    float x = 0.f;
+    if (p < tn) {
+      const uint32_t v = sv[p];
+      x = a.payload_kind == 1 ? __uint_as_float(v)
+                              : (static_cast<int64_t>(static_cast<int32_t>(v)) == row ? 1.f : 0.f);
+      cb += static_cast<double>(1.f - x);
+    }
+    va[j] = x;
+    ca += x;
+  }
+  double ia = ca, ib = cb;  // inclusive wave scans
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double ua = __shfl_up(ia, o, 64), ub = __shfl_up(ib, o, 64);
+    if (lane >= o) {
+      ia += ua;
+      ib += ub;
+    }
+  }
+  if (lane == 63) {
+    fw[0][w] = ia;
+    fw[1][w] = ib;
+  }
+  __syncthreads();
+  double ra = ia - ca, rb = ib - cb;
+#pragma unroll
+  for (int q = 0; q < kRWaves; ++q) {
+    if (q < w) {
+      ra += fw[0][q];
+      rb += fw[1][q];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < kRounds; ++j) {
+    const int p = t * kRounds + j;
+    fa[p] = ra;
+    fb[p] = rb;
+    ra += va[j];
+    rb += p < tn ? static_cast<double>(1.f - va[j]) : 0.0;
+  }
+  if (t == kRT - 1) {
+    fa[kRT * kRounds] = ra;
+    fb[kRT * kRounds] = rb;
+  }
+  __syncthreads();
+  if (cnt == 0 || (a.fold_probe & 1)) return;
+  const int64_t g0 = base[t], g1 = g0 + cnt;  // row-relative positions of this digit's run
+  const int s0 = static_cast<int>(tstart[t]);
+  double* out = a.fold_ab + row * a.fold_otiles * 2;
+  for (int64_t ot = g0 >> kFoldShift; ot <= (g1 - 1) >> kFoldShift; ++ot) {
+    const int64_t lo = max(g0, ot << kFoldShift), hi = min(g1, (ot + 1) << kFoldShift);
+    const int ps = s0 + static_cast<int>(lo - g0), pe = s0 + static_cast<int>(hi - g0);
+    atomicAdd(out + 2 * ot, fa[pe] - fa[ps]);
+    atomicAdd(out + 2 * ot + 1, fb[pe] - fb[ps]);
+  }
+}
+
 // one pass: load + rank as radix_downsweep_kernel, then publish / look back, then scatter
-template <int kRounds, int VMODE, typename PT = uint32_t, int KIND = 0>
+template <int kRounds, int VMODE, typename PT = uint32_t, int KIND = 0, bool FOLD = false>
 __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const uint32_t* keys_in,
                                                             const uint32_t* vals_in, uint32_t* keys_out,
                                                             uint32_t* vals_out, int pass) {
@@ -441,6 +516,9 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   __shared__ uint32_t wc[kRWaves][kBins];
   __shared__ uint32_t wsum[kRWaves];
   __shared__ uint32_t sk[kRTile], sv[kRTile];
+  __shared__ double fa[FOLD ? kRTile + 1 : 1], fb[FOLD ? kRTile + 1 : 1];
+  __shared__ double fw[2][kRWaves];
+  uint32_t my_cnt = 0;  // this tile's count of digit threadIdx.x
   // tile id = blockIdx: workgroups are dispatched in order per XCD, so the lowest unfinished
   // tile only ever waits on finished ones.  (Ids from a counter ticket, the textbook guard,
   // cost 512 serialised same-address atomics per launch: 18.9 vs 13.2 us per pass at 1M,
@@ -515,6 +593,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
       wc[q][t] = o;
       o += c;
     }
+    my_cnt = o;
     // publish this tile's count (ready-flagged) and add it to the group's word
     const int ngroups = static_cast<int>(a.ngroups);
     uint32_t* st = a.os_status + P * a.os_splane + row * a.tiles * kBins;
@@ -538,6 +617,11 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
       unsigned long long* go = a.os_gacc + (P ^ 1) * a.os_gplane;
       const int64_t ge = a.os_hdr[6 + (P ^ 1)];
       for (int64_t q = me; q < ge; q += nthr) go[q] = 0ull;
+      // pass 0 zeroes the tile-sum fold the last pass adds into (stream order separates them)
+      if (VMODE != 0 && a.fold_ab != nullptr) {
+        const int64_t fe = a.rows * a.fold_otiles * 2;
+        for (int64_t q = me; q < fe; q += nthr) a.fold_ab[q] = 0.0;
+      }
     }
     // tiles-before prefix: whole groups before this tile's group, then the group's earlier tiles
     uint32_t pre = 0;
@@ -604,6 +688,9 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   __syncthreads();
   const int64_t tn64 = a.n - tbase;
   const int tn = static_cast<int>(tn64 < kRTile ? tn64 : kRTile);
+  if constexpr (FOLD) {
+    if (!(a.fold_probe & 2)) fold_tile_sums<kRounds>(a, row, sv, tn, tstart, base, my_cnt, fa, fb, fw);
+  }
   if (tn == kRTile) {
     uint32_t kk[kRounds], vv[kRounds];
     int32_t pb[kRounds];
@@ -777,7 +864,9 @@ int radix_onesweep(const RadixArgs& a, hipStream_t stream) {
   for (int p = 0; p < 4; ++p) {
 #define TEA_PASS(...) \
   hipLaunchKernelGGL((onesweep_pass_kernel<R, __VA_ARGS__>), grid, dim3(kRT), 0, stream, a, kin[p], vin[p], kout[p], vout[p], p)
-    if (p > 0) {
+    if (p == 3 && a.fold_ab != nullptr) {
+      TEA_PASS(0, uint32_t, 0, true);
+    } else if (p > 0) {
       TEA_PASS(0);
     } else if (a.payload_kind == 0) {
       TEA_PASS(1);
@@ -822,6 +911,9 @@ int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
   if (a.os_hdr != nullptr) {
     if (!radix_onesweep_ok(a.rows, a.n) || a.os_splane < radix_onesweep_status_words(a.rows, a.n) ||
         a.os_gplane < radix_onesweep_group_words(a.rows, a.n))
+      return -2;
+    if (a.fold_ab != nullptr && ((a.payload_kind != 1 && a.payload_kind != 2) ||
+                                 a.fold_otiles != ((a.n + (1 << kFoldShift) - 1) >> kFoldShift)))
       return -2;
     return radix_sort_rounds(a.rows, a.n) == 16 ? radix_onesweep<16>(a, stream) : radix_onesweep<8>(a, stream);
   }

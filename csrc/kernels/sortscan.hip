@@ -4,7 +4,9 @@
 //   auroc.py:115-152, 206-235   diff != 0 -> pad -> gather x2 -> cumsum x2 -> masked_scatter x2
 //                               (host-synchronising) -> trapz -> where
 //   auprc.py / precision_recall_curve.py:156-231   same prefix + per-class Python loops
-// with three launches (rows of <= kFuseTiles tiles) or four that never leave the device:
+// with three launches (rows of <= kFuseTiles tiles) or four that never leave the device (one
+// fewer when the onesweep sort folded the tile totals, AucScanArgs::tsum_ext - opt-in, measured
+// slower: profiles/k3_fold_r5.json):
 //   1 tile_sums : per 1024-sample tile, the tile totals (double) of a = w*t, b = w*(1-t); when the
 //                 sort carried the targets / labels (payload kinds 1, 2) they are read in place,
 //                 otherwise (target, weight) are gathered through the permutation into float2 ab.
@@ -477,8 +479,15 @@ int launch_auc_scan(AucScanArgs a, void* workspace, hipStream_t stream) {
   // block reduction before the scan), which 100 rows x 98 tiles paid for with +12 us per call
   const bool direct = a.payload_kind != 0, fused = ntiles <= kFuseTiles && a.rows <= 4;
   const bool f64 = a.key_dt == DType::f64;
-  if (direct) hipLaunchKernelGGL(tile_sums_kernel<true>, grid, dim3(kT), 0, stream, a);
-  else hipLaunchKernelGGL(tile_sums_kernel<false>, grid, dim3(kT), 0, stream, a);
+  if (a.tsum_ext != nullptr) {
+    // the sort's last pass already added the tile totals (RadixArgs::fold_ab): no tile_sums launch
+    if (!direct) return -2;
+    a.tsum = const_cast<void*>(a.tsum_ext);
+  } else if (direct) {
+    hipLaunchKernelGGL(tile_sums_kernel<true>, grid, dim3(kT), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(tile_sums_kernel<false>, grid, dim3(kT), 0, stream, a);
+  }
   if (!fused) hipLaunchKernelGGL(tile_scan_kernel, dim3(a.rows), dim3(kT), 0, stream, a, ntiles);
 #define TEA_AREA(K, D, F) hipLaunchKernelGGL((tile_area_kernel<K, D, F>), grid, dim3(kT), 0, stream, a)
   if (f64) {

@@ -119,3 +119,65 @@ def test_tie_groups_across_tiles(group_len, offset):
     ts = torch.stack([t, t, t.flip(0)])
     torch.testing.assert_close(binary_auroc(xs.to(DEV), ts.to(DEV), num_tasks=3).cpu().double(),
                                binary_auroc(xs.double(), ts, num_tasks=3).double(), rtol=1e-9, atol=1e-12)
+
+
+def _tile_sums_cpu(sorted_payload: torch.Tensor, kind: int) -> torch.Tensor:
+    """(sum t, sum 1 - t) per 1024-sample tile of each row, float64, from the sorted payload."""
+    rows, n = sorted_payload.shape
+    if kind == 1:
+        t = sorted_payload.view(torch.float32).double()
+    else:
+        t = (sorted_payload.long() == torch.arange(rows)[:, None]).double()
+    b = (1.0 - t.float()).double()
+    tiles = (n + 1023) // 1024
+    pad = tiles * 1024 - n
+    t = torch.nn.functional.pad(t, (0, pad)).view(rows, tiles, 1024).sum(-1)
+    b = torch.nn.functional.pad(b, (0, pad)).view(rows, tiles, 1024).sum(-1)
+    return torch.stack([t, b], -1)
+
+
+@pytest.mark.parametrize("rows,n,kind,frac", [(1, 1_000_000, 1, False), (1, 1, 1, False), (1, 1025, 1, False),
+                                              (3, 70_001, 1, False), (8, 20_000, 2, False), (2, 2_100_000, 1, False),
+                                              (1, 300_000, 1, True), (5, 4097, 2, False)])
+def test_tile_sum_fold_matches_the_sorted_payload(rows, n, kind, frac):
+    """The last onesweep pass's tile-sum fold (sort_desc(fold=...)) against the tile totals of its
+    own sorted payload; then auc_scan with the fold equals auc_scan without it."""
+    from torcheval_amd.ops import native
+
+    g = torch.Generator().manual_seed(rows * 7 + n)
+    x = _keys(rows, n, n, 5 if n > 1000 else 0)
+    if kind == 1:
+        pl = torch.rand(rows, n, generator=g) if frac else (torch.rand(rows, n, generator=g) < 0.4).float()
+    else:
+        pl = torch.randint(0, rows + 2, (n,), generator=g)
+    xd = x.to(DEV)
+    s = torch.empty_like(xd)
+    idx = torch.empty(xd.shape, dtype=torch.int32, device=DEV)
+    fold = torch.full((rows, (n + 1023) // 1024, 2), float("nan"), dtype=torch.float64, device=DEV)
+    assert native().sort_desc(xd, s, idx, pl.to(DEV), kind, fold), "onesweep path expected to fold"
+    want = _tile_sums_cpu(idx.cpu(), kind)
+    if frac:
+        torch.testing.assert_close(fold.cpu(), want, rtol=1e-12, atol=1e-9)
+    else:
+        assert torch.equal(fold.cpu(), want)
+    # the scan with and without the fold
+    out = [torch.empty(rows, dtype=torch.float64, device=DEV) for _ in range(4)]
+    tgt = pl.to(DEV)
+    native().auc_scan(s, idx, tgt, None, kind == 2, out[0], out[1], None, None, kind)
+    native().auc_scan(s, idx, tgt, None, kind == 2, out[2], out[3], None, None, kind, fold)
+    torch.testing.assert_close(out[2], out[0], rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(out[3], out[1], rtol=1e-12, atol=1e-12)
+
+
+def test_fold_not_taken_off_the_onesweep_path():
+    """Past the onesweep tiling (or without a payload) the sort reports no fold."""
+    from torcheval_amd.ops import native
+
+    x = torch.rand(9, 5000, device=DEV)
+    s = torch.empty_like(x)
+    idx = torch.empty(x.shape, dtype=torch.int32, device=DEV)
+    fold = torch.empty(9, 5, 2, dtype=torch.float64, device=DEV)
+    assert not native().sort_desc(x, s, idx, torch.zeros(9, 5000, device=DEV), 1, fold)
+    x1 = torch.rand(1, 5000, device=DEV)
+    s1, i1 = torch.empty_like(x1), torch.empty(x1.shape, dtype=torch.int32, device=DEV)
+    assert not native().sort_desc(x1, s1, i1, None, 0, torch.empty(1, 5, 2, dtype=torch.float64, device=DEV))

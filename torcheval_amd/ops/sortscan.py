@@ -1,11 +1,15 @@
 """K3 sort-and-scan wrappers (csrc/kernels/sortscan.hip): exact tie-aware AUROC / AUPRC.
 
 Pipeline per call: one segmented device sort of the scores (descending, one row per task /
-class) followed by the four-launch K3 scan.  No host synchronisation anywhere.  (A bucketed
+class) followed by the K3 scan.  Opt-in (``TORCHEVAL_AMD_K3_FOLD=1``): with a target / label
+payload on the onesweep sort, the sort's last pass also folds the scan's 1024-sample tile totals,
+so the scan skips its tile_sums launch (7 launches for binary_auroc at 1M; measured slower, see
+``_FOLD``).  No host synchronisation anywhere.  (A bucketed
 no-global-sort variant, K3b, was built and measured slower at every size - see
 profiles/README.md, round 3 - and removed.)
 """
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -29,16 +33,38 @@ def _rows_f32(v: torch.Tensor) -> torch.Tensor:
     return v if v.dtype == torch.float32 and v.stride(-1) == 1 else v.float().contiguous()
 
 
+# TORCHEVAL_AMD_K3_FOLD=1: the onesweep sort's last pass folds the scan's tile totals (7 launches
+# for binary_auroc at 1M instead of 8).  Off by default: measured slower - 88.8 vs 82.6 us at 1M,
+# the fold's device atomics cost ~8 us against the ~4 us of the tile_sums launch they remove
+# (profiles/k3_fold_r5.json)
+_FOLD = os.environ.get("TORCHEVAL_AMD_K3_FOLD", "0") == "1"
+
+
+def _fold_buffer(x: torch.Tensor) -> Optional[torch.Tensor]:
+    """float64 [rows, ceil(n / 1024), 2] for the sort's tile-sum fold (uninitialised: the sort
+    zeroes it in its first pass)."""
+    rows, n = (1, x.shape[0]) if x.dim() == 1 else (x.shape[0], x.shape[-1])
+    return torch.empty(rows, (n + 1023) // 1024, 2, dtype=torch.float64, device=x.device)
+
+
 def _sort_rows(
     x: torch.Tensor, payload: Optional[torch.Tensor] = None, payload_kind: int = 0
 ) -> Tuple[torch.Tensor, torch.Tensor, int]:
-    """Descending per-row sort -> (sorted, order, kind).
+    """Descending per-row sort -> (sorted, order, kind); see ``_sort_rows_fold``."""
+    return _sort_rows_fold(x, payload, payload_kind, False)[:3]
+
+
+def _sort_rows_fold(
+    x: torch.Tensor, payload: Optional[torch.Tensor] = None, payload_kind: int = 0, fold: bool = True
+) -> Tuple[torch.Tensor, torch.Tensor, int, Optional[torch.Tensor]]:
+    """Descending per-row sort -> (sorted, order, kind, tile sums or None).
 
     f32 runs the K3a radix sort.  With ``payload`` it carries the per-sample target
     (``PAYLOAD_TARGET``: f32 value) or class label (``PAYLOAD_LABEL``: int32; a 1-D payload is
     shared by every row) through the sort instead of the source index, so K3 reads targets in
-    sorted order without a random gather (``kind`` echoes what ``order`` holds).  f64 keys go
-    through torch.sort (int64 permutation, kind 0)."""
+    sorted order without a random gather (``kind`` echoes what ``order`` holds); then the sort
+    may also return the scan's tile totals (``auc_scan(tsum=...)``).  f64 keys go through
+    torch.sort (int64 permutation, kind 0)."""
     if x.dtype not in (torch.float32, torch.float64):
         x = x.float()  # f16/bf16 -> f32 is exact and order preserving
     if x.dtype == torch.float32 and x.shape[-1] < 2**31:
@@ -53,10 +79,11 @@ def _sort_rows(
             payload = _rows_f32(payload)
         elif kind == PAYLOAD_LABEL and payload.dtype not in (torch.int64, torch.int32):
             payload = payload.long()
-        native().sort_desc(x, s, idx, payload, kind)
-        return s, idx, kind
+        buf = _fold_buffer(x) if fold and _FOLD and kind != 0 else None
+        folded = native().sort_desc(x, s, idx, payload, kind, buf)
+        return s, idx, kind, buf if folded else None
     s, idx = torch.sort(x.contiguous(), dim=-1, descending=True)
-    return s, idx, 0
+    return s, idx, 0, None
 
 
 def binary_auc(
@@ -75,11 +102,11 @@ def binary_auc(
         w = weight if weight.dim() == 2 else weight.unsqueeze(0)
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
-    s, idx, kind = _sort_rows(x, t if w is None else None, PAYLOAD_TARGET)
+    s, idx, kind, tsum = _sort_rows_fold(x, t if w is None else None, PAYLOAD_TARGET)
     rows = s.shape[0]
     out_roc = torch.empty(rows, dtype=torch.float64, device=x.device) if roc else None
     out_pr = torch.empty(rows, dtype=torch.float64, device=x.device) if pr else None
-    native().auc_scan(s, idx, t, w, False, out_roc, out_pr, None, None, kind)
+    native().auc_scan(s, idx, t, w, False, out_roc, out_pr, None, None, kind, tsum)
     return out_roc, out_pr
 
 
@@ -99,11 +126,11 @@ def multiclass_auc(
         native().transpose_f32(x, xt)  # LDS-tiled; torch's strided copy is ~10x slower here
     else:
         xt = x.t()
-    s, idx, kind = _sort_rows(xt, target, PAYLOAD_LABEL)
+    s, idx, kind, tsum = _sort_rows_fold(xt, target, PAYLOAD_LABEL)
     rows = s.shape[0]
     out_roc = torch.empty(rows, dtype=torch.float64, device=input.device) if roc else None
     out_pr = torch.empty(rows, dtype=torch.float64, device=input.device) if pr else None
-    native().auc_scan(s, idx, target, None, True, out_roc, out_pr, None, None, kind)
+    native().auc_scan(s, idx, target, None, True, out_roc, out_pr, None, None, kind, tsum)
     return out_roc, out_pr
 
 
@@ -117,8 +144,8 @@ def binary_auc_raw(
     if t.dtype == torch.bool:
         t = t.to(torch.uint8)
     w = None if weight is None else weight.reshape(1, -1)
-    s, idx, kind = _sort_rows(x, t if w is None else None, PAYLOAD_TARGET)
+    s, idx, kind, tsum = _sort_rows_fold(x, t if w is None else None, PAYLOAD_TARGET)
     init = torch.tensor([[tp0, fp0]], dtype=torch.float64, device=x.device)
     raw = torch.empty(1, 4, dtype=torch.float64, device=x.device)
-    native().auc_scan(s, idx, t, w, False, None, None, init, raw, kind)
+    native().auc_scan(s, idx, t, w, False, None, None, init, raw, kind, tsum)
     return raw[0]
