@@ -60,11 +60,18 @@ repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODES = [("1", "", "1"), ("1", "", "0"), ("0", "", "1")]
 if os.environ.get("K3_AB_FOLD_PROBE") == "1":  # fold cost split: no atomics / no fold work at all
     MODES = [("1", "", "1"), ("1", "", "1p1"), ("1", "", "1p2"), ("1", "", "0")]
+HIST = [h for h in os.environ.get("K3_AB_HIST_ROUNDS", "").split(",") if h]
+if HIST:  # histogram blocks of 4096 x h keys (TORCHEVAL_AMD_K3_HIST_ROUNDS), default sort otherwise
+    MODES = [("1", "", "0h" + h) for h in HIST]
 if os.environ.get("K3_AB_ROUNDS") == "1":
     MODES += [("1", "16", "1"), ("0", "16", "1")]
 for mode, rounds, fold in MODES:
     env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, TORCHEVAL_AMD_K3_ROUNDS=rounds,
-               TORCHEVAL_AMD_K3_FOLD=fold[0], TORCHEVAL_AMD_K3_FOLD_PROBE=fold[2:], REPO=repo)
+               TORCHEVAL_AMD_K3_FOLD=fold[0], REPO=repo)
+    if fold[1:2] == "p":
+        env["TORCHEVAL_AMD_K3_FOLD_PROBE"] = fold[2:]
+    if fold[1:2] == "h":
+        env["TORCHEVAL_AMD_K3_HIST_ROUNDS"] = fold[2:]
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     if out.returncode != 0:
         print(out.stdout[-2000:], out.stderr[-4000:])
@@ -73,6 +80,7 @@ for mode, rounds, fold in MODES:
     line["onesweep"] = mode == "1"
     line["rounds"] = rounds or "default"
     line["tile_sums_fold"] = fold[0] == "1" and mode == "1"
-    line["fold_probe"] = fold[2:] or None
+    line["fold_probe"] = fold[2:] if fold[1:2] == "p" else None
+    line["hist_rounds"] = fold[2:] if fold[1:2] == "h" else "1"
     line["n"] = int(os.environ.get("AUROC_N", "1000000"))
     print(json.dumps(line), flush=True)

@@ -853,7 +853,14 @@ template <int R>
 int radix_onesweep(const RadixArgs& a, hipStream_t stream) {
   // histogram: one 4096-key round per block (245 blocks at 1M keys; many-row sorts get their
   // parallelism from the rows: 2 blocks per 100k-key row ran 13 serial rounds each)
-  const int64_t per = static_cast<int64_t>(kRT) * kHistKeys;
+  // TORCHEVAL_AMD_K3_HIST_ROUNDS (A/B): 4096-key rounds per histogram block (fewer blocks, fewer
+  // device atomics into the digit totals, more serial rounds per block)
+  static const int hist_rounds = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K3_HIST_ROUNDS");
+    const int v = e != nullptr ? std::atoi(e) : 1;
+    return v >= 1 && v <= 16 ? v : 1;
+  }();
+  const int64_t per = static_cast<int64_t>(kRT) * kHistKeys * hist_rounds;
   const dim3 hgrid(static_cast<unsigned>((a.n + per - 1) / per), static_cast<unsigned>(a.rows));
   hipLaunchKernelGGL(onesweep_hist_kernel, hgrid, dim3(kRT), 0, stream, a, per);
   const dim3 grid(static_cast<unsigned>(a.rows * a.tiles));
