@@ -142,7 +142,12 @@ def _tile_sums_cpu(sorted_payload: torch.Tensor, kind: int) -> torch.Tensor:
 def test_tile_sum_fold_matches_the_sorted_payload(rows, n, kind, frac):
     """The last onesweep pass's tile-sum fold (sort_desc(fold=...)) against the tile totals of its
     own sorted payload; then auc_scan with the fold equals auc_scan without it."""
+    import os
+
     from torcheval_amd.ops import native
+
+    if os.environ.get("TORCHEVAL_AMD_K3_ONESWEEP") == "0":
+        pytest.skip("the fold rides the onesweep sort, turned off in this process")
 
     g = torch.Generator().manual_seed(rows * 7 + n)
     x = _keys(rows, n, n, 5 if n > 1000 else 0)
