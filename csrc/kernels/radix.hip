@@ -367,6 +367,18 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
 //     row's digit totals once every tile of the row has consumed them (its look-back saw all
 //     of them publish, and each publishes only after its digit-start scan).  Every spin is
 //     bounded (a timeout sets hdr[8]).
+#ifdef TEA_RADIX_TRACE  // csrc/bench/k3_pass_trace.hip: s_memrealtime per phase, thread 0 of every block
+__device__ unsigned long long* g_radix_trace;
+#define RDX_TRACE(i)                                                                             \
+  do {                                                                                           \
+    if (threadIdx.x == 0) g_radix_trace[(static_cast<size_t>(pass) * 4096 + blockIdx.x) * 8 + (i)] = \
+        __builtin_amdgcn_s_memrealtime();                                                        \
+  } while (0)
+#else
+#define RDX_TRACE(i) \
+  do {               \
+  } while (0)
+#endif
 constexpr int kOSMaxTiles = 1024;
 constexpr uint32_t kReady = 0x80000000u;
 constexpr int kSpinLimit = 1 << 22;
@@ -532,6 +544,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   const int w = threadIdx.x >> 6;
   const int64_t tbase = static_cast<int64_t>(tile) * kRTile;
   const int64_t wbase = tbase + static_cast<int64_t>(w) * kSub;
+  RDX_TRACE(0);
   uint32_t k[kRounds], v[kRounds], r[kRounds];
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
@@ -583,6 +596,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     if (valid && pb == 0ull) wc[w][d] += static_cast<uint32_t>(__popcll(peers));
   }
   __syncthreads();
+  RDX_TRACE(1);
   const int P = pass & 1;
   {  // thread t owns digit t
     const int t = threadIdx.x;
@@ -601,6 +615,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     const int g = tile / kGroup;
     os_put(st + static_cast<int64_t>(tile) * kBins + t, kReady | o);
     os_add64(ga + static_cast<int64_t>(g) * kBins + t, (1ull << 32) | o);
+    RDX_TRACE(2);
     uint32_t inc = o;
 #pragma unroll
     for (int s2 = 1; s2 < 64; s2 <<= 1) {
@@ -665,6 +680,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     }
     if (lane == 63) wsum[w] = inc;
     __syncthreads();
+    RDX_TRACE(3);
     uint32_t off = 0;
 #pragma unroll
     for (int q = 0; q < kRWaves; ++q)
@@ -686,6 +702,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     }
   }
   __syncthreads();
+  RDX_TRACE(4);
   const int64_t tn64 = a.n - tbase;
   const int tn = static_cast<int>(tn64 < kRTile ? tn64 : kRTile);
   if constexpr (FOLD) {
@@ -715,6 +732,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
         vals_out[pos] = vv[j];
       }
     }
+    RDX_TRACE(5);
     return;
   }
   for (int p = threadIdx.x; p < tn; p += kRT) {
