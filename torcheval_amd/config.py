@@ -36,11 +36,14 @@ Engine policies (read once per process; not flags):
 
 Kernel A/B knobs (benchmarks only; defaults are the measured winners, ``profiles/README.md``):
 ``TORCHEVAL_AMD_K1_MICRO`` / ``_K1_WPB`` (K1 micro kernel, waves per workgroup),
-``_K3_ONESWEEP`` (0: the upsweep / downsweep sort), ``_K5_V2`` / ``_K5_CG`` / ``_K5_MAXR`` /
+``_K3_ONESWEEP`` (0: the upsweep / downsweep sort), ``_K3_ROUNDS`` (8 / 16 keys per thread),
+``_K3_HIST_ROUNDS`` (onesweep histogram rounds per block), ``_K3_FOLD`` (1: tile sums folded into
+the last onesweep pass, 7 launches, measured slower) / ``_K3_FOLD_PROBE``, ``_K5_V2 / ``_K5_CG`` / ``_K5_MAXR`` /
 ``_K5_BLOCKS`` / ``_K5_PIPE`` / ``_K5_AB_SKIP_FOLD`` (K5 geometry; read per call only with
 ``_AB_DYNAMIC``), ``_K5B_MODE`` / ``_K5B_GRID`` / ``_K5B_PEND_VPT`` (K5b launch shape),
 ``_K8_MODE`` / ``_K8_SPLIT`` / ``_K8_EXACT`` / ``_FID_STAGE_ROWS`` (FID covariance),
-``_PPL_U2`` / ``_PPL_MAXGRID`` (K7), ``_SYMEIG_COOP`` (K9b cooperative launch),
+``_PPL_U2`` / ``_PPL_MAXGRID`` (K7), ``_SYMEIG_COOP`` (K9b cooperative launch), ``_SYMEIG_WAVE``
+(1: the rows-per-wave K9b reduction, measured slower),
 ``_MAX_BLOCKS`` (grid cap), ``_ARCH`` (build target, default gfx950).
 """
 
