@@ -67,12 +67,14 @@ int main() {
   CK(hipMemcpy(tr.data(), trace, tr.size() * 8, hipMemcpyDeviceToHost));
   const char* names[] = {"wait", "R1", "house", "pass", "R3", "publish"};
   for (int b = 0; b < 2; ++b) {
-    std::printf("workgroup %d (cycles): wait R1 house pass R3 publish | phase total\n", b ? 100 : 0);
+    std::printf("workgroup %d (cycles): wait R1 house(update + reflector) pass R3(row publish + reduction) publish | phase total\n",
+                b ? 100 : 0);
     for (int j = 1; j < 16; ++j) {
       const unsigned long long* t = &tr[b * 128 + j * 8];
       const unsigned long long* p = &tr[b * 128 + (j - 1) * 8];
-      std::printf("  j=%d: %llu %llu %llu %llu %llu %llu | %llu\n", 1000 + j, t[0] - p[5], t[1] - t[0],
-                  t[2] - t[1], t[3] - t[2], t[4] - t[3], t[5] - t[4], t[5] - p[5]);
+      std::printf("  j=%d: %llu %llu %llu(%llu + %llu) %llu %llu(%llu + %llu) %llu | %llu\n", 1000 + j, t[0] - p[5],
+                  t[1] - t[0], t[2] - t[1], t[6] - t[1], t[2] - t[6], t[3] - t[2], t[4] - t[3], t[7] - t[3],
+                  t[4] - t[7], t[5] - t[4], t[5] - p[5]);
     }
   }
   (void)names;

@@ -334,6 +334,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       }
     }
 
+    SYM_TRACE(j, 6);
     if (j == n - 3) {
       // last step: row n-2 is final; the owner of row n-1 finishes its diagonal
       if (blockIdx.x == 0) {
@@ -393,6 +394,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
         if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, k, row_elem<C, RM>(rw, ro, s));
       }
     }
+    SYM_TRACE(j, 7);
     const double pt = block_sum_own<RM>(acc, red[2]);
     SYM_TRACE(j, 4);
     if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, row0 + t, hn.tau * pt);
