@@ -9,7 +9,8 @@
 //
 // MI355X design: the whole D x D FP64 matrix lives on chip for the whole reduction, in the
 // vector registers of one workgroup per CU (2048 x 2048 x 8 B = 32 MiB = 256 CUs x 128 KB;
-// each thread holds 8 rows x 8 columns), one cooperative launch.  Workgroup g owns R consecutive rows; the matrix never goes
+// at D = 2048 a 512-thread workgroup, each thread holding 8 rows x 4 columns), one cooperative
+// launch.  Workgroup g owns R consecutive rows; the matrix never goes
 // back to HBM.  Householder tridiagonalisation (unblocked, LAPACK sytd2 semantics) with ONE
 // grid-wide hand-off per column:
 //   phase j publishes p_j = tau_j A v_j for the owned rows (8 B each) and, from the owner of
@@ -120,26 +121,26 @@ __device__ __forceinline__ void row_partials(const double (&v)[N], double* scrat
 }
 
 // every thread gets every total
-template <int N>
+template <int N, int NT = kThreads>
 __device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
   row_partials<N>(v, scratch);
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     double s = 0.0;
 #pragma unroll
-    for (int q = 0; q < 16; ++q) s += scratch[q * N + i];
+    for (int q = 0; q < NT / 16; ++q) s += scratch[q * N + i];
     v[i] = s;
   }
 }
 
 // thread t < N gets total t (the per-row p values, published by thread t)
-template <int N>
+template <int N, int NT = kThreads>
 __device__ __forceinline__ double block_sum_own(const double (&v)[N], double* scratch) {
   row_partials<N>(v, scratch);
   double s = 0.0;
   if (threadIdx.x < N) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) s += scratch[q * N + threadIdx.x];
+    for (int q = 0; q < NT / 16; ++q) s += scratch[q * N + threadIdx.x];
   }
   return s;
 }
@@ -150,7 +151,7 @@ struct Reflector {
 
 // LAPACK dlarfg on x = a[j+1 .. n): alpha = a[j+1], sigma = sum_{k >= j+2} a[k]^2; also
 // broadcasts the diagonal a[j].  v[k] = 1 at k = j+1, a[k] * scale beyond, 0 before.
-template <int C>
+template <int C, int NT = kThreads>
 __device__ __forceinline__ Reflector householder(const double (&a)[C], int j, int n,
                                                  double* scratch, double* bcast) {
   // sigma by the block reduction; alpha = a[j+1] and the diagonal a[j] are single elements,
@@ -159,13 +160,13 @@ __device__ __forceinline__ Reflector householder(const double (&a)[C], int j, in
   double r[1] = {0.0};
 #pragma unroll
   for (int s = 0; s < C; ++s) {
-    const int k = threadIdx.x + s * kThreads;
+    const int k = threadIdx.x + s * NT;
     const double x = a[s];
     r[0] += (k >= j + 2 && k < n) ? x * x : 0.0;
     if (k == j + 1) bcast[0] = x;
     if (k == j) bcast[1] = x;
   }
-  block_sum<1>(r, scratch);
+  block_sum<1, NT>(r, scratch);
   Reflector h;
   const double sigma = r[0], alpha = bcast[0];
   h.diag = bcast[1];
@@ -182,12 +183,12 @@ __device__ __forceinline__ Reflector householder(const double (&a)[C], int j, in
   return h;
 }
 
-template <int C>
+template <int C, int NT = kThreads>
 __device__ __forceinline__ void make_v(const double (&a)[C], const Reflector& h, int j,
                                        double (&v)[C]) {
 #pragma unroll
   for (int s = 0; s < C; ++s) {
-    const int k = threadIdx.x + s * kThreads;
+    const int k = threadIdx.x + s * NT;
     v[s] = k == j + 1 ? 1.0 : (k >= j + 2 ? a[s] * h.scale : 0.0);
   }
 }
@@ -210,12 +211,14 @@ __device__ __forceinline__ double row_elem(const double (&rw)[RM][C], int r, int
 // LDS-bandwidth bound, ~16 B of LDS traffic per element per column).  Slot planes of
 // [n - 2, ld] each at slots + {0, 1} * plane: p_q, then row q+1 (as updated through step q-1);
 // all sentinel-filled by the launcher.  ctl[1] = abort word, zeroed by the launcher.
-template <int C, int RM>
-__global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restrict__ A, int n,
-                                                           int R, int64_t ld, double* d_out,
-                                                           double* e_out, unsigned long long* slots,
-                                                           unsigned* ctl) {
-  __shared__ double red[3][16 * RM];
+// NT threads per workgroup (256, or 512 for the two-waves-per-SIMD A/B arm: half the columns
+// per thread, twice the row partials per reduction)
+template <int C, int RM, int NT = kThreads>
+__global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ A, int n,
+                                                     int R, int64_t ld, double* d_out,
+                                                     double* e_out, unsigned long long* slots,
+                                                     unsigned* ctl) {
+  __shared__ double red[3][(NT / 16) * RM];
   __shared__ double bc[2][4];  // single-element broadcasts riding on the reductions' barriers
   __shared__ double vw[2][RM];
   const int64_t plane = (int64_t)(n - 2) * ld;
@@ -225,26 +228,26 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
   const int t = threadIdx.x;
   const int row0 = blockIdx.x * R;
   const int nrows = min(R, n - row0);
-  double rw[RM][C];  // owned row r, column t + s * kThreads
+  double rw[RM][C];  // owned row r, column t + s * NT
 #pragma unroll
   for (int r = 0; r < RM; ++r)
 #pragma unroll
     for (int s = 0; s < C; ++s) {
-      const int k = t + s * kThreads;
+      const int k = t + s * NT;
       rw[r][s] = (r < nrows && k < n) ? A[(int64_t)(row0 + r) * n + k] : 0.0;
     }
 
   double a[C], v[C], w[C], vn[C];
 #pragma unroll
   for (int s = 0; s < C; ++s) {
-    const int k = t + s * kThreads;
+    const int k = t + s * NT;
     a[s] = k < n ? A[k] : 0.0;  // row 0
   }
   __syncthreads();
 
   // ---- phase 0: reflector 0 and p_0 from the original rows
-  Reflector h = householder(a, 0, n, red[0], bc[0]);
-  make_v(a, h, 0, v);
+  Reflector h = householder<C, NT>(a, 0, n, red[0], bc[0]);
+  make_v<C, NT>(a, h, 0, v);
   if (blockIdx.x == 0 && t == 0) {
     d_out[0] = h.diag;
     e_out[0] = h.beta;
@@ -257,17 +260,17 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       if (r < nrows) {
 #pragma unroll
         for (int s = 0; s < C; ++s) {
-          const int k = t + s * kThreads;
+          const int k = t + s * NT;
           if (k < n) acc[r] += rw[r][s] * v[s];
         }
       }
     }
-    const double pt = block_sum_own<RM>(acc, red[2]);
+    const double pt = block_sum_own<RM, NT>(acc, red[2]);
     if (t < nrows && row0 + t >= 1) put(gp0, row0 + t, h.tau * pt);
     if (1 >= row0 && 1 < row0 + nrows) {
 #pragma unroll
       for (int s = 0; s < C; ++s) {
-        const int k = t + s * kThreads;
+        const int k = t + s * NT;
         if (k >= 1 && k < n) put(gr0, k, row_elem<C, RM>(rw, 1 - row0, s));
       }
     }
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       bool ok = true;
 #pragma unroll
       for (int s = 0; s < C; ++s) {
-        const int k = t + s * kThreads;
+        const int k = t + s * NT;
         if (k >= j + 1 && k < n) {
           const unsigned long long x0 = get(gp + k), y0 = get(gr + k);
           ok = ok && x0 != kSentBits && y0 != kSentBits;
@@ -314,11 +317,11 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     double r1[1] = {0.0};
 #pragma unroll
     for (int s = 0; s < C; ++s) {
-      const int k = t + s * kThreads;
+      const int k = t + s * NT;
       r1[0] += w[s] * v[s];
       if (k == j + 1) bc[0][2] = w[s];  // p_j[j+1], published by the reduction's barrier
     }
-    block_sum<1>(r1, red[0]);
+    block_sum<1, NT>(r1, red[0]);
     SYM_TRACE(j, 1);
     const double c = 0.5 * h.tau * r1[0];
     const double wj1 = bc[0][2] - c;  // w_j[j+1] (v_j[j+1] = 1)
@@ -326,7 +329,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     for (int s = 0; s < C; ++s) {
       w[s] -= c * v[s];
       a[s] -= w[s] + wj1 * v[s];  // row j+1 <- row j+1 - v_j[j+1] w_j - w_j[j+1] v_j
-      const int k = t + s * kThreads;
+      const int k = t + s * NT;
       const int r = k - row0;
       if (r >= 0 && r < nrows) {  // the owned rows' v_j[i], w_j[i] for the rank-2 update
         vw[0][r] = v[s];
@@ -340,7 +343,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       if (blockIdx.x == 0) {
 #pragma unroll
         for (int s = 0; s < C; ++s) {
-          const int k = t + s * kThreads;
+          const int k = t + s * NT;
           if (k == n - 2) d_out[n - 2] = a[s];
           if (k == n - 1) e_out[n - 2] = a[s];
         }
@@ -350,7 +353,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
       if (r >= 0 && r < nrows) {
 #pragma unroll
         for (int s = 0; s < C; ++s) {
-          const int k = t + s * kThreads;
+          const int k = t + s * NT;
           if (k == n - 1) d_out[n - 1] = row_elem<C, RM>(rw, r, s) - 2.0 * vw[0][r] * vw[1][r];
         }
       }
@@ -358,8 +361,8 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     }
 
     // ---- reflector j+1 (redundant in every workgroup)
-    const Reflector hn = householder(a, j + 1, n, red[1], bc[1]);  // its barrier publishes vw
-    make_v(a, hn, j + 1, vn);
+    const Reflector hn = householder<C, NT>(a, j + 1, n, red[1], bc[1]);  // its barrier publishes vw
+    make_v<C, NT>(a, hn, j + 1, vn);
     SYM_TRACE(j, 2);
     if (blockIdx.x == 0 && t == 0) {
       d_out[j + 1] = hn.diag;
@@ -390,12 +393,12 @@ __global__ __launch_bounds__(kThreads) void tridiag_kernel(const double* __restr
     if (ro >= 0 && ro < nrows) {
 #pragma unroll
       for (int s = 0; s < C; ++s) {
-        const int k = t + s * kThreads;
+        const int k = t + s * NT;
         if (k >= j + 2 && k < n) put(gr0 + (int64_t)(j + 1) * ld, k, row_elem<C, RM>(rw, ro, s));
       }
     }
     SYM_TRACE(j, 7);
-    const double pt = block_sum_own<RM>(acc, red[2]);
+    const double pt = block_sum_own<RM, NT>(acc, red[2]);
     SYM_TRACE(j, 4);
     if (t < nrows && row0 + t >= j + 2) put(gp0 + (int64_t)(j + 1) * ld, row0 + t, hn.tau * pt);
 #pragma unroll
@@ -849,6 +852,39 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
                      : need <= 8 ? reinterpret_cast<const void*>(&tridiag_kernel<8, 8>)
                      : need <= 9 ? reinterpret_cast<const void*>(&tridiag_kernel<9, 9>)
                                  : reinterpret_cast<const void*>(&tridiag_kernel<kMaxCols, kMaxRows>);
+  // 512-thread workgroups over the same rows (two waves per SIMD, half the columns per thread)
+  // where the 256-thread instance is the 8 x 8 one (1536 < n <= 2048, the FID's D = 2048): that
+  // instance holds 256 VGPRs + AGPRs at one wave per SIMD, and every dependent FP64 chain of the
+  // pass and the reductions stalls; 512 threads: 12.9 vs 14.7 ms at D = 2048, but 2-5% slower at
+  // D = 512 / 1000, where the 256-thread instances are small (profiles/symeig_nt_ab_r5.json).
+  // TORCHEVAL_AMD_SYMEIG_NT=256 / 512 / 1024 forces a size (A/B; 1024 measured slower everywhere)
+  static const int nt_env = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_NT");
+    return e ? std::atoi(e) : 0;
+  }();
+  int nt = kThreads;
+  if (nt_env == 512 || (nt_env == 0 && need > 6 && need <= 8)) {
+    const int64_t c = (a.n + 511) / 512;
+    const void* k512 = (c <= 1 && R <= 2)    ? reinterpret_cast<const void*>(&tridiag_kernel<1, 2, 512>)
+                       : (c <= 2 && R <= 4)  ? reinterpret_cast<const void*>(&tridiag_kernel<2, 4, 512>)
+                       : (c <= 3 && R <= 6)  ? reinterpret_cast<const void*>(&tridiag_kernel<3, 6, 512>)
+                       : (c <= 4 && R <= 8)  ? reinterpret_cast<const void*>(&tridiag_kernel<4, 8, 512>)
+                                             : nullptr;  // (5 x 10 spills: n > 2048 stays at 256)
+    if (k512) {
+      kern = k512;
+      nt = 512;
+    }
+  } else if (nt_env == 1024) {
+    const int64_t c = (a.n + 1023) / 1024;
+    const void* k1k = (c <= 1 && R <= 2)    ? reinterpret_cast<const void*>(&tridiag_kernel<1, 2, 1024>)
+                      : (c <= 1 && R <= 4)  ? reinterpret_cast<const void*>(&tridiag_kernel<1, 4, 1024>)
+                      : (c <= 2 && R <= 8)  ? reinterpret_cast<const void*>(&tridiag_kernel<2, 8, 1024>)
+                                            : nullptr;  // (3 x 10 spills: n > 2048 stays at 256)
+    if (k1k) {
+      kern = k1k;
+      nt = 1024;
+    }
+  }
   if (hipMemsetAsync(a.ctl, 0, kCtlBytes, stream) != hipSuccess) return 2;
   if (hipMemsetAsync(a.slots, 0xff, (size_t)symeig_slot_bytes(a.n), stream) != hipSuccess) return 2;
   const double* A = a.a;
@@ -869,8 +905,9 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   const void* lk = wkern ? wkern : kern;
   void** la = wkern ? wargs : args;
   const int lg = wkern ? GW : G;
-  const hipError_t lrc = coop ? hipLaunchCooperativeKernel(lk, dim3(lg), dim3(kThreads), la, 0, stream)
-                              : hipLaunchKernel(lk, dim3(lg), dim3(kThreads), la, 0, stream);
+  const int lt = wkern ? kThreads : nt;
+  const hipError_t lrc = coop ? hipLaunchCooperativeKernel(lk, dim3(lg), dim3(lt), la, 0, stream)
+                              : hipLaunchKernel(lk, dim3(lg), dim3(lt), la, 0, stream);
   if (lrc != hipSuccess) return 3;
   sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
   if (n >= 1536)
