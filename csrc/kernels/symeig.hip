@@ -121,28 +121,34 @@ __device__ __forceinline__ void row_partials(const double (&v)[N], double* scrat
 }
 
 // every thread gets every total
+// the NT / 16 row partials of one value, added as a pairwise tree (depth log2 instead of a
+// chain of NT / 16 dependent FP64 adds; fixed order, so still deterministic)
+template <int N, int NT>
+__device__ __forceinline__ double tree_partials(const double* scratch, int i) {
+  constexpr int NP = NT / 16;
+  double p[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) p[q] = scratch[q * N + i];
+#pragma unroll
+  for (int w = NP / 2; w >= 1; w /= 2) {
+#pragma unroll
+    for (int q = 0; q < w; ++q) p[q] += p[q + w];
+  }
+  return p[0];
+}
+
 template <int N, int NT = kThreads>
 __device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
   row_partials<N>(v, scratch);
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    double s = 0.0;
-#pragma unroll
-    for (int q = 0; q < NT / 16; ++q) s += scratch[q * N + i];
-    v[i] = s;
-  }
+  for (int i = 0; i < N; ++i) v[i] = tree_partials<N, NT>(scratch, i);
 }
 
 // thread t < N gets total t (the per-row p values, published by thread t)
 template <int N, int NT = kThreads>
 __device__ __forceinline__ double block_sum_own(const double (&v)[N], double* scratch) {
   row_partials<N>(v, scratch);
-  double s = 0.0;
-  if (threadIdx.x < N) {
-#pragma unroll
-    for (int q = 0; q < NT / 16; ++q) s += scratch[q * N + threadIdx.x];
-  }
-  return s;
+  return threadIdx.x < N ? tree_partials<N, NT>(scratch, threadIdx.x) : 0.0;
 }
 
 struct Reflector {
