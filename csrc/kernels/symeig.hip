@@ -104,11 +104,12 @@ __device__ __forceinline__ double row16_sum(double x) {
   return x;
 }
 
-// Block-wide sums of N values: the 16 row sums of the block (4 waves x 4 rows) go to LDS
-// straight from lane 15 of each row, one barrier, then the 16 partials are added in a fixed
-// order.  `scratch` holds 16 * N doubles; callers rotate scratch slots so consecutive
-// reductions need one barrier each.  (Readlane-ing the 4 row sums of every wave first took
-// ~15% more of the column's cycles, profiles/k9b_phase_trace_r2.txt.)
+// Block-wide sums of N values: the NT / 16 row sums of the block go to LDS from the row's
+// lanes, one barrier, then the partials are added as a fixed-order tree.  `scratch` holds
+// (NT / 16) * N doubles; callers rotate scratch slots so consecutive reductions need one barrier
+// each.  (Readlane-ing the 4 row sums of every wave first took ~15% more of the column's
+// cycles, profiles/k9b_phase_trace_r2.txt; DPP transposes / row broadcasts instead, round 5:
+// profiles/symeig_timing_dpp_reductions_r5.json.)
 template <int N>
 __device__ __forceinline__ void row_partials(const double (&v)[N], double* scratch) {
   if constexpr (N == 8) {
@@ -161,11 +162,38 @@ __device__ __forceinline__ double tree_partials(const double* scratch, int i) {
   return p[0];
 }
 
+template <int Ctrl, int RowMask>
+__device__ __forceinline__ double dpp_f64_rows(double x) {  // 0 in the rows RowMask leaves out
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(x), Ctrl, RowMask, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(x), Ctrl, RowMask, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+
 template <int N, int NT = kThreads>
 __device__ __forceinline__ void block_sum(double (&v)[N], double* scratch) {
-  row_partials<N>(v, scratch);
+  if constexpr (N == 1) {
+    // one value: the wave total by DPP (row sums, then row_bcast:15 / row_bcast:31 into lane
+    // 63), so the tree below adds NT / 64 wave partials instead of NT / 16 row partials
+    double x = row16_sum(v[0]);
+    x += dpp_f64_rows<0x142, 0xa>(x);
+    x += dpp_f64_rows<0x143, 0xc>(x);
+    if ((threadIdx.x & 63) == 63) scratch[threadIdx.x >> 6] = x;
+    __syncthreads();
+    constexpr int NP = NT / 64;
+    double q[NP];
 #pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = tree_partials<N, NT>(scratch, i);
+    for (int k = 0; k < NP; ++k) q[k] = scratch[k];
+#pragma unroll
+    for (int w = NP / 2; w >= 1; w /= 2) {
+#pragma unroll
+      for (int k = 0; k < w; ++k) q[k] += q[k + w];
+    }
+    v[0] = q[0];
+  } else {
+    row_partials<N>(v, scratch);
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = tree_partials<N, NT>(scratch, i);
+  }
 }
 
 // thread t < N gets total t (the per-row p values, published by thread t)
