@@ -399,6 +399,9 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
     unsigned long long* const gr = gr0 + (int64_t)j * ld;
     bool aborted = false;
     for (unsigned spins = 0;; ++spins) {
+      // the abort word is loaded with the slots, in the same round trip (loaded after a failed
+      // poll it doubled every poll period: one more ~1 us round trip before the next poll)
+      const unsigned abort_word = __hip_atomic_load((gu32*)&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       bool ok = true;
 #pragma unroll
       for (int s = 0; s < C; ++s) {
@@ -414,7 +417,7 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
         }
       }
       if (ok) break;
-      if (__hip_atomic_load((gu32*)&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      if (abort_word != 0u) {
         aborted = true;
         break;
       }
@@ -644,6 +647,7 @@ __global__ __launch_bounds__(kThreads, 1) void tridiag_wave_kernel(const double*
     double* const R = sr[j & 1];
     bool aborted = false;
     for (unsigned spins = 0;; ++spins) {
+      const unsigned abort_word = __hip_atomic_load((gu32*)&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       bool ok = true;
 #pragma unroll
       for (int q = 0; q < kQ; ++q) {
@@ -659,7 +663,7 @@ __global__ __launch_bounds__(kThreads, 1) void tridiag_wave_kernel(const double*
         }
       }
       if (ok) break;
-      if (__hip_atomic_load((gu32*)&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      if (abort_word != 0u) {
         aborted = true;
         break;
       }
