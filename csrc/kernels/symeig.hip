@@ -402,19 +402,24 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
       // the abort word is loaded with the slots, in the same round trip (loaded after a failed
       // poll it doubled every poll period: one more ~1 us round trip before the next poll)
       const unsigned abort_word = __hip_atomic_load((gu32*)&ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // every slot load issued unconditionally (dead columns read a live slot, masked after): a
+      // per-lane `if (live) load` can compile to a branch and a wait per column
+      unsigned long long xs[C], ys[C];
+#pragma unroll
+      for (int s = 0; s < C; ++s) {
+        const int k = t + s * NT;
+        const int kc = k < j + 1 ? j + 1 : (k < n ? k : n - 1);
+        xs[s] = get(gp + kc);
+        ys[s] = get(gr + kc);
+      }
       bool ok = true;
 #pragma unroll
       for (int s = 0; s < C; ++s) {
         const int k = t + s * NT;
-        if (k >= j + 1 && k < n) {
-          const unsigned long long x0 = get(gp + k), y0 = get(gr + k);
-          ok = ok && x0 != kSentBits && y0 != kSentBits;
-          w[s] = as_double(x0);
-          a[s] = as_double(y0);
-        } else {
-          w[s] = 0.0;
-          a[s] = 0.0;
-        }
+        const bool live = k >= j + 1 && k < n;
+        ok = ok && (!live || (xs[s] != kSentBits && ys[s] != kSentBits));
+        w[s] = live ? as_double(xs[s]) : 0.0;
+        a[s] = live ? as_double(ys[s]) : 0.0;
       }
       if (ok) break;
       if (abort_word != 0u) {
