@@ -781,15 +781,22 @@ __global__ __launch_bounds__(kThreads, 1) void tridiag_wave_kernel(const double*
 }
 
 // # eigenvalues of the tridiagonal (d, e2 = e^2) below x (LAPACK dstebz's Sturm count).
-// (A v_rcp_f64 + Newton reciprocal with two interleaved chains per lane measured 13% slower
-// than this plain division at D = 2048: 2.15 vs 1.9 ms.)
+// (Round 3: the bare v_rcp_f64 was faster but cost 6e-9 of accuracy, and rcp + Newton with two
+// interleaved chains per lane measured 13% slower; round 5: one chain, rcp + one Newton step,
+// D = 2048 eigenvalues 9.85 -> 9.40 ms at unchanged accuracy, profiles/symeig_timing_sturm_rcp_newton_r5.json.)
 __device__ __forceinline__ int sturm_count(const double* d, const double* e2, int n, double x,
                                            double pivmin) {
   double q = d[0] - x;
   if (fabs(q) < pivmin) q = -pivmin;
   int cnt = q < 0.0;
   for (int k = 1; k < n; ++k) {
-    q = d[k] - x - e2[k - 1] / q;
+    // e2 / q as e2 * (v_rcp_f64 + one Newton step): 4 dependent ops on the recurrence's critical
+    // path instead of the IEEE division's ~9.  q is finite and |q| >= pivmin >= DBL_MIN (normal),
+    // and e2 / |q| <= 1 / DBL_MIN, so no overflow / denormal special case arises (LAPACK's pivmin
+    // argument); the refined reciprocal is within an ulp or two of the quotient's
+    double r = __builtin_amdgcn_rcp(q);
+    r = fma(r, fma(-q, r, 1.0), r);
+    q = d[k] - x - e2[k - 1] * r;
     if (fabs(q) < pivmin) q = -pivmin;
     cnt += q < 0.0;
   }
