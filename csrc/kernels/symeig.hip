@@ -1041,8 +1041,18 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
                               : hipLaunchKernel(lk, dim3(lg), dim3(lt), la, 0, stream);
   if (lrc != hipSuccess) return 3;
   sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
-  if (n >= 1536)
+  // lanes per eigenvalue: 32 from D = 1536 (with the rcp + Newton Sturm steps 32 lanes edge out
+  // 16: 9.34-9.36 vs 9.40-9.42 ms at D = 2048, profiles/symeig_L_ab_r5.json), else 64;
+  // TORCHEVAL_AMD_SYMEIG_L=16 / 32 / 64 forces (A/B)
+  static const int l_env = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_L");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int L = (l_env == 16 || l_env == 32 || l_env == 64) ? l_env : (n >= 1536 ? 32 : 64);
+  if (L == 16)
     tridiag_eigvals_kernel<16><<<(n + kWaves * 4 - 1) / (kWaves * 4), kThreads, 0, stream>>>(d, e, n, a.grid, a.lam);
+  else if (L == 32)
+    tridiag_eigvals_kernel<32><<<(n + kWaves * 2 - 1) / (kWaves * 2), kThreads, 0, stream>>>(d, e, n, a.grid, a.lam);
   else
     tridiag_eigvals_kernel<64><<<(n + kWaves - 1) / kWaves, kThreads, 0, stream>>>(d, e, n, a.grid, a.lam);
   return hipGetLastError() == hipSuccess ? 0 : 2;
