@@ -334,6 +334,7 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
   __shared__ double red[3][(NT / 16) * RM];
   __shared__ double bc[2][4];  // single-element broadcasts riding on the reductions' barriers
   __shared__ double vw[2][RM];
+  __shared__ int s_abort;  // a poll timed out / saw the abort word (read after R1's barrier)
   const int64_t plane = (int64_t)(n - 2) * ld;
   unsigned long long* const gp0 = slots;          // p plane
   unsigned long long* const gr0 = slots + plane;  // row plane
@@ -356,6 +357,7 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
     const int k = t + s * NT;
     a[s] = k < n ? A[k] : 0.0;  // row 0
   }
+  if (t == 0) s_abort = 0;
   __syncthreads();
 
   // ---- phase 0: reflector 0 and p_0 from the original rows
@@ -433,7 +435,9 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    if (__syncthreads_or(aborted)) return;
+    // no barrier of its own: the abort vote rides R1's reduction barrier (every LDS slot it
+    // writes was last read before the previous column's reflector barrier)
+    if (aborted) s_abort = 1;
     SYM_TRACE(j, 0);
     double r1[1] = {0.0};
 #pragma unroll
@@ -443,6 +447,7 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
       if (k == j + 1) bc[0][2] = w[s];  // p_j[j+1], published by the reduction's barrier
     }
     block_sum<1, NT>(r1, red[0]);
+    if (s_abort) return;  // block-uniform
     SYM_TRACE(j, 1);
     const double c = 0.5 * h.tau * r1[0];
     const double wj1 = bc[0][2] - c;  // w_j[j+1] (v_j[j+1] = 1)
