@@ -112,35 +112,11 @@ __device__ __forceinline__ double row16_sum(double x) {
 // profiles/symeig_timing_dpp_reductions_r5.json.)
 template <int N>
 __device__ __forceinline__ void row_partials(const double (&v)[N], double* scratch) {
-  if constexpr (N == 8) {
-    // eight values (the p reduction of 8 owned rows): a transposing reduction - each exchange
-    // step halves the values a lane keeps and doubles the lanes each is summed over (row
-    // mirror, half-row mirror, quad reverse, quad swap): 8 DPP exchanges instead of 8 x 4, and
-    // the 8 row sums leave from 8 lanes in one LDS store
-    const int p = threadIdx.x & 15;
-    const bool b3 = (p & 8) != 0, b2 = (p & 4) != 0, b1 = (p & 2) != 0;
-    double u1[4], u2[2];
+  const bool tail = (threadIdx.x & 15) == 15;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {  // keep values 4 * b3 + k, summed with lane 15 - p
-      const double send = b3 ? v[k] : v[k + 4], keep = b3 ? v[k + 4] : v[k];
-      u1[k] = keep + dpp_f64<0x140>(send);
-    }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {  // keep values 4 * b3 + 2 * b2 + k, with lane p ^ 7
-      const double send = b2 ? u1[k] : u1[k + 2], keep = b2 ? u1[k + 2] : u1[k];
-      u2[k] = keep + dpp_f64<0x141>(send);
-    }
-    const double send3 = b1 ? u2[0] : u2[1], keep3 = b1 ? u2[1] : u2[0];
-    double u = keep3 + dpp_f64<0x1B>(send3);  // value 4 * b3 + 2 * b2 + b1, with lane p ^ 3
-    u += dpp_f64<0xB1>(u);                    // with lane p ^ 1: the 16-lane row sum
-    if (!(p & 1)) scratch[(threadIdx.x >> 4) * 8 + (b3 ? 4 : 0) + (b2 ? 2 : 0) + (b1 ? 1 : 0)] = u;
-  } else {
-    const bool tail = (threadIdx.x & 15) == 15;
-#pragma unroll
-    for (int i = 0; i < N; ++i) {
-      const double x = row16_sum(v[i]);
-      if (tail) scratch[(threadIdx.x >> 4) * N + i] = x;
-    }
+  for (int i = 0; i < N; ++i) {
+    const double x = row16_sum(v[i]);
+    if (tail) scratch[(threadIdx.x >> 4) * N + i] = x;
   }
   __syncthreads();
 }
@@ -218,8 +194,11 @@ __device__ __forceinline__ double perm_pair_sum32(double x) {
 template <int N, int NT = kThreads>
 __device__ __forceinline__ double block_sum_own(const double (&v)[N], double* scratch) {
   if constexpr (N == 8) {
-    // the transposing row reduction, then the 4 rows of the wave by permlane swaps: NT / 64
-    // wave partials per value instead of NT / 16 row partials (11.05 -> 10.93 ms at D = 2048)
+    // eight values (the p reduction of 8 owned rows): a transposing reduction inside each
+    // 16-lane row - every exchange step halves the values a lane keeps and doubles the lanes each
+    // is summed over (row mirror, half-row mirror, quad reverse, quad swap: 8 DPP exchanges
+    // instead of 8 x 4, 12.17 -> 11.86 ms at D = 2048) - then the 4 rows of the wave by permlane
+    // swaps: NT / 64 wave partials per value instead of NT / 16 row partials (-> 10.93 ms)
     const int p = threadIdx.x & 15;
     const bool b3 = (p & 8) != 0, b2 = (p & 4) != 0, b1 = (p & 2) != 0;
     double u1[4], u2[2];
