@@ -24,7 +24,8 @@ the elapsed time, max-reduced over ranks.
 Rehearsal switches (not used by the driver): ``BENCH_BACKEND=gloo`` runs the multi-rank path
 over gloo, ``BENCH_DEVICE=cpu`` on CPU tensors (so the exact ``torchrun --nproc-per-node 8``
 launch can be exercised without GPUs, tests/test_bench_rehearsal.py), ``BENCH_EXTRAS=0`` skips
-the secondary sync timings.
+the secondary sync timings, ``BENCH_EXTRAS=sync`` runs only the sync diagnostics (the headline's
+own closing sync, its path, the direct-RCCL arm).
 """
 
 import argparse
@@ -72,26 +73,50 @@ def _reference_eager_rate(x_pool, y_pool, iters: int) -> float:
     return iters / (time.perf_counter() - t0)
 
 
-def _sync_extras(dev: torch.device, world: int, barrier) -> dict:
-    """BASELINE.json secondary configs at N > 1 (max over ranks, ms per call): RCCL sync of a
-    1000x1000 confusion matrix, of BinaryAUROC's 1M samples per rank (all-gather-v + K3a sort
-    of the union), and of FID's D=2048 states (one all-reduce of 2 x 16 MB + sums)."""
-    from torcheval_amd.metrics import BinaryAUROC, MulticlassConfusionMatrix
+def _sync_path(metric) -> str:
+    """Which engine the metric's last sync took: ``direct-rccl`` (the sync engine's own RCCL
+    communicator, one grouped call) or ``c10d`` (torch.distributed collectives + seg_reduce)."""
+    from torcheval_amd.parallel.state_buffer import buffer_of
+
+    plans = list(buffer_of(metric).plans.values())
+    if not plans:
+        return "none"
+    return "direct-rccl" if any(p.comm is not None for p in plans) else "c10d"
+
+
+def _sync_extras(dev: torch.device, world: int, barrier, headline_metric) -> dict:
+    """Diagnostics at N > 1, after the headline is final (max over ranks, ms per call):
+
+    * the headline's own closing ``sync_and_compute(MulticlassAccuracy)`` and the path it took
+      (``sync_path``: c10d by default at ws > 1, parallel/rccl_direct.py policy);
+    * a direct-RCCL arm: ``TORCHEVAL_AMD_DIRECT_RCCL=1`` set identically on every rank, fresh
+      metrics (new state buffers, so new plans), so the engine's bootstrap + self-check + MIN
+      vote run here for the first time at this world size; the accuracy and CM(1000) syncs are
+      timed again and ``sync_path`` says whether the vote kept the direct path or fell back;
+    * BASELINE.json secondary configs: RCCL sync of a 1000x1000 confusion matrix, of
+      BinaryAUROC's 1M samples per rank (all-gather-v + K3a sort of the union), and of FID's
+      D=2048 states (one all-reduce of 2 x 16 MB + sums)."""
+    from torcheval_amd.metrics import BinaryAUROC, MulticlassAccuracy, MulticlassConfusionMatrix
     from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
     from torcheval_amd.metrics.toolkit import get_synced_metric, sync_and_compute
 
     out = {}
     g = torch.Generator(device=dev).manual_seed(7 + dist.get_rank())
+    only_sync = os.environ.get("BENCH_EXTRAS", "1") == "sync"  # the rehearsal's subset
+
+    def dsync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
 
     def timed(name, fn, reps):
         try:
             fn()
-            torch.cuda.synchronize()
+            dsync()
             barrier()
             t0 = time.perf_counter()
             for _ in range(reps):
                 fn()
-            torch.cuda.synchronize()
+            dsync()
             barrier()
             t = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64)
             if dist.get_backend() == "nccl":
@@ -101,9 +126,34 @@ def _sync_extras(dev: torch.device, world: int, barrier) -> dict:
         except Exception as e:  # an extra must never cost the headline number
             out[name] = f"error: {type(e).__name__}: {e}"[:160]
 
+    # the headline metric's own closing sync (its state: world * steps * 8192 counted samples)
+    timed("accuracy_sync_and_compute", lambda: sync_and_compute(headline_metric), 20)
+    out["sync_path"] = _sync_path(headline_metric)
     cm = MulticlassConfusionMatrix(1000, device=dev)
     cm.update(torch.randn(8192, 1000, device=dev, generator=g), torch.randint(0, 1000, (8192,), device=dev, generator=g))
     timed("confusion_matrix_1000_sync_and_compute", lambda: sync_and_compute(cm), 20)
+
+    # direct-RCCL arm (opt-in policy at ws > 1): same env on every rank, fresh state buffers
+    prev = os.environ.get("TORCHEVAL_AMD_DIRECT_RCCL")
+    os.environ["TORCHEVAL_AMD_DIRECT_RCCL"] = "1"
+    try:
+        acc_d = MulticlassAccuracy(device=dev)
+        acc_d.update(torch.randn(8192, 1000, device=dev, generator=g), torch.randint(0, 1000, (8192,), device=dev, generator=g))
+        timed("direct_accuracy_sync_and_compute", lambda: sync_and_compute(acc_d), 20)
+        cm_d = MulticlassConfusionMatrix(1000, device=dev)
+        cm_d.update(torch.randn(8192, 1000, device=dev, generator=g), torch.randint(0, 1000, (8192,), device=dev, generator=g))
+        timed("direct_confusion_matrix_1000_sync_and_compute", lambda: sync_and_compute(cm_d), 20)
+        try:
+            out["direct_sync_path"] = _sync_path(acc_d)
+        except Exception as e:  # noqa: BLE001
+            out["direct_sync_path"] = f"error: {type(e).__name__}: {e}"[:160]
+    finally:
+        if prev is None:
+            os.environ.pop("TORCHEVAL_AMD_DIRECT_RCCL", None)
+        else:
+            os.environ["TORCHEVAL_AMD_DIRECT_RCCL"] = prev
+    if only_sync:
+        return out
     auroc = BinaryAUROC(device=dev)
     auroc.update(torch.rand(1_000_000, device=dev, generator=g), torch.randint(0, 2, (1_000_000,), device=dev, generator=g))
     timed("binary_auroc_1M_per_rank_sync_and_compute", lambda: sync_and_compute(auroc), 5)
@@ -270,7 +320,7 @@ def main() -> None:
         watchdog = threading.Timer(float(os.environ.get("BENCH_EXTRAS_BUDGET_S", "180")), _bail)
         watchdog.daemon = True
         watchdog.start()
-        extras = _sync_extras(dev, world, barrier)
+        extras = _sync_extras(dev, world, barrier, metric)
         watchdog.cancel()
         if rank == 0:
             out["sync_ms"] = extras

@@ -136,3 +136,51 @@ def test_sum_mean_deferred_long_rows():
     s.merge_state([s2])
     assert float(s.weighted_sum) == pytest.approx(2 * float(x.double().sum()), rel=1e-10, abs=1e-6)
     assert float(s.state_dict()["weighted_sum"]) == pytest.approx(2 * float(x.double().sum()), rel=1e-10, abs=1e-6)
+
+
+def test_graph_replays_fold_every_replay():
+    """a HIP-graph replay of a deferred update adds to the pending slots with
+    no Python running, so the fold after it must still cover the captured update's slots."""
+    import warnings
+
+    from torcheval_amd.metrics import Mean, Sum
+    from torcheval_amd.utils.graphs import GraphedUpdate
+
+    g = torch.Generator().manual_seed(21)
+    xs, ys = zip(*[_data(4096, 1001, 30 + s) for s in range(4)])
+    m = MeanSquaredError(multioutput="raw_values", device=DEV)
+    xd, yd = xs[0].to(DEV), ys[0].to(DEV)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", RuntimeWarning)  # replay-vs-direct speed warning
+        step = GraphedUpdate(m, xd, yd)
+    assert float(m.sum_weight) == 0.0 and not bool(m.sum_squared_error.any())  # capture restored
+    seen_x, seen_y = [], []
+    for i in range(6):
+        x, y = xs[i % 4], ys[i % 4]
+        step(x.to(DEV), y.to(DEV))
+        seen_x.append(x)
+        seen_y.append(y)
+        if i % 2 == 1:  # compute() between replays folds; later replays must fold again
+            ref = _sse(seen_x, seen_y) / (4096 * len(seen_x))
+            torch.testing.assert_close(m.compute().cpu().double(), ref, rtol=1e-6, atol=1e-6)
+    # an eager update of the same metric between replays, then replays again
+    m.update(xs[1].to(DEV), ys[1].to(DEV))
+    step(xs[2].to(DEV), ys[2].to(DEV))
+    seen_x += [xs[1], xs[2]]
+    seen_y += [ys[1], ys[2]]
+    torch.testing.assert_close(m.sum_squared_error.cpu().double(), _sse(seen_x, seen_y), rtol=1e-6, atol=1e-4)
+    assert float(m.sum_weight) == 4096 * len(seen_x)
+
+    # Sum / Mean with a long 1-D batch (K5b deferred mode), compute between replays
+    for cls in (Sum, Mean):
+        met = cls(device=DEV)
+        v = [torch.randn(200_003, generator=g) for _ in range(3)]
+        with warnings.catch_warnings():
+            warnings.simplefilter("ignore", RuntimeWarning)
+            st = GraphedUpdate(met, v[0].to(DEV))
+        tot = 0.0
+        for i in range(5):
+            st(v[i % 3].to(DEV))
+            tot += float(v[i % 3].double().sum())
+            want = tot if cls is Sum else tot / (200_003 * (i + 1))
+            assert float(met.compute()) == pytest.approx(want, rel=1e-9, abs=1e-6)

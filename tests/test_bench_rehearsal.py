@@ -18,7 +18,7 @@ def _port() -> int:
 
 
 def test_bench_8_rank_launch_on_cpu():
-    env = dict(os.environ, BENCH_DEVICE="cpu", BENCH_EXTRAS="0", OMP_NUM_THREADS="1")
+    env = dict(os.environ, BENCH_DEVICE="cpu", BENCH_EXTRAS="sync", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py",
            "--gpus", "8", "--steps", "3", "--warmup", "1"]
@@ -31,3 +31,12 @@ def test_bench_8_rank_launch_on_cpu():
     assert out["config"]["parallelism"] == "dp8" and out["config"]["global_batch"] == 8 * 8192
     assert out["value"] > 0 and out["higher_is_better"] is True and out["scaling"] == "weak"
     assert "CPU rehearsal" in out["data"]
+    # N > 1 diagnostics: the headline's own closing sync, the path it took,
+    # and the direct-RCCL arm - timed, or its voted fallback (gloo: no direct communicator)
+    sync = out["sync_ms"]
+    assert isinstance(sync, dict), sync
+    for key in ("accuracy_sync_and_compute", "confusion_matrix_1000_sync_and_compute",
+                "direct_accuracy_sync_and_compute", "direct_confusion_matrix_1000_sync_and_compute"):
+        assert isinstance(sync[key], float) and sync[key] > 0, (key, sync[key])
+    assert sync["sync_path"] == "c10d"
+    assert sync["direct_sync_path"] in ("direct-rccl", "c10d")

@@ -76,8 +76,10 @@ class PendingMixin:
     _pend_states: tuple = ()
 
     def _raw_state(self, name: str) -> torch.Tensor:
-        """The state tensor without folding (for the update that adds to the pending sums)."""
-        return self.__dict__["_pv_" + name]
+        """The state tensor without folding (for the update that adds to the pending sums, and
+        for HIP-graph replays' state-pointer checks)."""
+        t = self.__dict__.get("_pv_" + name)
+        return getattr(self, name) if t is None else t
 
     def _pend_buffer(self, numel: int, device: torch.device, spec=None) -> torch.Tensor:
         """The pending buffer for an update that will add ``spec``'s sums (pending sums of a
@@ -134,10 +136,40 @@ class PendingMixin:
             d["_pend_dirty"] = False
             d["_pend_r"] = 0
 
-    def _mark_updated(self) -> None:
-        """Called after a HIP-graph replay of ``update`` (torcheval_amd.utils.graphs)."""
+    def _pend_capture(self):
+        """Right after a HIP-graph capture of ``update``: what every replay adds to, as
+        ``(buffer, spec, slots)`` (None when the captured update did not run deferred).  A replay
+        launches the captured kernels only - no Python - so ``_mark_updated`` must restore the
+        spec and slot count the fold needs (a fold resets ``_pend_r`` to 0)."""
         d = self.__dict__
-        if d.get("_pend") is not None and d.get("_pend_spec"):
+        if not d.get("_pend_dirty") or d.get("_pend") is None:
+            return None
+        return (d["_pend"], d.get("_pend_spec"), d.get("_pend_r", 0))
+
+    def _pend_prepare(self, captured) -> None:
+        """Before a replay: the captured launches add ``captured``'s sums into ``captured``'s
+        buffer, so pending sums of another spec (an eager update in between) are folded first,
+        and a buffer replaced since the capture (``to()``, a larger eager batch) is refused."""
+        if captured is None:
+            return
+        d = self.__dict__
+        if d.get("_pend") is not captured[0]:
+            raise RuntimeError(
+                f"{type(self).__name__}: the deferred-sum buffer was replaced after graph capture "
+                "(to() or a larger eager update); re-create the GraphedUpdate"
+            )
+        if d.get("_pend_dirty") and d.get("_pend_spec") != captured[1]:
+            self._fold_pending()
+
+    def _mark_updated(self, captured=None) -> None:
+        """Called after a HIP-graph replay of ``update`` (torcheval_amd.utils.graphs) with the
+        ``_pend_capture()`` of the captured update: its sums are pending again, over its slots."""
+        d = self.__dict__
+        if captured is not None:
+            d["_pend_spec"] = captured[1]
+            d["_pend_r"] = max(d.get("_pend_r", 0), captured[2])
+            d["_pend_dirty"] = True
+        elif d.get("_pend") is not None and d.get("_pend_spec"):
             d["_pend_dirty"] = True
 
     def reset(self):

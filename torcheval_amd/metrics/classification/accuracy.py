@@ -169,10 +169,15 @@ class MulticlassAccuracy(Metric[torch.Tensor]):
         native().micro_accuracy_finish(d["_pend"], d["_nc"], d["num_total"], out)
         d["_pend_dirty"] = False
 
-    def _mark_updated(self) -> None:
-        """Called after a HIP-graph replay of ``update`` (torcheval_amd.utils.graphs)."""
+    def _mark_updated(self, captured=None) -> None:
+        """Called after a HIP-graph replay of ``update`` (torcheval_amd.utils.graphs); the K1
+        pending cells are a fixed set, folded whole, so the capture token is not needed."""
         if self.__dict__.get("_pend") is not None:
             self.__dict__["_pend_dirty"] = True
+
+    def _raw_state(self, name: str) -> torch.Tensor:
+        """A state without folding the pending cells (graph replays' state-pointer checks)."""
+        return self.__dict__["_nc"] if name == "num_correct" else getattr(self, name)
 
     def __getstate__(self):
         # copies (copy / deepcopy / pickle) carry folded states and no pending cells

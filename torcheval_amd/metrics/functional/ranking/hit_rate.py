@@ -11,15 +11,21 @@ __all__ = ["hit_rate"]
 
 @torch.inference_mode()
 def hit_rate(
-    input: torch.Tensor, target: torch.Tensor, *, k: Optional[int] = None, _err: Optional[torch.Tensor] = None
+    input: torch.Tensor, target: torch.Tensor, *, k: Optional[int] = None
 ) -> torch.Tensor:
     """Per-sample 1.0 if the target is within the top-k scores.  Class: ``HitRate``."""
+    return _hit_rate(input, target, k, None)
+
+
+def _hit_rate(input: torch.Tensor, target: torch.Tensor, k: Optional[int], err: Optional[torch.Tensor]) -> torch.Tensor:
+    """``hit_rate`` with the class metric's device error flag (``err``, or None for the
+    functional's own)."""
     _rank_input_check(input, target)
     if k is not None and k <= 0:
         raise ValueError(f"k should be None or positive, got {k}.")
     if k is None or k >= input.size(dim=-1):
         return input.new_ones(target.size())
-    out = _native_rank_scores(input, target, 0, k, _err)
+    out = _native_rank_scores(input, target, 0, k, err)
     if out is not None:
         return out
     return (_rank_of_target(input, target) < k).float()

@@ -10,7 +10,9 @@ MI355X path:
   state_dict, copies), so the states always reflect every update;
 * compute: tr sqrt(S1 S2) in FP64 from the symmetric L^T S2 L (S1 = L L^T, Cholesky) with an
   eigenvalues-only ``eigvalsh``, instead of the reference's non-symmetric ``linalg.eigvals``
-  (better conditioned, identical in exact arithmetic; singular S1 falls back to eigh);
+  (better conditioned, identical in exact arithmetic; singular S1 falls back to eigh).  On
+  ROCm: one covariance pass per side (fid_prep.hip), the one-launch K9d Cholesky, the
+  triangle-aware sandwich and the on-chip K9b eigenvalues;
 * sync: every state is ``merge="sum"``, so syncing is one RCCL all-reduce of 2 x D^2 + 2 x D
   floats; the model itself is never pickled or transferred (the reference all-gathers the
   whole pickled metric, Inception-v3 included).
@@ -57,26 +59,26 @@ def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
 
 
 def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
-    """tr sqrt(S1 S2) for symmetric PSD S1, S2 (FP64).
+    """tr sqrt(S1 S2) for symmetric PSD S1, S2 (FP64, both exactly symmetric).
 
     The eigenvalues of S1 S2 equal those of the symmetric L^T S2 L when S1 = L L^T, so the
-    fast path is one Cholesky, two triangular products and ONE eigenvalues-only ``eigvalsh``
-    (no eigenvectors, no back-transformation).  A singular S1 (fewer samples than features)
-    has no Cholesky factor; the same holds with the roles swapped when S2 has one.  When both
-    are singular, a full ``eigh`` gives S1 = W W^T with W = V_r sqrt(lam_r) over
+    fast path is one Cholesky (K9d), the triangle-aware sandwich and ONE eigenvalues-only
+    ``eigvalsh`` (K9b; no eigenvectors, no back-transformation).  A singular S1 (fewer samples
+    than features) has no Cholesky factor; the same holds with the roles swapped when S2 has
+    one.  When both are singular, a full ``eigh`` gives S1 = W W^T with W = V_r sqrt(lam_r) over
     the numerically non-zero eigenvalues (rank r, the ``matrix_rank`` tolerance of the FP64
     matrix), and the eigvalsh runs on the r x r matrix W^T S2 W: the same non-zero spectrum as
     S1 S2.  The tolerance is deliberately the FP64 one: covariances assembled from FP32 state
     sums carry rounding "noise" eigenvalues well above it, and the reference's
     ``eigvals(S1 S2)`` includes their square roots too, so they are kept (r is then the FP64
     numerical rank, usually above the sample rank - the r x r saving shrinks accordingly)."""
-    L, info = cholesky_ex(s1)
-    if int(info) == 0:
-        m = L.T @ s2 @ L
-    elif int((L2 := cholesky_ex(s2))[1]) == 0:
+    L, info = _chol(s1)
+    if info == 0:
+        m = _lt_s_l(L, s2)
+    elif (L2 := _chol(s2))[1] == 0:
         # S1 singular, S2 not: S1 S2 and S2 S1 share their spectrum, so factor S2 instead
         # (one more Cholesky rather than a full eigh with eigenvectors)
-        m = L2[0].T @ s1 @ L2[0]
+        m = _lt_s_l(L2[0], s1)
     else:
         lam, vec = torch.linalg.eigh(s1)
         keep = lam > lam.max().clamp(min=0) * lam.numel() * torch.finfo(lam.dtype).eps
@@ -84,37 +86,80 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
         if w.shape[1] == 0:
             return torch.zeros((), dtype=s1.dtype, device=s1.device)
         m = w.T @ s2 @ w
-    ev = sym_eigvalsh((m + m.T) / 2)
+        m = (m + m.T) / 2
+    ev = sym_eigvalsh(m)
     return ev.clamp(min=0).sqrt().sum()
+
+
+def _sandwich_blocks(n: int) -> int:
+    # 4 block columns: 1.875 n^3 flops instead of the dense 4 n^3, in 8 library GEMMs
+    return 4 if n >= 512 else 1
+
+
+def _lt_s_l(L: Tensor, s: Tensor) -> Tensor:
+    """L^T S L for lower-triangular L and symmetric S, exactly symmetric (FP64).
+
+    On ROCm, triangle-aware: with L cut into p block columns, Y^T = L^T S is p GEMMs whose
+    inner dimension skips L's zero blocks (block c: L[c0:, c]^T S[c0:, :]), and M = L^T Y is
+    computed for its lower block triangle only (block row r: L[r0:, r]^T Y[r0:, :r1]) - 1.875
+    n^3 instead of 4 n^3 flops at p = 4 - then ``sym_fill_upper`` mirrors the lower triangle
+    (the diagonal blocks are computed whole)."""
+    n = L.shape[0]
+    p = _sandwich_blocks(n) if use_native(L) else 1
+    if p == 1:
+        m = L.T @ s @ L
+        return (m + m.T) / 2
+    from torcheval_amd.ops import native
+
+    b = -(-n // p)
+    b = -(-b // 64) * 64
+    yt = torch.empty(n, n, dtype=L.dtype, device=L.device)
+    for c0 in range(0, n, b):
+        c1 = min(n, c0 + b)
+        torch.mm(L[c0:, c0:c1].T, s[c0:, :], out=yt[c0:c1])
+    m = torch.empty(n, n, dtype=L.dtype, device=L.device)
+    for r0 in range(0, n, b):
+        r1 = min(n, r0 + b)
+        torch.mm(L[r0:, r0:r1].T, yt[:r1, r0:].T, out=m[r0:r1, :r1])
+    native().sym_fill_upper(m)
+    return m
+
+
+def _chol(s: Tensor) -> "tuple[Tensor, int]":
+    """(lower Cholesky factor, LAPACK info as a host int) of a symmetric FP64 matrix."""
+    n = s.shape[0]
+    if use_native(s) and s.dtype == torch.float64 and s.dim() == 2 and 1 <= n <= 16384:
+        from torcheval_amd.ops import native
+        from torcheval_amd.ops.hostread import read_ints
+
+        nat = native()
+        nt = nat.cholesky_tiles(n)
+        N = 64 * nt
+        a = s if s.stride(1) == 1 else s.contiguous()
+        L = torch.empty(N, N, dtype=torch.float64, device=s.device)
+        linv = torch.empty(nt * 4096, dtype=torch.float64, device=s.device)
+        ctl = torch.empty(1, dtype=torch.int32, device=s.device)
+        status = torch.empty(2, dtype=torch.int32, device=s.device)
+        nat.cholesky_factor(a, L, linv, ctl, status)
+        info, abort = read_ints(status)
+        if not abort:
+            return L[:n, :n], info
+        warnings.warn("K9d Cholesky grid aborted (a hand-off timed out); using torch.linalg.cholesky_ex",
+                      RuntimeWarning)
+    L, info = torch.linalg.cholesky_ex(s)
+    return L, int(info)
 
 
 def cholesky_ex(s: Tensor) -> "tuple[Tensor, Tensor]":
     """Lower Cholesky factor of a symmetric FP64 matrix and an int ``info`` (0 = success, as
     ``torch.linalg.cholesky_ex``).
 
-    On ROCm, blocked right-looking with K9c (``csrc/kernels/symeig.hip``): one workgroup
-    factors each 64 x 64 diagonal block in LDS and inverts it, the panel below is one GEMM with
-    that inverse and the trailing update one GEMM - instead of rocSOLVER's chain of ~160 us
-    potf2 launches and its forward-substitution trsm."""
-    n = s.shape[0]
-    if use_native(s) and s.dtype == torch.float64 and s.dim() == 2 and n >= 2:
-        from torcheval_amd.ops import native
-
-        b = native().potrf_block_size()
-        a = s.contiguous().clone()
-        info = torch.zeros(1, dtype=torch.int32, device=s.device)
-        linv_full = torch.empty(b * b, dtype=torch.float64, device=s.device)  # reused (stream order)
-        for k0 in range(0, n, b):
-            bb = min(b, n - k0)
-            linv = linv_full[: bb * bb].view(bb, bb)
-            native().potrf_block(a, k0, bb, linv, info)
-            k1 = k0 + bb
-            if k1 < n:
-                l21 = a[k1:, k0:k1] @ linv.T
-                a[k1:, k0:k1] = l21
-                a[k1:, k1:].addmm_(l21, l21.T, alpha=-1.0)
-        return a.tril_(), info[0]
-    return torch.linalg.cholesky_ex(s)
+    On ROCm, K9d (``csrc/kernels/cholesky.hip``): the whole blocked factorisation in one
+    persistent launch (64 x 64 tiles on FP64 MFMA, a dataflow of ticket-ordered tile tasks,
+    one cross-CU hand-off per tile column) - instead of rocSOLVER's chain of ~160 us potf2
+    launches and its trsm, or round 5's per-block launch loop."""
+    L, info = _chol(s)
+    return L, torch.tensor(info, dtype=torch.int32)
 
 
 def sym_eigvalsh(m: Tensor) -> Tensor:
@@ -138,13 +183,32 @@ def sym_eigvalsh(m: Tensor) -> Tensor:
 
 def frechet_distance(mu1: Tensor, sigma1: Tensor, mu2: Tensor, sigma2: Tensor) -> Tensor:
     """||mu1 - mu2||^2 + tr S1 + tr S2 - 2 tr sqrt(S1 S2)  (FP64, symmetric formulation)."""
-    mu1, mu2 = mu1.double(), mu2.double()
     s1 = sigma1.double()
     s2 = sigma2.double()
-    s1 = (s1 + s1.T) / 2
-    s2 = (s2 + s2.T) / 2
+    return _frechet_symmetric(mu1, (s1 + s1.T) / 2, mu2, (s2 + s2.T) / 2)
+
+
+def _frechet_symmetric(mu1: Tensor, s1: Tensor, mu2: Tensor, s2: Tensor) -> Tensor:
+    """``frechet_distance`` of exactly symmetric FP64 covariances."""
+    mu1, mu2 = mu1.double(), mu2.double()
     tr_sqrt = _tr_sqrt_product(s1, s2)
     return (mu1 - mu2).square().sum() + s1.trace() + s2.trace() - 2 * tr_sqrt
+
+
+def _covariance(cov_sum: Tensor, col_sum: Tensor, n: int) -> Tensor:
+    """The exactly symmetric FP64 covariance (C / 2 + C^T / 2 - n mu mu^T) / (n - 1) from the
+    states (reference fid.py:239-250 forms it with the outer product in the states' dtype).
+    On ROCm one ``cov_finalize`` pass (csrc/kernels/fid_prep.hip) instead of ~10 FP64 passes."""
+    if (use_native(cov_sum) and cov_sum.dtype == torch.float32 and col_sum.dtype == torch.float32
+            and cov_sum.is_contiguous() and col_sum.is_contiguous() and n > 1):
+        from torcheval_amd.ops import native
+
+        out = torch.empty(cov_sum.shape, dtype=torch.float64, device=cov_sum.device)
+        native().cov_finalize(cov_sum, col_sum, float(n), out)
+        return out
+    mean = col_sum.double() / n
+    c = (cov_sum.double() - n * torch.outer(mean, mean)) / (n - 1)
+    return (c + c.T) / 2
 
 
 _STATES = (("real_sum", "real_cov_sum", "num_real_images"), ("fake_sum", "fake_cov_sum", "num_fake_images"))
@@ -304,9 +368,9 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
             return torch.tensor(0.0)
         real_mean = self.real_sum.double() / nr
         fake_mean = self.fake_sum.double() / nf
-        real_cov = (self.real_cov_sum.double() - nr * torch.outer(real_mean, real_mean)) / (nr - 1)
-        fake_cov = (self.fake_cov_sum.double() - nf * torch.outer(fake_mean, fake_mean)) / (nf - 1)
-        return frechet_distance(real_mean, real_cov, fake_mean, fake_cov).to(torch.float32)
+        real_cov = _covariance(self.real_cov_sum, self.real_sum, nr)
+        fake_cov = _covariance(self.fake_cov_sum, self.fake_sum, nf)
+        return _frechet_symmetric(real_mean, real_cov, fake_mean, fake_cov).to(torch.float32)
 
     real_sum = _staged_state("real_sum", 0)
     real_cov_sum = _staged_state("real_cov_sum", 0)

@@ -4,7 +4,7 @@ import torch
 
 from torcheval_amd.metrics.metric import inference_update
 
-from torcheval_amd.metrics.functional.ranking import hit_rate
+from torcheval_amd.metrics.functional.ranking.hit_rate import _hit_rate
 from torcheval_amd.metrics.ranking._score_list import _RankScoreList
 
 __all__ = ["HitRate"]
@@ -15,5 +15,5 @@ class HitRate(_RankScoreList):
 
     @inference_update
     def update(self, input: torch.Tensor, target: torch.Tensor) -> "HitRate":
-        self.scores.append(hit_rate(input, target, k=self.k, _err=self._err_for(input)))
+        self.scores.append(_hit_rate(input, target, self.k, self._err_for(input)))
         return self

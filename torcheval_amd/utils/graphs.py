@@ -33,10 +33,17 @@ from torcheval_amd.metrics.metric import Metric
 __all__ = ["GraphedUpdate"]
 
 
+def _raw(metric: Metric, name: str) -> torch.Tensor:
+    """A state tensor without folding pending device sums (the pointer check runs per replay;
+    a fold per replay would add a launch and reset the slot count the replays add to)."""
+    raw = getattr(metric, "_raw_state", None)
+    return raw(name) if raw is not None else getattr(metric, name)
+
+
 def _state_ptrs(metric: Metric) -> Dict[str, Any]:
     out: Dict[str, Any] = {}
     for name in metric._state_name_to_default:
-        v = getattr(metric, name)
+        v = _raw(metric, name)
         if isinstance(v, torch.Tensor):
             out[name] = v.data_ptr()
         elif isinstance(v, list):
@@ -86,6 +93,10 @@ class GraphedUpdate:
             raise RuntimeError(
                 f"{type(metric).__name__}.update cannot be captured into a HIP graph: {e}"
             ) from e
+        # deferred-fold metrics (metrics/_pending.py): the buffer / spec / slots every replay adds
+        # to, taken before anything reads (and so folds) the states
+        cap = getattr(metric, "_pend_capture", None)
+        self._pend_cap = cap() if cap is not None else None
         if _state_ptrs(metric) != ptrs:
             raise RuntimeError(
                 f"{type(metric).__name__}.update rebinds its states; it cannot be replayed from a graph"
@@ -123,15 +134,22 @@ class GraphedUpdate:
             t0 = time.perf_counter()
             for _ in range(n):
                 if replay:
-                    self.graph.replay()
+                    self._replay()
                 else:
                     metric.update(*self._static)
             torch.cuda.synchronize()
             out.append((time.perf_counter() - t0) / n * 1e6)
-        mark = getattr(metric, "_mark_updated", None)
-        if mark is not None:  # replays added into deferred folds: let the restore see them
-            mark()
         return out[0], out[1]
+
+    def _replay(self) -> None:
+        m = self.metric
+        prep = getattr(m, "_pend_prepare", None)
+        if prep is not None:
+            prep(self._pend_cap)
+        self.graph.replay()
+        mark = getattr(m, "_mark_updated", None)
+        if mark is not None:  # deferred folds (K1 micro's pending cells, K5 / K5b pending slots)
+            mark(self._pend_cap)
 
     @property
     def static_inputs(self) -> Tuple[torch.Tensor, ...]:
@@ -148,13 +166,10 @@ class GraphedUpdate:
             if src.data_ptr() != dst.data_ptr():
                 dst.copy_(src, non_blocking=True)
         m = self.metric
-        if tuple(getattr(m, n).data_ptr() for n in self._names) != self._ptrs:
+        if tuple(_raw(m, n).data_ptr() for n in self._names) != self._ptrs:
             raise RuntimeError(
                 f"{type(m).__name__}: a state was rebound after graph capture (load_state_dict / to()); "
                 "re-create the GraphedUpdate"
             )
-        self.graph.replay()
-        mark = getattr(self.metric, "_mark_updated", None)
-        if mark is not None:  # metrics with deferred folds (K1 micro's pending cells)
-            mark()
+        self._replay()
         return self.metric
