@@ -746,10 +746,12 @@ int64_t row_sums_pend(const Tensor& x_in, const optional<Tensor>& t_in, const op
   Tensor x;
   tea::RowSumsArgs a = row_sums_args(x_in, t_in, w_in, w_scalar, outs, codes, rows, &x);
   if (!x.is_cuda() || a.n == 0) return 0;
-  for (int k = 0; k < a.nout; ++k)
-    if (a.out[k].op != tea::kAdd || a.out[k].stat == tea::kTMIN || a.out[k].stat == tea::kTMAX ||
-        a.out[k].stat == tea::kRANGE)
-      return 0;
+  for (int k = 0; k < a.nout; ++k) {  // sums / COUNT added, extrema min / max, RANGE set
+    const auto& o = a.out[k];
+    const bool ok = o.stat == tea::kTMIN ? o.op == tea::kMin : o.stat == tea::kTMAX ? o.op == tea::kMax
+                  : o.stat == tea::kRANGE ? o.op == tea::kSet : o.op == tea::kAdd;
+    if (!ok) return 0;
+  }
   const int blocks = tea::row_sums_blocks(a.rows, a.n);
   if (blocks < 2 || blocks > tea::kRowPendBlocks) return 0;
   TORCH_CHECK(pend.scalar_type() == at::kDouble && pend.is_contiguous() && pend.device() == x.device() &&
@@ -1184,6 +1186,96 @@ void potrf_block(const Tensor& a, int64_t k0, int64_t b, const Tensor& linv, con
                "potrf_block");
 }
 
+// K9d: the whole blocked FP64 Cholesky in one persistent launch (csrc/kernels/cholesky.hip).
+// l: padded [64 nt, 64 nt] float64 output (upper triangle zeroed), linv: >= nt * 4096 float64
+// scratch, ctl: >= 1 int32 scratch, status: >= 2 int32 -> [LAPACK info, abort].
+void cholesky_factor(const Tensor& a, const Tensor& l, const Tensor& linv, const Tensor& ctl, const Tensor& status) {
+  check_gpu(a, "matrix");
+  TORCH_CHECK(a.dim() == 2 && a.size(0) == a.size(1) && a.scalar_type() == at::kDouble && a.stride(1) == 1,
+              "cholesky_factor: matrix must be a row-contiguous float64 [n, n]");
+  const int64_t n = a.size(0);
+  const int64_t N = 64 * static_cast<int64_t>(tea::cholesky_tiles(n));
+  TORCH_CHECK(l.scalar_type() == at::kDouble && l.is_contiguous() && l.numel() == N * N && l.device() == a.device(),
+              "cholesky_factor: l must be a contiguous float64 [", N, ", ", N, "]");
+  TORCH_CHECK(linv.scalar_type() == at::kDouble && linv.is_contiguous() && linv.numel() >= (N / 64) * 4096 &&
+                  linv.device() == a.device(),
+              "cholesky_factor: linv too small");
+  TORCH_CHECK(ctl.scalar_type() == at::kInt && ctl.numel() >= 1 && ctl.device() == a.device(), "cholesky_factor: ctl");
+  TORCH_CHECK(status.scalar_type() == at::kInt && status.is_contiguous() && status.numel() >= 2 &&
+                  status.device() == a.device(),
+              "cholesky_factor: status must be int32 [2]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(a.device());
+  check_launch(tea::launch_cholesky(a.data_ptr<double>(), a.stride(0), n, l.data_ptr<double>(), linv.data_ptr<double>(),
+                                    ctl.data_ptr<int>(), status.data_ptr<int>(), stream_for(a)),
+               "cholesky_factor");
+}
+
+// test / profiling hook: cholesky_factor with per-tile-column phase stamps (s_memrealtime,
+// 100 MHz) of the pair-owner tasks in trace (int64 [nt * 8]), then the shader-clock stamps of every
+// column of tile column 1's factorisation (wave 0: [nt * 8, + 65), wave 1: [nt * 8 + 65, + 65))
+void cholesky_factor_traced(const Tensor& a, const Tensor& l, const Tensor& linv, const Tensor& ctl,
+                            const Tensor& status, const Tensor& trace) {
+  const int64_t nt = tea::cholesky_tiles(a.size(0));
+  TORCH_CHECK(trace.scalar_type() == at::kLong && trace.is_contiguous() && trace.numel() >= nt * 8 + 130 &&
+                  trace.device() == a.device(),
+              "cholesky_factor_traced: trace must be int64 [nt * 8 + 130]");
+  check_gpu(a, "matrix");
+  TORCH_CHECK(l.numel() == 64 * nt * 64 * nt && linv.numel() >= nt * 4096 && status.numel() >= 2,
+              "cholesky_factor_traced: workspace sizes");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(a.device());
+  check_launch(tea::launch_cholesky(a.data_ptr<double>(), a.stride(0), a.size(0), l.data_ptr<double>(),
+                                    linv.data_ptr<double>(), ctl.data_ptr<int>(), status.data_ptr<int>(), stream_for(a),
+                                    reinterpret_cast<unsigned long long*>(trace.data_ptr<int64_t>())),
+               "cholesky_factor_traced");
+}
+
+// K3t: trapezoid area per row of x-sorted (x, y) pairs (csrc/kernels/trapz.hip); y is the f32
+// payload K3a carried through its sort (the int32 order buffer, reinterpreted)
+void trapz_sorted(const Tensor& x, const Tensor& y_bits, const Tensor& out) {
+  check_gpu(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kFloat && x.is_contiguous(), "trapz_sorted: x must be contiguous f32 [rows, n]");
+  TORCH_CHECK((y_bits.scalar_type() == at::kInt || y_bits.scalar_type() == at::kFloat) && y_bits.is_contiguous() &&
+                  y_bits.sizes() == x.sizes() && y_bits.device() == x.device(),
+              "trapz_sorted: y must be contiguous f32 / int32 bits shaped like x");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.numel() == x.size(0) &&
+                  out.device() == x.device(),
+              "trapz_sorted: out must be f32 [rows]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(x.device());
+  const hipStream_t st = stream_for(x);
+  auto* part = static_cast<double*>(scratch_workspace(x, st, x.size(0) * tea::trapz_blocks(x.size(1)) * 8, 13));
+  check_launch(tea::launch_trapz_sorted(x.data_ptr<float>(), static_cast<const float*>(y_bits.data_ptr()), x.size(0),
+                                        x.size(1), part, out.data_ptr<float>(), st),
+               "trapz_sorted");
+}
+
+// FID compute glue (csrc/kernels/fid_prep.hip): FP64 symmetric covariance from the FP32 states.
+void cov_finalize(const Tensor& cov_sum, const Tensor& colsum, double n, const Tensor& out) {
+  check_gpu(cov_sum, "cov_sum");
+  const int64_t d = colsum.numel();
+  TORCH_CHECK(cov_sum.scalar_type() == at::kFloat && cov_sum.is_contiguous() && cov_sum.numel() == d * d,
+              "cov_finalize: cov_sum must be a contiguous float32 [d, d]");
+  TORCH_CHECK(colsum.scalar_type() == at::kFloat && colsum.is_contiguous() && colsum.device() == cov_sum.device(),
+              "cov_finalize: colsum must be a contiguous float32 [d]");
+  TORCH_CHECK(out.scalar_type() == at::kDouble && out.is_contiguous() && out.numel() == d * d &&
+                  out.device() == cov_sum.device(),
+              "cov_finalize: out must be a contiguous float64 [d, d]");
+  TORCH_CHECK(n > 1.0, "cov_finalize: needs n > 1");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(cov_sum.device());
+  check_launch(tea::launch_cov_finalize(cov_sum.data_ptr<float>(), colsum.data_ptr<float>(), n, d,
+                                        out.data_ptr<double>(), stream_for(cov_sum)),
+               "cov_finalize");
+}
+
+void sym_fill_upper(const Tensor& m) {
+  check_gpu(m, "matrix");
+  TORCH_CHECK(m.dim() == 2 && m.size(0) == m.size(1) && m.scalar_type() == at::kDouble && m.stride(1) == 1 &&
+                  m.stride(0) >= m.size(1),
+              "sym_fill_upper: matrix must be a row-contiguous float64 [n, n]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(m.device());
+  check_launch(tea::launch_sym_fill_upper(m.data_ptr<double>(), m.stride(0), m.size(0), stream_for(m)),
+               "sym_fill_upper");
+}
+
 // K2: multilabel accuracy counts straight into float32 state scalars.
 void multilabel_counts(const Tensor& input, const Tensor& target, double threshold, int64_t k,
                        int64_t criteria, const Tensor& num_correct, const optional<Tensor>& num_total,
@@ -1248,7 +1340,8 @@ void transpose_f32(const Tensor& x, const Tensor& out) {
 // (RadixArgs::fold_ab) and the call returns true; pass it to auc_scan as `tsum`.  False: not
 // folded (legacy sort, no payload), auc_scan must run its own tile_sums.
 bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_order,
-               const optional<Tensor>& payload, int64_t payload_kind, const optional<Tensor>& fold) {
+               const optional<Tensor>& payload, int64_t payload_kind, const optional<Tensor>& fold,
+               bool ascending = false) {
   check_gpu(x, "x");
   TORCH_CHECK(x.dim() == 2 && x.scalar_type() == at::kFloat && x.stride(1) == 1,
               "sort_desc: x must be float32 [rows, n] with contiguous rows");
@@ -1283,6 +1376,7 @@ bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   a.region = (cap / 4 - 4) / 4;  // fixed per buffer, so the next call finds region 3 at the same place
   a.out_sorted = out_sorted.data_ptr<float>();
   a.out_order = out_order.data_ptr<int32_t>();
+  a.key_xor = ascending ? ~0u : 0u;  // stable either way; ascending puts NaN last (torch.sort)
   static const bool onesweep = [] {
     const char* e = std::getenv("TORCHEVAL_AMD_K3_ONESWEEP");
     return e == nullptr || e[0] != '0';
@@ -1581,9 +1675,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("out"));
   m.def("sort_desc_timeouts", &sort_desc_timeouts, "test hook: onesweep look-back timeout word (0 = none)",
         pybind11::arg("x"), pybind11::arg("clear") = true);
-  m.def("sort_desc", &sort_desc, "K3a segmented descending radix sort (f32 -> sorted, int32 order)",
+  m.def("sort_desc", &sort_desc, "K3a segmented stable radix sort, descending or ascending (f32 -> sorted, int32 order)",
         py::arg("x"), py::arg("out_sorted"), py::arg("out_order"), py::arg("payload") = py::none(),
-        py::arg("payload_kind") = 0, py::arg("fold") = py::none());
+        py::arg("payload_kind") = 0, py::arg("fold") = py::none(), py::arg("ascending") = false);
   m.def("binned_finalize", &binned_finalize, "binned AUROC / AUPRC / PR-curve points from counts",
         py::arg("tp"), py::arg("fp"), py::arg("fn") = py::none(), py::arg("out_auroc") = py::none(),
         py::arg("out_auprc") = py::none(), py::arg("out_prec") = py::none(),
@@ -1593,6 +1687,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("potrf_block", &potrf_block, "K9c diagonal-block FP64 Cholesky + inverse (blocked Cholesky step)",
         py::arg("a"), py::arg("k0"), py::arg("b"), py::arg("linv"), py::arg("info"));
   m.def("potrf_block_size", &tea::potrf_block_size, "K9c block size");
+  m.def("cholesky_factor", &cholesky_factor, "K9d one-launch blocked FP64 Cholesky (padded factor, info, abort)",
+        py::arg("a"), py::arg("l"), py::arg("linv"), py::arg("ctl"), py::arg("status"));
+  m.def("cholesky_tiles", &tea::cholesky_tiles, "K9d 64 x 64 tiles per side");
+  m.def("cholesky_factor_traced", &cholesky_factor_traced, "K9d with per-column phase stamps (profiling hook)");
+  m.def("trapz_sorted", &trapz_sorted, "K3t trapezoid area per row of x-sorted (x, y)", py::arg("x"),
+        py::arg("y_bits"), py::arg("out"));
+  m.def("cov_finalize", &cov_finalize, "FP64 symmetric covariance from FP32 FID states",
+        py::arg("cov_sum"), py::arg("colsum"), py::arg("n"), py::arg("out"));
+  m.def("sym_fill_upper", &sym_fill_upper, "mirror the lower triangle of a float64 matrix into its upper",
+        py::arg("m"));
   m.def("sym_eigvals", &sym_eigvals, "K9b eigenvalues of a symmetric float64 matrix (on-chip Householder + multisection)",
         py::arg("m"), py::arg("lam"), py::arg("status"));
   tea_register_runtime(m);
@@ -1613,8 +1717,9 @@ void op_row_sums(const Tensor& x, const optional<Tensor>& t, const optional<Tens
                  at::TensorList outs, at::IntArrayRef codes, int64_t rows) {
   row_sums(x, t, w, w_scalar, outs.vec(), codes.vec(), rows);
 }
-void op_sort_desc(const Tensor& x, const Tensor& s, const Tensor& o, const optional<Tensor>& p, int64_t kind) {
-  sort_desc(x, s, o, p, kind, c10::nullopt);
+void op_sort_desc(const Tensor& x, const Tensor& s, const Tensor& o, const optional<Tensor>& p, int64_t kind,
+                  bool ascending) {
+  sort_desc(x, s, o, p, kind, c10::nullopt, ascending);
 }
 void op_auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target, const optional<Tensor>& weight,
                  bool class_mode, const optional<Tensor>& out_auroc, const optional<Tensor>& out_auprc,
@@ -1699,6 +1804,9 @@ void op_binned_finalize(const Tensor& tp, const Tensor& fp, const optional<Tenso
   binned_finalize(tp, fp, fn, out_auroc, out_auprc, out_prec, out_rec);
 }
 int64_t op_sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) { return sym_eigvals(m, lam, status); }
+void op_cholesky_factor(const Tensor& a, const Tensor& l, const Tensor& linv, const Tensor& ctl, const Tensor& status) {
+  cholesky_factor(a, l, linv, ctl, status);
+}
 void op_potrf_block(const Tensor& a, int64_t k0, int64_t b, const Tensor& linv, const Tensor& info) {
   potrf_block(a, k0, b, linv, info);
 }
@@ -1734,10 +1842,14 @@ TORCH_LIBRARY(torcheval_amd, m) {
         "Tensor(c!)? out_prec, Tensor(d!)? out_rec) -> ()");
   m.def("sym_eigvals(Tensor m, Tensor(a!) lam, Tensor(b!) status) -> int");
   m.def("potrf_block(Tensor(a!) a, int k0, int b, Tensor(b!) linv, Tensor(c!) info) -> ()");
+  m.def("cholesky_factor(Tensor a, Tensor(a!) l, Tensor(b!) linv, Tensor(c!) ctl, Tensor(d!) status) -> ()");
+  m.def("cov_finalize(Tensor cov_sum, Tensor colsum, float n, Tensor(a!) out) -> ()");
+  m.def("sym_fill_upper(Tensor(a!) m) -> ()");
+  m.def("trapz_sorted(Tensor x, Tensor y_bits, Tensor(a!) out) -> ()");
   m.def("seg_reduce_rows(Tensor rows, Tensor(a!) out, int ws, int[] offs, int[] counts, int[] dtypes, "
         "int[] ops) -> ()");
   m.def("row_sums(Tensor x, Tensor? t, Tensor? w, float w_scalar, Tensor(a!)[] outs, int[] codes, int rows) -> ()");
-  m.def("sort_desc(Tensor x, Tensor(a!) sorted, Tensor(b!) order, Tensor? payload, int payload_kind) -> ()");
+  m.def("sort_desc(Tensor x, Tensor(a!) sorted, Tensor(b!) order, Tensor? payload, int payload_kind, bool ascending=False) -> ()");
   m.def("auc_scan(Tensor sorted, Tensor order, Tensor target, Tensor? weight, bool class_mode, "
         "Tensor(a!)? out_auroc, Tensor(b!)? out_auprc, Tensor? init, Tensor(c!)? out_raw, int payload_kind) -> ()");
   m.def("rafp(Tensor sorted, Tensor order, Tensor target, bool class_mode, int payload_kind, float min_precision, "
@@ -1766,6 +1878,10 @@ TORCH_LIBRARY_IMPL(torcheval_amd, CUDA, m) {
   m.impl("binned_finalize", &op_binned_finalize);
   m.impl("sym_eigvals", &op_sym_eigvals);
   m.impl("potrf_block", &op_potrf_block);
+  m.impl("cholesky_factor", &op_cholesky_factor);
+  m.impl("cov_finalize", &cov_finalize);
+  m.impl("sym_fill_upper", &sym_fill_upper);
+  m.impl("trapz_sorted", &trapz_sorted);
   m.impl("seg_reduce_rows", &op_seg_reduce_rows);
   m.impl("row_sums", &op_row_sums);
   m.impl("sort_desc", &op_sort_desc);
@@ -1804,6 +1920,10 @@ TORCH_LIBRARY_IMPL(torcheval_amd, Meta, m) {
   m.impl("binned_finalize", [](const Tensor&, const Tensor&, const optional<Tensor>&, const optional<Tensor>&,
                                const optional<Tensor>&, const optional<Tensor>&, const optional<Tensor>&) {});
   m.impl("potrf_block", [](const Tensor&, int64_t, int64_t, const Tensor&, const Tensor&) {});
+  m.impl("cholesky_factor", [](const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&) {});
+  m.impl("cov_finalize", [](const Tensor&, const Tensor&, double, const Tensor&) {});
+  m.impl("sym_fill_upper", [](const Tensor&) {});
+  m.impl("trapz_sorted", [](const Tensor&, const Tensor&, const Tensor&) {});
   m.impl("seg_reduce_rows", [](const Tensor&, const Tensor&, int64_t, at::IntArrayRef, at::IntArrayRef,
                                at::IntArrayRef, at::IntArrayRef) {});
   m.impl("cls_counts", [](const Tensor&, const Tensor&, int64_t, int64_t, const optional<Tensor>&,
@@ -1818,7 +1938,7 @@ TORCH_LIBRARY_IMPL(torcheval_amd, Meta, m) {
                                const optional<Tensor>&, bool) {});
   m.impl("row_sums", [](const Tensor&, const optional<Tensor>&, const optional<Tensor>&, double, at::TensorList,
                         at::IntArrayRef, int64_t) {});
-  m.impl("sort_desc", [](const Tensor&, const Tensor&, const Tensor&, const optional<Tensor>&, int64_t) {});
+  m.impl("sort_desc", [](const Tensor&, const Tensor&, const Tensor&, const optional<Tensor>&, int64_t, bool) {});
   m.impl("fid_cov_update", [](const Tensor&, const Tensor&, const optional<Tensor>&) {});
   m.impl("transpose_f32", [](const Tensor&, const Tensor&) {});
 }

@@ -323,7 +323,8 @@ struct SampleAurocArgs {
 };
 int launch_sample_binned_auroc(const SampleAurocArgs& a, hipStream_t stream);
 
-constexpr int kRowPendStats = kRowSums + 1;  // the six sums, then COUNT
+constexpr int kRowPendStats = kRowSums + 3;  // the six sums, COUNT, then the target min / max
+                                             // (a slot's extrema are valid while its COUNT != 0)
 constexpr int kRowPendBlocks = 2048;
 // pending slots b < blocks_used of every row -> the outputs of a (ADD), slots zeroed
 int launch_row_sums_fold(const RowSumsArgs& a, int blocks_used, hipStream_t stream);
@@ -474,6 +475,9 @@ struct RadixArgs {
   double* fold_ab = nullptr;      // [rows, fold_otiles, 2]
   int64_t fold_otiles = 0;        // ceil(n / 1024)
   int fold_probe = 0;             // A/B probe (TORCHEVAL_AMD_K3_FOLD_PROBE): 1 no atomics, 2 no fold work
+  // 0: descending (NaN first); ~0u: ascending (NaN last, as torch.sort ascending), both stable -
+  // XORed into every key at load and out of it at the final store
+  uint32_t key_xor = 0;
 };
 bool radix_onesweep_ok(int64_t rows, int64_t n);  // the tiling the onesweep passes take
 int64_t radix_onesweep_status_words(int64_t rows, int64_t n);
@@ -534,6 +538,20 @@ namespace tea {
 // in place into its lower Cholesky factor (upper part zeroed) and write its inverse to Linv
 // [b, b]; a non-positive pivot sets *info = k0 + column + 1 (if still 0).  b <= 64.
 int potrf_block_size();
+// K9d (cholesky.hip): the whole blocked Cholesky in one persistent launch.  L: padded
+// [64 nt, 64 nt] factor, Linv: nt x 64 x 64, ctl: 1 int (ticket), status: 2 ints (info, abort)
+int cholesky_tiles(int64_t n);
+// fid_prep.hip: S = ((C + C^T) / 2 - n mu mu^T) / (n - 1) in FP64 from the FP32 K8 states;
+// M[i][j] = M[j][i] above the diagonal (in place)
+// trapz.hip: per-row trapezoid area of x-sorted rows (x, y f32 [rows, n]) -> out f32 [rows];
+// part: FP64 scratch of rows * trapz_blocks(n)
+int trapz_blocks(int64_t n);
+int launch_trapz_sorted(const float* x, const float* y, int64_t rows, int64_t n, double* part, float* out,
+                        hipStream_t stream);
+int launch_cov_finalize(const float* C, const float* colsum, double n, int64_t d, double* S, hipStream_t stream);
+int launch_sym_fill_upper(double* M, int64_t ld, int64_t n, hipStream_t stream);
+int launch_cholesky(const double* A, int64_t lda, int64_t n, double* L, double* Linv, int* ctl, int* status,
+                    hipStream_t stream, unsigned long long* trace = nullptr);
 int launch_potrf_block(double* A, int64_t lda, int k0, int b, double* Linv, int* info, hipStream_t stream);
 }  // namespace tea
 

@@ -57,7 +57,7 @@ __device__ __forceinline__ float key2f_desc(uint32_t k) {
 
 __device__ __forceinline__ uint32_t load_key(const RadixArgs& a, const uint32_t* keys_in, int pass,
                                              int64_t row, int64_t i) {
-  if (pass == 0) return f2key_desc(a.in[row * a.in_row_stride + i]);
+  if (pass == 0) return f2key_desc(a.in[row * a.in_row_stride + i]) ^ a.key_xor;
   return keys_in[row * a.n + i];
 }
 
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     for (int j = 0; j < kRounds; ++j) {
       const int64_t pos = row * a.n + static_cast<int64_t>(pb[j]) + (threadIdx.x + j * kRT);
       if (last) {
-        a.out_sorted[pos] = key2f_desc(kk[j]);
+        a.out_sorted[pos] = key2f_desc(kk[j] ^ a.key_xor);
         a.out_order[pos] = static_cast<int32_t>(vv[j]);
       } else {
         keys_out[pos] = kk[j];
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(kRT) void radix_downsweep_kernel(RadixArgs a, const
     const uint32_t d = (key >> shift) & 0xffu;
     const int64_t pos = row * a.n + base[d] + (p - tstart[d]);
     if (last) {
-      a.out_sorted[pos] = key2f_desc(key);
+      a.out_sorted[pos] = key2f_desc(key ^ a.key_xor);
       a.out_order[pos] = static_cast<int32_t>(sv[p]);
     } else {
       keys_out[pos] = key;
@@ -421,7 +421,7 @@ __global__ __launch_bounds__(kRT) void onesweep_hist_kernel(RadixArgs a, int64_t
 #pragma unroll
     for (int j = 0; j < kHistKeys; ++j) {  // clamped loads, all in flight; the tail masked below
       const int64_t i = i0 + j * kRT + threadIdx.x;
-      k[j] = f2key_desc(in[i < hi ? i : hi - 1]);
+      k[j] = f2key_desc(in[i < hi ? i : hi - 1]) ^ a.key_xor;
     }
 #pragma unroll
     for (int j = 0; j < kHistKeys; ++j) {
@@ -725,7 +725,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     for (int j = 0; j < kRounds; ++j) {
       const int64_t pos = row * a.n + static_cast<int64_t>(pb[j]) + (threadIdx.x + j * kRT);
       if (last) {
-        a.out_sorted[pos] = key2f_desc(kk[j]);
+        a.out_sorted[pos] = key2f_desc(kk[j] ^ a.key_xor);
         a.out_order[pos] = static_cast<int32_t>(vv[j]);
       } else {
         keys_out[pos] = kk[j];
@@ -740,7 +740,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     const uint32_t d = (key >> shift) & 0xffu;
     const int64_t pos = row * a.n + base[d] + (p - tstart[d]);
     if (last) {
-      a.out_sorted[pos] = key2f_desc(key);
+      a.out_sorted[pos] = key2f_desc(key ^ a.key_xor);
       a.out_order[pos] = static_cast<int32_t>(sv[p]);
     } else {
       keys_out[pos] = key;

@@ -125,6 +125,20 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
   acc_init(a);
   const int need = g.need;
   if constexpr (VEC) {
+    // target extrema of f32 rows: fminf / fmaxf in f32 (exact) plus a NaN flag, merged into the
+    // FP64 accumulator once at the end - the NaN-propagating FP64 min / max per element made PSNR
+    // (auto range) 2.6 us slower than its fixed-range form at 8192 x 1000
+    constexpr bool FX = NEED != kAll && (NEED & (bit(kTMIN) | bit(kTMAX))) != 0;
+    constexpr int NB = FX ? (NEED & ~(bit(kTMIN) | bit(kTMAX))) : NEED;
+    float fmn = __builtin_inff(), fmx = -__builtin_inff();
+    bool fnan = false;
+    auto fx = [&](float t, bool ok) {
+      if constexpr (FX) {
+        fmn = fminf(fmn, ok ? t : fmn);
+        fmx = fmaxf(fmx, ok ? t : fmx);
+        fnan |= ok && t != t;
+      }
+    };
     const float* xr = static_cast<const float*>(g.x) + r * g.x_rs;
     const float* tr = HAS_T ? static_cast<const float*>(g.t) + r * g.t_rs : nullptr;
     const float* wr = HAS_W ? static_cast<const float*>(g.w) + r * g.w_rs : nullptr;
@@ -148,10 +162,14 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
       if (base + kChunk <= vhi) {  // whole chunk in range (block-uniform): no per-lane branch
 #pragma unroll
         for (int u = 0; u < VPT; ++u) {
-          acc_elem<NEED, HAS_W>(a, need, xv[u].x, tv[u].x, wv[u].x);
-          acc_elem<NEED, HAS_W>(a, need, xv[u].y, tv[u].y, wv[u].y);
-          acc_elem<NEED, HAS_W>(a, need, xv[u].z, tv[u].z, wv[u].z);
-          acc_elem<NEED, HAS_W>(a, need, xv[u].w, tv[u].w, wv[u].w);
+          acc_elem<NB, HAS_W>(a, need, xv[u].x, tv[u].x, wv[u].x);
+          acc_elem<NB, HAS_W>(a, need, xv[u].y, tv[u].y, wv[u].y);
+          acc_elem<NB, HAS_W>(a, need, xv[u].z, tv[u].z, wv[u].z);
+          acc_elem<NB, HAS_W>(a, need, xv[u].w, tv[u].w, wv[u].w);
+          fx(tv[u].x, true);
+          fx(tv[u].y, true);
+          fx(tv[u].z, true);
+          fx(tv[u].w, true);
         }
       } else {
         // the row's last, partial chunk: the same loads, out-of-range lanes zeroed by selects
@@ -165,12 +183,21 @@ __device__ Acc reduce_range(const RowSumsArgs& g, int64_t r, int64_t lo, int64_t
           const float4 xm = make_float4(ok ? xv[u].x : 0.f, ok ? xv[u].y : 0.f, ok ? xv[u].z : 0.f, ok ? xv[u].w : 0.f);
           const float4 tm = make_float4(ok ? tv[u].x : 0.f, ok ? tv[u].y : 0.f, ok ? tv[u].z : 0.f, ok ? tv[u].w : 0.f);
           const float4 wm = make_float4(ok ? wv[u].x : 0.f, ok ? wv[u].y : 0.f, ok ? wv[u].z : 0.f, ok ? wv[u].w : 0.f);
-          acc_elem<NEED, HAS_W>(a, need, xm.x, tm.x, wm.x, ok);
-          acc_elem<NEED, HAS_W>(a, need, xm.y, tm.y, wm.y, ok);
-          acc_elem<NEED, HAS_W>(a, need, xm.z, tm.z, wm.z, ok);
-          acc_elem<NEED, HAS_W>(a, need, xm.w, tm.w, wm.w, ok);
+          acc_elem<NB, HAS_W>(a, need, xm.x, tm.x, wm.x, ok);
+          acc_elem<NB, HAS_W>(a, need, xm.y, tm.y, wm.y, ok);
+          acc_elem<NB, HAS_W>(a, need, xm.z, tm.z, wm.z, ok);
+          acc_elem<NB, HAS_W>(a, need, xm.w, tm.w, wm.w, ok);
+          fx(tv[u].x, ok);
+          fx(tv[u].y, ok);
+          fx(tv[u].z, ok);
+          fx(tv[u].w, ok);
         }
       }
+    }
+    if constexpr (FX) {
+      const double nan = __builtin_nan("");
+      if (NEED & bit(kTMIN)) a.v[kTMIN] = nmin(a.v[kTMIN], fnan ? nan : static_cast<double>(fmn));
+      if (NEED & bit(kTMAX)) a.v[kTMAX] = nmax(a.v[kTMAX], fnan ? nan : static_cast<double>(fmx));
     }
     // ragged head / tail (< 4 elements each side)
     for (int64_t i = lo + threadIdx.x; i < min(vlo, hi); i += BS)
@@ -272,6 +299,15 @@ __global__ __launch_bounds__(kB) void row_sums_grid_kernel(RowSumsArgs g, int64_
         } else if (NEED & bit(k)) {
           pend_add(p + k * g.pend_blocks, k == kSSE ? a.v[k] : ws * a.v[k]);
         }
+      }
+      if constexpr ((NEED & (bit(kTMIN) | bit(kTMAX))) != 0) {
+        // the extrema slots are this block's own (plain read-modify-write, stream-ordered across
+        // launches); a slot whose COUNT is still 0 holds no extrema yet (the buffer is zeroed)
+        const bool fresh = p[kRowSums * g.pend_blocks] == 0.0;
+        double* pmin = p + (kRowSums + 1) * g.pend_blocks;
+        double* pmax = p + (kRowSums + 2) * g.pend_blocks;
+        if (NEED & bit(kTMIN)) *pmin = fresh ? a.v[kTMIN] : nmin(*pmin, a.v[kTMIN]);
+        if (NEED & bit(kTMAX)) *pmax = fresh ? a.v[kTMAX] : nmax(*pmax, a.v[kTMAX]);
       }
       pend_add(p + kRowSums * g.pend_blocks, cnt);
     }
@@ -418,14 +454,31 @@ __global__ __launch_bounds__(kB) void row_sums_wt_kernel(RowSumsArgs g, int64_t 
   if (threadIdx.x == 0) finish_row<HAS_W>(g, r, m);
 }
 
-// deferred-mode fold: one block per row; every thread sums a strided share of the slots of
+// deferred-mode fold: one block per row; every thread folds a strided share of the slots of
 // each statistic (fixed partition + fixed LDS tree: deterministic), zeroes them, and thread 0
-// applies the ADD outputs
+// applies the outputs as finish_row does (sums / COUNT added, extrema min / max-merged with the
+// states, RANGE set from the merged extrema)
 __global__ __launch_bounds__(kB) void row_sums_pend_fold_kernel(RowSumsArgs g, int used) {
   const int64_t r = blockIdx.x;
   __shared__ double lds[kRowPendStats][kB];
   double* base = g.pend + r * kRowPendStats * g.pend_blocks;
-  for (int k = 0; k < kRowPendStats; ++k) {
+  {  // extrema first, while the COUNT slots still tell which slots hold any
+    double mn = __builtin_inf(), mx = -__builtin_inf();
+    double* cnt = base + kRowSums * g.pend_blocks;
+    double* pmin = base + (kRowSums + 1) * g.pend_blocks;
+    double* pmax = base + (kRowSums + 2) * g.pend_blocks;
+    for (int b = threadIdx.x; b < used; b += kB) {
+      if (cnt[b] != 0.0) {
+        mn = nmin(mn, pmin[b]);
+        mx = nmax(mx, pmax[b]);
+      }
+      pmin[b] = 0.0;
+      pmax[b] = 0.0;
+    }
+    lds[kRowSums + 1][threadIdx.x] = mn;
+    lds[kRowSums + 2][threadIdx.x] = mx;
+  }
+  for (int k = 0; k <= kRowSums; ++k) {
     double v = 0.0;
     for (int b = threadIdx.x; b < used; b += kB) {
       v += base[k * g.pend_blocks + b];
@@ -435,16 +488,39 @@ __global__ __launch_bounds__(kB) void row_sums_pend_fold_kernel(RowSumsArgs g, i
   }
   __syncthreads();
   for (int h = kB / 2; h >= 1; h >>= 1) {
-    if (threadIdx.x < h)
-      for (int k = 0; k < kRowPendStats; ++k) lds[k][threadIdx.x] += lds[k][threadIdx.x + h];
+    if (threadIdx.x < h) {
+      for (int k = 0; k <= kRowSums; ++k) lds[k][threadIdx.x] += lds[k][threadIdx.x + h];
+      lds[kRowSums + 1][threadIdx.x] = nmin(lds[kRowSums + 1][threadIdx.x], lds[kRowSums + 1][threadIdx.x + h]);
+      lds[kRowSums + 2][threadIdx.x] = nmax(lds[kRowSums + 2][threadIdx.x], lds[kRowSums + 2][threadIdx.x + h]);
+    }
     __syncthreads();
   }
   if (threadIdx.x != 0) return;
+  double merged_min = 0.0, merged_max = 0.0;
   for (int k = 0; k < g.nout; ++k) {
     const RowSumsOut& o = g.out[k];
     if (o.first_row_only && r != 0) continue;
-    store_out(o, r, o.stat == kCOUNT ? lds[kRowSums][0] : lds[o.stat][0]);
+    double v;
+    if (o.stat == kCOUNT) v = lds[kRowSums][0];
+    else if (o.stat == kTMIN) v = lds[kRowSums + 1][0];
+    else if (o.stat == kTMAX) v = lds[kRowSums + 2][0];
+    else if (o.stat == kRANGE) v = merged_max - merged_min;
+    else v = lds[o.stat][0];
+    store_out(o, r, v);
+    if (o.stat == kTMIN) merged_min = load_out(o, r);
+    if (o.stat == kTMAX) merged_max = load_out(o, r);
   }
+}
+
+// the outputs a deferred update can fold: sums / COUNT added, extrema min / max, RANGE set
+bool pend_outputs_ok(const RowSumsArgs& a) {
+  for (int k = 0; k < a.nout; ++k) {
+    const RowSumsOut& o = a.out[k];
+    const bool ok = o.stat == kTMIN ? o.op == kMin : o.stat == kTMAX ? o.op == kMax
+                  : o.stat == kRANGE ? o.op == kSet : o.op == kAdd;
+    if (!ok) return false;
+  }
+  return true;
 }
 
 bool vec_ok(const void* p, DType dt, int64_t /*rs*/, int64_t cs) {
@@ -538,9 +614,7 @@ int row_sums_fold_blocks(int64_t rows, int64_t n) {
 
 int launch_row_sums_fold(const RowSumsArgs& a, int blocks_used, hipStream_t stream) {
   if (a.rows <= 0 || blocks_used <= 0 || !a.pend) return 0;
-  if (blocks_used > a.pend_blocks) return -2;
-  for (int k = 0; k < a.nout; ++k)
-    if (a.out[k].op != kAdd || a.out[k].stat == kTMIN || a.out[k].stat == kTMAX || a.out[k].stat == kRANGE) return -2;
+  if (blocks_used > a.pend_blocks || !pend_outputs_ok(a)) return -2;
   hipLaunchKernelGGL(row_sums_pend_fold_kernel, dim3(static_cast<unsigned>(a.rows)), dim3(kB), 0, stream, a,
                      blocks_used);
   return static_cast<int>(hipGetLastError());
@@ -549,10 +623,7 @@ int launch_row_sums_fold(const RowSumsArgs& a, int blocks_used, hipStream_t stre
 int launch_row_sums(const RowSumsArgs& a, hipStream_t stream) {
   if (a.rows <= 0) return 0;
   if (a.pend) {  // deferred mode: grid blocks only, within the slots, sums / W / COUNT ADD outputs
-    if (a.blocks < 2 || a.blocks > a.pend_blocks || a.ticket) return -2;
-    for (int k = 0; k < a.nout; ++k)
-      if (a.out[k].op != kAdd || a.out[k].stat == kTMIN || a.out[k].stat == kTMAX || a.out[k].stat == kRANGE)
-        return -2;
+    if (a.blocks < 2 || a.blocks > a.pend_blocks || a.ticket || !pend_outputs_ok(a)) return -2;
   }
   if ((a.n > 0 && a.x == nullptr) || (a.blocks > 1 && !a.ws && !a.pend)) return -2;  // empty rows: outputs only
   if (a.ticket && a.blocks < 2) return -2;

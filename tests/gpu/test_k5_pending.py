@@ -184,3 +184,64 @@ def test_graph_replays_fold_every_replay():
             tot += float(v[i % 3].double().sum())
             want = tot if cls is Sum else tot / (200_003 * (i + 1))
             assert float(met.compute()) == pytest.approx(want, rel=1e-9, abs=1e-6)
+
+
+def test_psnr_ctr_wc_deferred():
+    """PSNR (SSE / count / target extrema / data range), CTR and WeightedCalibration on the K5b
+    deferred mode: fold on every read against fp64 references (reference psnr.py:68-85,
+    click_through_rate.py:53-68, weighted_calibration.py)."""
+    from torcheval_amd.metrics import ClickThroughRate, PeakSignalNoiseRatio, WeightedCalibration
+
+    g = torch.Generator().manual_seed(17)
+    xs = [torch.rand(64, 3, 33, 35, generator=g) * 2 - 0.3 for _ in range(3)]
+    ts = [torch.rand(64, 3, 33, 35, generator=g) * (1.5 + i) - i for i in range(3)]
+    for auto in (True, False):
+        m = PeakSignalNoiseRatio(data_range=None if auto else 2.0, device=DEV)
+        for x, t in zip(xs, ts):
+            m.update(x.to(DEV), t.to(DEV))
+        assert m.__dict__["_pend_dirty"]
+        sse = sum(float(((x.double() - t.double()) ** 2).sum()) for x, t in zip(xs, ts))
+        n = sum(x.numel() for x in xs)
+        assert float(m.sum_squared_error) == pytest.approx(sse, rel=1e-6)
+        assert float(m.num_observations) == n
+        if auto:
+            lo, hi = min(float(t.min()) for t in ts), max(float(t.max()) for t in ts)
+            assert float(m.min_target) == lo and float(m.max_target) == hi
+            assert float(m.data_range) == pytest.approx(hi - lo, rel=1e-7)
+        rng = (hi - lo) if auto else 2.0
+        want = 10 * torch.log10(torch.tensor(rng ** 2 / (sse / n), dtype=torch.float64))
+        assert float(m.compute()) == pytest.approx(float(want), rel=1e-5)
+        # updates after a fold; a NaN target poisons the range like torch.minimum / maximum
+        m.update(xs[0].to(DEV), ts[0].to(DEV))
+        assert float(m.num_observations) == n + xs[0].numel()
+        bad = ts[1].clone()
+        bad[0, 0, 0, 0] = float("nan")
+        m.update(xs[1].to(DEV), bad.to(DEV))
+        if auto:
+            assert torch.isnan(m.min_target.cpu()) and torch.isnan(m.data_range.cpu())
+        m.reset()
+        assert float(m.num_observations) == 0.0 and float(m.sum_squared_error) == 0.0
+        m.update(xs[2].to(DEV), ts[2].to(DEV))
+        assert float(m.sum_squared_error) == pytest.approx(float(((xs[2].double() - ts[2].double()) ** 2).sum()), rel=1e-6)
+
+    tasks = 16
+    x = [torch.rand(tasks, 40_000, generator=g) for _ in range(2)]
+    w = [torch.rand(tasks, 40_000, generator=g) for _ in range(2)]
+    t = [torch.rand(tasks, 40_000, generator=g) for _ in range(2)]
+    ctr = ClickThroughRate(num_tasks=tasks, device=DEV)
+    ctr.update(x[0].to(DEV), w[0].to(DEV))
+    ctr.update(x[1].to(DEV), 0.5)
+    assert ctr.__dict__["_pend_dirty"]
+    clicks = (x[0].double() * w[0].double()).sum(1) + 0.5 * x[1].double().sum(1)
+    weights = w[0].double().sum(1) + 0.5 * 40_000
+    torch.testing.assert_close(ctr.compute().cpu(), clicks / weights, rtol=1e-10, atol=1e-12)
+    wc = WeightedCalibration(num_tasks=tasks, device=DEV)
+    wc.update(x[0].to(DEV), t[0].to(DEV), w[0].to(DEV))
+    wc.update(x[1].to(DEV), t[1].to(DEV), 2.0)
+    num = (x[0].double() * w[0].double()).sum(1) + 2.0 * x[1].double().sum(1)
+    den = (t[0].double() * w[0].double()).sum(1) + 2.0 * t[1].double().sum(1)
+    torch.testing.assert_close(wc.compute().cpu(), num / den, rtol=1e-10, atol=1e-12)
+    # one task, 1-D batches; a state_dict read folds
+    c1 = ClickThroughRate(device=DEV)
+    c1.update(x[0][0].repeat(3).to(DEV))
+    assert float(c1.state_dict()["click_total"][0]) == pytest.approx(3 * float(x[0][0].double().sum()), rel=1e-12)

@@ -27,7 +27,7 @@ import torch
 from torcheval_amd.ops import compiling, native
 
 PEND_SLOTS = 64  # csrc/include/tea_kernels.h kMomentsPendSlots
-ROWSUMS_PEND_STATS = 7  # kRowPendStats
+ROWSUMS_PEND_STATS = 9  # kRowPendStats: six sums, COUNT, target min / max
 ROWSUMS_PEND_BLOCKS = 2048  # kRowPendBlocks
 ROWSUMS_PEND_MIN = 32768  # rowsums.hip kSingle: shorter rows are one block, folded in-launch
 
@@ -116,13 +116,14 @@ class PendingMixin:
                                          st.get("stt"), st.get("sx"), st.get("sw"))
         d["_pend_r"] = 0
 
-    def _rowsums_deferred(self, x: torch.Tensor, w, w_scalar: float, spec: "RowSumsSpec") -> bool:
-        """K5b deferred update of ``spec``'s states from a long ROCm batch viewed as one row
-        (Sum / Mean): True when the launch ran (the states now have pending sums)."""
-        if not x.is_cuda or x.numel() <= ROWSUMS_PEND_MIN or compiling():
+    def _rowsums_deferred(self, x: torch.Tensor, w, w_scalar: float, spec: "RowSumsSpec", t=None) -> bool:
+        """K5b deferred update of ``spec``'s states from a long ROCm batch (``spec.rows`` rows;
+        one for Sum / Mean / PSNR, the tasks for CTR / WC), with an optional target operand:
+        True when the launch ran (the states now have pending sums)."""
+        if not x.is_cuda or x.numel() <= ROWSUMS_PEND_MIN * spec.rows or compiling():
             return False
         pend = self._pend_buffer(spec.rows * ROWSUMS_PEND_STATS * ROWSUMS_PEND_BLOCKS, x.device, spec)
-        used = native().row_sums_pend(x, None, w, w_scalar, [self.__dict__["_pv_" + n] for n in spec.names],
+        used = native().row_sums_pend(x, t, w, w_scalar, [self.__dict__["_pv_" + n] for n in spec.names],
                                       list(spec.codes), spec.rows, pend)
         if not used:
             return False

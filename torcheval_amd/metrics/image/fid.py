@@ -92,8 +92,14 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
 
 
 def _sandwich_blocks(n: int) -> int:
-    # 4 block columns: 1.875 n^3 flops instead of the dense 4 n^3, in 8 library GEMMs
-    return 4 if n >= 512 else 1
+    # 2 block columns: 2.5 n^3 flops instead of the dense 4 n^3 in 4 library GEMMs, 0.41 ms at
+    # D = 2048 against 0.54 for the two dense GEMMs; 3 / 4 / 8 blocks skip more zeros but their
+    # narrow GEMMs run at half the rate: 0.51 / 0.55 / 0.83 ms (profiles/fid_compute_timing_r6.json).
+    # TORCHEVAL_AMD_FID_SANDWICH_P: A/B of the block count (1 = the dense two GEMMs)
+    import os
+
+    p = int(os.environ.get("TORCHEVAL_AMD_FID_SANDWICH_P", "2"))
+    return p if n >= 512 else 1
 
 
 def _lt_s_l(L: Tensor, s: Tensor) -> Tensor:
@@ -101,9 +107,9 @@ def _lt_s_l(L: Tensor, s: Tensor) -> Tensor:
 
     On ROCm, triangle-aware: with L cut into p block columns, Y^T = L^T S is p GEMMs whose
     inner dimension skips L's zero blocks (block c: L[c0:, c]^T S[c0:, :]), and M = L^T Y is
-    computed for its lower block triangle only (block row r: L[r0:, r]^T Y[r0:, :r1]) - 1.875
-    n^3 instead of 4 n^3 flops at p = 4 - then ``sym_fill_upper`` mirrors the lower triangle
-    (the diagonal blocks are computed whole)."""
+    computed for its lower block triangle only (block row r: L[r0:, r]^T Y[r0:, :r1]) - 2.5 n^3
+    instead of 4 n^3 flops at p = 2 - then ``sym_fill_upper`` mirrors the lower triangle (the
+    diagonal blocks are computed whole)."""
     n = L.shape[0]
     p = _sandwich_blocks(n) if use_native(L) else 1
     if p == 1:
