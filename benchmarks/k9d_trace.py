@@ -27,9 +27,8 @@ def main() -> None:
     for _ in range(3):
         native().cholesky_factor_traced(s, L, linv, ctl, st, tr)
     torch.cuda.synchronize()
-    cyc = tr[nt * 8:].cpu()
-    w0 = (cyc[1:65] - cyc[0:64]).tolist()
-    w1 = (cyc[66:130] - cyc[65:129]).tolist()
+    cyc = tr[nt * 8: nt * 8 + 32].view(4, 8).cpu()
+    steps = [(cyc[k, 1:6] - cyc[k, 0:5]).tolist() for k in range(4)]
     t = tr[: nt * 8].view(nt, 8).cpu().double() * 0.01  # 100 MHz -> us
     t0 = float(t[0, 0])
     rows = []
@@ -51,7 +50,7 @@ def main() -> None:
     total = round(float(t[nt - 1, 6]) - t0, 1)
     print(json.dumps({"n": n, "status": st.cpu().tolist(), "total_us_first_stamp_to_last": total,
                       "median_us_per_column": med, "column_2": rows[min(2, nt - 1)], "column_last": rows[-1],
-                      "tile1_wave0_cycles_per_column": w0, "tile1_wave1_cycles_per_column": w1}))
+                      "tile1_phase0_step_cycles_gather_chol44_coef_publish_elim": steps}))
 
 
 if __name__ == "__main__":

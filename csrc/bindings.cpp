@@ -7,6 +7,8 @@
 #include <torch/extension.h>
 
 #include <cstdlib>
+#include <cstring>
+#include <atomic>
 #include <array>
 #include <mutex>
 #include <unordered_map>
@@ -428,6 +430,8 @@ void auc_scan(const Tensor& sorted, const Tensor& order, const Tensor& target,
                 "auc_scan: out_raw must be contiguous float64 [rows, 4]");
     a.out_raw = out_raw->data_ptr<double>();
   }
+  // the latest onesweep sort's timeout word on this stream (zero when none ever ran or it was clean)
+  a.sort_fault = static_cast<const uint32_t*>(zeroed_workspace(sorted, stream_for(sorted), 16 * 4, 10)) + 8;
   Tensor ws = at::empty({tea::auc_scan_workspace_bytes(rows, n)},
                         at::TensorOptions().dtype(at::kByte).device(sorted.device()));
   check_launch(tea::launch_auc_scan(a, ws.data_ptr(), stream_for(sorted)), "auc_scan");
@@ -1335,6 +1339,70 @@ void transpose_f32(const Tensor& x, const Tensor& out) {
 }
 
 // K3a: segmented descending radix sort of f32 rows -> (sorted scores, int32 permutation)
+// Onesweep look-back timeouts (RadixArgs::os_hdr[8], set by a pass whose tile gave up waiting on
+// its predecessors - forward progress relies on in-order workgroup dispatch per XCD).  Surfaced,
+// never silent: the K3 scan reading that sort's output returns NaN (AucScanArgs::sort_fault), the
+// word is copied asynchronously into pinned host memory after every onesweep sort, and the next
+// sort on the stream that finds it set warns and sends every later sort of the process through
+// the legacy (upsweep + downsweep) passes, which never wait on other workgroups.
+struct OnesweepHealth {
+  std::mutex mu;
+  std::unordered_map<uint64_t, uint32_t*> host_word;  // (device, stream) -> pinned copy of hdr[8]
+  std::atomic<bool> disabled{false};
+};
+
+OnesweepHealth& onesweep_health() {
+  static auto& h = *new OnesweepHealth();  // process lifetime (no teardown after HIP's)
+  return h;
+}
+
+uint64_t stream_key(const Tensor& x, hipStream_t st) {
+  return (static_cast<uint64_t>(x.device().index()) << 56) ^ reinterpret_cast<uint64_t>(st);
+}
+
+// true when a previous onesweep sort on this stream reported a timeout (then the device word is
+// cleared and onesweep is off for the process)
+bool onesweep_faulted(const Tensor& x, hipStream_t st) {
+  auto& h = onesweep_health();
+  if (h.disabled.load()) return true;
+  std::lock_guard<std::mutex> lock(h.mu);
+  auto it = h.host_word.find(stream_key(x, st));
+  if (it == h.host_word.end() || *reinterpret_cast<volatile uint32_t*>(it->second) == 0u) return false;
+  h.disabled.store(true);
+  auto* hdr = static_cast<uint32_t*>(zeroed_workspace(x, st, 16 * 4, 10));
+  TORCH_CHECK(hipMemsetAsync(hdr + 8, 0, 4, st) == hipSuccess, "sort_desc: timeout word reset failed");
+  static const char* kMsg =
+      "torcheval_amd K3a: an onesweep radix sort timed out in its look-back (its K3 result was NaN); "
+      "every later sort of this process takes the legacy radix passes";
+  // a Python warning when called from Python (pybind11 entry points hold the GIL; TORCH_WARN from a
+  // plain pybind11 function only reaches stderr), else c10's handler
+  if (Py_IsInitialized() && PyGILState_Check()) {
+    if (PyErr_WarnEx(PyExc_UserWarning, kMsg, 1) != 0) throw pybind11::error_already_set();
+  } else {
+    TORCH_WARN(kMsg);
+  }
+  return true;
+}
+
+void onesweep_watch(const Tensor& x, hipStream_t st, const uint32_t* hdr) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+  auto& h = onesweep_health();
+  uint32_t* word = nullptr;
+  {
+    std::lock_guard<std::mutex> lock(h.mu);
+    auto it = h.host_word.find(stream_key(x, st));
+    if (it == h.host_word.end()) {
+      void* p = nullptr;
+      if (hipHostMalloc(&p, 64, hipHostMallocDefault) != hipSuccess) return;
+      std::memset(p, 0, 64);
+      it = h.host_word.emplace(stream_key(x, st), static_cast<uint32_t*>(p)).first;
+    }
+    word = it->second;
+  }
+  (void)hipMemcpyAsync(word, hdr + 8, 4, hipMemcpyDeviceToHost, st);
+}
+
 // `fold` (optional, float64 [rows, ceil(n / 1024), 2]): with a target / label payload on the
 // onesweep path, the last pass also writes the K3 scan's 1024-sample tile totals there
 // (RadixArgs::fold_ab) and the call returns true; pass it to auc_scan as `tsum`.  False: not
@@ -1381,7 +1449,12 @@ bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
     const char* e = std::getenv("TORCHEVAL_AMD_K3_ONESWEEP");
     return e == nullptr || e[0] != '0';
   }();
-  if (onesweep && tea::radix_onesweep_ok(a.rows, a.n)) {
+  a.spin_limit = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K3_SPIN_LIMIT");  // test hook: force timeouts
+    const int v = e != nullptr ? std::atoi(e) : 0;
+    return v > 0 ? v : (1 << 22);
+  }();
+  if (onesweep && tea::radix_onesweep_ok(a.rows, a.n) && !onesweep_faulted(x, stream_for(x))) {
     // self-cleaning onesweep state (tea_kernels.h RadixArgs): header + digit totals, the status
     // planes and the group planes in three zeroed workspaces whose plane strides depend only on
     // their capacity; if any of them is (re)allocated, all three restart from zero together
@@ -1454,6 +1527,7 @@ bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
     }
   }
   check_launch(tea::launch_radix_sort_desc(a, stream_for(x)), "sort_desc");
+  if (a.os_hdr != nullptr) onesweep_watch(x, stream_for(x), a.os_hdr);
   return a.fold_ab != nullptr;
 }
 

@@ -102,6 +102,10 @@ struct AucScanArgs {
   int64_t n = 0;
   double* out_auroc = nullptr;  // [rows]
   double* out_auprc = nullptr;  // [rows]
+  // the onesweep sort's look-back timeout word of this stream (RadixArgs::os_hdr + 8) or null:
+  // non-zero means the sort that produced `sorted` may have misplaced keys, and every output of
+  // this scan is NaN instead of a wrong number
+  const uint32_t* sort_fault = nullptr;
   // sample-sharded (distributed) mode: per-row (TP, FP) that precede this shard in the global
   // descending order, and raw sums [rows, 4] = (roc sum, pr sum, local P, local N) instead of
   // the normalised areas (the caller all-reduces them and normalises by the global P, N)
@@ -463,7 +467,9 @@ struct RadixArgs {
   // passes that each rank, look back and scatter in ONE launch (no upsweeps).  Self-cleaning,
   // zero-initialised workspaces:
   uint32_t* os_hdr = nullptr;     // [16]: [4..7] dirty extents of the status / group planes,
-                                  // [8] look-back timeout flag
+                                  // [8] look-back timeout flag (cleared by each sort's histogram
+                                  // launch, so it describes the latest onesweep sort of the stream)
+  int spin_limit = 1 << 22;       // look-back polls before a tile gives up (TORCHEVAL_AMD_K3_SPIN_LIMIT)
   uint32_t* os_g = nullptr;       // [rows, 8 copies, 4, 256] digit totals (hist kernel; cleared by pass 3)
   uint32_t* os_status = nullptr;  // 2 planes of [rows * tiles, 256] ready-flagged tile counts
   int64_t os_splane = 0;          // words per status plane

@@ -36,6 +36,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "tea_kernels.h"
 
@@ -75,6 +76,9 @@ struct ChArgs {
   int* status;      // [0] info, [1] abort (zeroed)
   int ntasks;
   unsigned long long* trace;  // optional: [nt][8] s_memrealtime stamps of the D_c phases
+  int exp;                    // A/B probe (TORCHEVAL_AMD_K9D_PROBE, results invalid when set):
+                              // 1 skip the window updates, 2 skip the inverse's wave, 8 skip the
+                              // diagonal factorisation
 };
 
 // phase stamps of pair owner c (thread 0): 0 start, 1 updates done, 2 inverse arrived,
@@ -186,10 +190,14 @@ __device__ __forceinline__ double bcast(double x, int lane) {
   return __hiloint2double(hi, lo);
 }
 
+constexpr int kPB = 4;  // columns per elimination step of the diagonal-tile factorisation
+
 struct alignas(16) PotrfLds {
-  double col[kTB + 2][kTB];  // column j of the elimination (unscaled), slot j: written once (two
-                             // spare rows: the windows below read up to 64 values past slot j)
-  double rs[kTB], rd[kTB];
+  double col[kTB + 4][kTB];  // column j of L below the step's 4 x 4 pivot block (by row), slot j
+                             // written once; four spare rows for the reads past the last column
+  double piv[kTB / kPB][16]; // per step: L44 (l00, l10, l11, l20, l21, l22, l30, l31, l32, l33)
+                             // and 1 / l_qq (q = 0..3) for the inverse's wave
+  double g[kPB][kPB];        // the step's pivot block rows, gathered by their lanes
   int flag;                  // columns published by wave 0
 };
 
@@ -198,101 +206,253 @@ __shared__ double sB[kTB][kLd];
 __shared__ double sC[kTB][kLd];
 __shared__ PotrfLds pl;
 
-// The diagonal tile is factored by two waves with runtime column loops over a SHIFTING register
-// window: slot m of a lane's window holds column j + m at step j, every FMA writes its result one
-// slot down (r[m] <- r[m + 1] - u col[j + 1 + m]), so the pivot is always slot 0 and every
-// register index stays a compile-time constant without unrolling the 64 columns.  The window
-// narrows in four phases of 16 columns (64, 48, 32, 16 slots: 2496 FMAs per lane instead of the
-// triangle's 2016).  Fully unrolled column loops (round 6's first K9d, and K9c before it) ran
-// ~160 KB of straight-line code per tile and were instruction-fetch bound: ~900 cycles per
-// column, 24.8 us per tile (profiles/k9d_trace_r6.json).
-//
-// wave 0: lane i = row i of L; each column is published to the LDS ring (unscaled) with its
-// 1/sqrt(d) and 1/d, and its finished L entries go straight to Z (= sA) column j.
-// r[m] <- r[m + 1] - u c[m] for m < W - 1, r[W - 1] <- 0: the window shift of one elimination
-// step.  The column is read in 16-value chunks, each chunk's reads issued one chunk ahead of its
-// FMAs behind a compiler memory fence (unfenced, the compiler hoists all W reads and spills).
-template <int W>
-__device__ __forceinline__ void shift_elim(double (&r)[kTB], const double* c, double u) {
-  constexpr int kC = 16;
-  constexpr int NC = (W - 1 + kC - 1) / kC;
-  double v[2][kC];
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Two consecutive doubles of LDS (8-byte aligned; a broadcast read when every lane passes the same
+// address), by inline asm so that a chunk's reads are all in flight together; the caller waits
+// explicitly.  (Compiler-scheduled, such reads ran two in flight with a full LDS round trip per
+// pair, csrc/bench/fp64_rates.hip.)
+__device__ __forceinline__ u32x4 lds_2x64(unsigned addr) {
+  u32x4 v;
+  asm volatile("ds_read2_b64 %0, %1 offset1:1" : "=v"(v) : "v"(addr) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ double lo64(u32x4 v) { return __hiloint2double(static_cast<int>(v.y), static_cast<int>(v.x)); }
+__device__ __forceinline__ double hi64(u32x4 v) { return __hiloint2double(static_cast<int>(v.w), static_cast<int>(v.z)); }
+
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return static_cast<unsigned>(reinterpret_cast<uintptr_t>(p));
+}
+
+// N pairs of doubles from consecutive LDS (a broadcast read), all issued before one wait: the
+// compiler's own schedule of such reads keeps two in flight with a full round trip per pair
+// (~130 cycles each: the 16-value pivot-block gather alone cost ~1000 cycles per step)
+template <int N>
+__device__ __forceinline__ void lds_read_pairs(const void* p, double (&out)[2 * N]) {
+  const unsigned a = lds_addr(p);
+  u32x4 v[N];
 #pragma unroll
-  for (int q = 0; q < kC; ++q) v[0][q] = q < W - 1 ? c[q] : 0.0;
+  for (int t = 0; t < N; ++t) v[t] = lds_2x64(a + 16 * t);
+  if constexpr (N == 5) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]));
+  } else {
+    static_assert(N == 8, "lds_read_pairs: 5 or 8 pairs");
+    asm volatile("s_waitcnt lgkmcnt(0)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7]));
+  }
+#pragma unroll
+  for (int t = 0; t < N; ++t) {
+    out[2 * t] = lo64(v[t]);
+    out[2 * t + 1] = hi64(v[t]);
+  }
+}
+
+// 1 / sqrt(d): the hardware estimate + two Newton steps
+__device__ __forceinline__ double rsqrt_nr(double d) {
+  double r = __builtin_amdgcn_rsq(d);
+  r = fma(0.5 * r, fma(-d * r, r, 1.0), r);
+  r = fma(0.5 * r, fma(-d * r, r, 1.0), r);
+  return r;
+}
+
+// The window update of one 4-column step: r[m] <- r[m + 4] - sum_q c[q] col[j + q][j + 4 + m] for
+// m < W - 4, the top four slots cleared (slot m holds column j + m before, j + 4 + m after).  The
+// four columns' values are read 2 slots at a time (one ds_read2_b64 per column), each chunk
+// issued three chunks ahead of its FMAs (lgkmcnt counts at most 15), one explicit wait per chunk
+// (one chunk of 4 slots ahead left LDS latency exposed: 3500-4400 cycles per 60-slot step).
+template <int W>
+__device__ __forceinline__ void block_elim(double (&r)[kTB], const PotrfLds& p, int j, const double (&c)[kPB]) {
+  constexpr int kS = 2;                        // slots per chunk
+  constexpr int NC = (W - kPB + kS - 1) / kS;  // chunks
+  constexpr int kR = kPB * kS / 2;             // reads per chunk (4)
+  constexpr int kAhead = 3;                    // chunks in flight ahead of the one consumed
+  unsigned base[kPB];
+#pragma unroll
+  for (int q = 0; q < kPB; ++q) base[q] = lds_addr(&p.col[j + q][j + kPB]);
+  u32x4 v[kAhead + 1][kR];
+  auto issue = [&](int ch, u32x4 (&dst)[kR]) {
+#pragma unroll
+    for (int q = 0; q < kPB; ++q)
+#pragma unroll
+      for (int h = 0; h < kS / 2; ++h) dst[q * (kS / 2) + h] = lds_2x64(base[q] + 8 * (ch * kS + 2 * h));
+  };
+#pragma unroll
+  for (int ch = 0; ch < kAhead && ch < NC; ++ch) issue(ch, v[ch]);
 #pragma unroll
   for (int ch = 0; ch < NC; ++ch) {
-    if (ch + 1 < NC) {
+    u32x4 (&cur)[kR] = v[ch % (kAhead + 1)];
+    if (ch + kAhead < NC) issue(ch + kAhead, v[(ch + kAhead) % (kAhead + 1)]);
+    // reads still allowed in flight behind this chunk's (in order): min(kAhead, NC - 1 - ch) chunks
+    constexpr int kFull = kAhead * kR;
+    const int behind = (NC - 1 - ch < kAhead ? NC - 1 - ch : kAhead) * kR;
+    if (behind == kFull) {
+      asm volatile("s_waitcnt lgkmcnt(12)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
+    } else if (behind == 8) {
+      asm volatile("s_waitcnt lgkmcnt(8)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
+    } else if (behind == 4) {
+      asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur[0]), "+v"(cur[1]), "+v"(cur[2]), "+v"(cur[3]));
+    }
 #pragma unroll
-      for (int q = 0; q < kC; ++q) {
-        const int m = (ch + 1) * kC + q;
-        v[(ch + 1) & 1][q] = m < W - 1 ? c[m] : 0.0;
+    for (int sl = 0; sl < kS; ++sl) {
+      const int m = ch * kS + sl;
+      if (m < W - kPB) {
+        double acc = r[m + kPB];
+#pragma unroll
+        for (int q = 0; q < kPB; ++q) {
+          const u32x4 w = cur[q * (kS / 2) + (sl >> 1)];
+          acc = fma(-c[q], (sl & 1) ? hi64(w) : lo64(w), acc);
+        }
+        asm volatile("" : "+v"(acc));  // keep the FMAs here (sunk, they hold every read live)
+        r[m] = acc;
       }
     }
-    asm volatile("" ::: "memory");
+  }
 #pragma unroll
-    for (int q = 0; q < kC; ++q) {
-      const int m = ch * kC + q;
-      if (m < W - 1) r[m] = fma(-u, v[ch & 1][q], r[m + 1]);
-    }
-  }
-  r[W - 1] = 0.0;
+  for (int m = W - kPB; m < W; ++m) r[m] = 0.0;
 }
 
+// The diagonal tile's factorisation, 4 columns per step (a blocked right-looking Cholesky inside
+// the tile: the step's 4 x 4 pivot block factored redundantly in every lane, then a rank-4 window
+// update), by two waves with runtime step loops over a SHIFTING register window (slot m holds
+// column j + m, every update writes 4 slots down, so every register index is a compile-time
+// constant without unrolling the columns).  The window narrows in four phases of 16 columns
+// (64, 48, 32, 16 slots).  Measured per-column costs that motivated the blocking: a one-column
+// step spends ~700 cycles on its pivot, broadcast and hand-off whatever its window (~830 cycles
+// at 16 slots, profiles/k9d_trace_windowed_r6.json) - four columns per step pay that once.
+//
+// wave 0: lane i = row i of L.  Each step publishes the 4 finished columns below the pivot block
+// (col ring) and the block itself (piv) for wave 1, and writes its L entries to Z (= sA).
 template <int W>
-__device__ __forceinline__ void l_phase(double (&r)[kTB], int j0, int& fb, double (*Z)[kLd], PotrfLds& p,
+__device__ __forceinline__ void l_phase(double (&r)[kTB], int j0, int& fb, double (*Z)[kLd], PotrfLds& p, int probe,
                                         unsigned long long* cyc) {
+#define CH_CYC(k) do { if (cyc != nullptr && lane == 0) cyc[(js / kPB) * 8 + (k)] = clock64(); } while (0)
   const int lane = threadIdx.x & 63;
-  for (int j = j0; j < j0 + 16; ++j) {
-    if (cyc != nullptr && lane == 0) cyc[j] = clock64();
-    double d = bcast(r[0], j);
-    fb = (fb < 0 && !(d > 0.0)) ? j : fb;
-    d = fb >= 0 ? 1.0 : d;  // keep every later value finite; the caller discards the factor
-    const double aij = r[0];
-    p.col[j][lane] = lane > j ? aij : 0.0;
-    double rs = __builtin_amdgcn_rsq(d);
-    rs = fma(0.5 * rs, fma(-d * rs, rs, 1.0), rs);
-    rs = fma(0.5 * rs, fma(-d * rs, rs, 1.0), rs);
-    const double rd = rs * rs;
-    if (lane == 0) {
-      p.rs[j] = rs;
-      p.rd[j] = rd;
+  // the 4 steps of a phase unrolled: a runtime step loop made the back edge rotate every window
+  // register (r[m] <- r[m + 4] lands in a new register: ~1300 extra moves per wave and tile)
+#pragma unroll
+  for (int js = 0; js < 16; js += kPB) {
+    const int j = j0 + js;
+    CH_CYC(0);
+    // gather the pivot block rows j..j+3 (slots 0..3 of lanes j..j+3)
+    if (lane >= j && lane < j + kPB) {
+#pragma unroll
+      for (int b = 0; b < kPB; ++b) p.g[lane - j][b] = r[b];
     }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the column is in LDS before the flag
-    if (lane == 0) __hip_atomic_store(&p.flag, j + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    const double u = lane > j ? aij * rd : 0.0;
-    Z[lane][j] = lane > j ? aij * rs : (lane == j ? d * rs : 0.0);
-    shift_elim<W>(r, &p.col[j][j + 1], u);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    double gv[16];
+    lds_read_pairs<8>(&p.g[0][0], gv);
+    double a[kPB][kPB];
+#pragma unroll
+    for (int x = 0; x < kPB; ++x)
+#pragma unroll
+      for (int y = 0; y < kPB; ++y) a[x][y] = gv[kPB * x + y];
+    CH_CYC(1);
+    // 4 x 4 Cholesky (uniform: every lane the same values)
+    double l[kPB][kPB], rs[kPB];
+#pragma unroll
+    for (int q = 0; q < kPB; ++q) {
+      double d = a[q][q];
+#pragma unroll
+      for (int b = 0; b < q; ++b) d = fma(-l[q][b], l[q][b], d);
+      fb = (fb < 0 && !(d > 0.0)) ? j + q : fb;
+      d = fb >= 0 ? 1.0 : d;  // keep every later value finite; the caller discards the factor
+      rs[q] = rsqrt_nr(d);
+      l[q][q] = d * rs[q];
+#pragma unroll
+      for (int x = q + 1; x < kPB; ++x) {
+        double t = a[x][q];
+#pragma unroll
+        for (int b = 0; b < q; ++b) t = fma(-l[x][b], l[q][b], t);
+        l[x][q] = t * rs[q];
+      }
+    }
+    CH_CYC(2);
+    // this lane's coefficients l_i,j..j+3 (forward substitution with the pivot block)
+    double c[kPB];
+#pragma unroll
+    for (int q = 0; q < kPB; ++q) {
+      double t = r[q];
+#pragma unroll
+      for (int b = 0; b < q; ++b) t = fma(-c[b], l[q][b], t);
+      c[q] = t * rs[q];
+    }
+    const bool below = lane >= j + kPB;
+#pragma unroll
+    for (int q = 0; q < kPB; ++q) {
+      c[q] = below ? c[q] : 0.0;
+      p.col[j + q][lane] = c[q];
+      // L entries: below the block c, inside it the block's row, above it zero
+      const int rb = lane - j;
+      double lv = 0.0;
+#pragma unroll
+      for (int x = 0; x < kPB; ++x) lv = (rb == x && q <= x) ? l[x][q] : lv;
+      Z[lane][j + q] = below ? c[q] : lv;
+    }
+    CH_CYC(3);
+    if (lane == 0) {
+      double* pv = p.piv[j / kPB];
+      pv[0] = l[1][0];
+      pv[1] = l[2][0];
+      pv[2] = l[2][1];
+      pv[3] = l[3][0];
+      pv[4] = l[3][1];
+      pv[5] = l[3][2];
+#pragma unroll
+      for (int q = 0; q < kPB; ++q) pv[8 + q] = rs[q];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the step is in LDS before the flag
+    if (lane == 0) __hip_atomic_store(&p.flag, j + kPB, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    CH_CYC(4);
+    if (!(probe & 1)) block_elim<W>(r, p, j, c);
+    CH_CYC(5);
   }
+#undef CH_CYC
 }
 
-// wave 1: lane c = column c of inv(L), trailing wave 0 through the flag; x[m] holds row j + m
+// wave 1: lane c = column c of inv(L), trailing wave 0 through the flag; x[m] holds row j + m.
+// Per step: the pivot rows j..j+3 by forward substitution with the block, then the rank-4 update
+// of the rows below with the published columns.
 template <int W>
 __device__ __forceinline__ void x_phase(double (&x)[kTB], int j0, int* status, double (*X)[kLd], PotrfLds& p,
-                                        unsigned long long* cyc) {
+                                        int probe) {
   const int lane = threadIdx.x & 63;
-  for (int j = j0; j < j0 + 16; ++j) {
-    if (cyc != nullptr && lane == 0) cyc[j] = clock64();
+#pragma unroll
+  for (int js = 0; js < 16; js += kPB) {
+    const int j = j0 + js;
     unsigned spins = 0;
-    while (__hip_atomic_load(&p.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <= j) {
+    while (__hip_atomic_load(&p.flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < j + kPB) {
       if (++spins > kChSpin) {
         status[1] = 1;
         break;
       }
       __builtin_amdgcn_s_sleep(1);
     }
-    const double u = x[0] * p.rd[j];
-    X[j][lane] = x[0] * p.rs[j];
-    shift_elim<W>(x, &p.col[j][j + 1], u);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    double pv[16];
+    lds_read_pairs<8>(p.piv[j / kPB], pv);
+    const double l10 = pv[0], l20 = pv[1], l21 = pv[2], l30 = pv[3], l31 = pv[4], l32 = pv[5];
+    double xn[kPB];
+    xn[0] = x[0] * pv[8];
+    xn[1] = fma(-l10, xn[0], x[1]) * pv[9];
+    xn[2] = fma(-l21, xn[1], fma(-l20, xn[0], x[2])) * pv[10];
+    xn[3] = fma(-l32, xn[2], fma(-l31, xn[1], fma(-l30, xn[0], x[3]))) * pv[11];
+#pragma unroll
+    for (int q = 0; q < kPB; ++q) X[j + q][lane] = xn[q];
+    if (!(probe & 1)) block_elim<W>(x, p, j, xn);
   }
 }
 
 // Factor the symmetric tile in sA (row-major, full) in place: on return sA holds L (zero above
 // the diagonal) and sC holds inv(L).  Waves 0 and 1 only (the caller barriers).
-__device__ __noinline__ void potrf_tile(int* status, int c, unsigned long long* trace, int nt8) {
+__device__ __noinline__ void potrf_tile(int* status, int c, unsigned long long* trace, int probe) {
   double (*Z)[kLd] = sA;
   double (*X)[kLd] = sC;
   PotrfLds& p = pl;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (probe & 8) return;
   if (w == 0) {
     double r[kTB];
 #pragma unroll
@@ -302,25 +462,21 @@ __device__ __noinline__ void potrf_tile(int* status, int c, unsigned long long* 
       r[k + 1] = v.y;
     }
     int fb = -1;  // first non-positive (or NaN) pivot: LAPACK info - 1
-    // profiling hook: shader-clock stamps of every column of tile column 1 (trace[nt*8 ...])
-    unsigned long long* cyc = (trace != nullptr && c == 1) ? trace + nt8 : nullptr;
-    l_phase<64>(r, 0, fb, Z, p, cyc);
-    l_phase<48>(r, 16, fb, Z, p, cyc);
-    l_phase<32>(r, 32, fb, Z, p, cyc);
-    l_phase<16>(r, 48, fb, Z, p, cyc);
-    if (cyc != nullptr && lane == 0) cyc[64] = clock64();
+    unsigned long long* cyc = (trace != nullptr && c == 1) ? trace + 32 * 8 : nullptr;  // (nt = 32 in the probe)
+    l_phase<64>(r, 0, fb, Z, p, probe, cyc);
+    l_phase<48>(r, 16, fb, Z, p, probe, nullptr);
+    l_phase<32>(r, 32, fb, Z, p, probe, nullptr);
+    l_phase<16>(r, 48, fb, Z, p, probe, nullptr);
     if (lane == 0 && fb >= 0) atomicCAS(status, 0, kTB * c + fb + 1);
     if (trace != nullptr && lane == 0) trace[c * 8 + 7] = wall_clock64();  // wave 0's eliminations done
-  } else if (w == 1) {
+  } else if (w == 1 && !(probe & 2)) {
     double x[kTB];  // column `lane` of the inverse, window from row j
 #pragma unroll
     for (int k = 0; k < kTB; ++k) x[k] = k == lane ? 1.0 : 0.0;
-    unsigned long long* cyc = (trace != nullptr && c == 1) ? trace + nt8 + 65 : nullptr;
-    x_phase<64>(x, 0, status, X, p, cyc);
-    x_phase<48>(x, 16, status, X, p, cyc);
-    x_phase<32>(x, 32, status, X, p, cyc);
-    x_phase<16>(x, 48, status, X, p, cyc);
-    if (cyc != nullptr && lane == 0) cyc[64] = clock64();
+    x_phase<64>(x, 0, status, X, p, probe);
+    x_phase<48>(x, 16, status, X, p, probe);
+    x_phase<32>(x, 32, status, X, p, probe);
+    x_phase<16>(x, 48, status, X, p, probe);
   }
 }
 
@@ -379,7 +535,7 @@ __global__ __launch_bounds__(kCT, 1) void cholesky_kernel(ChArgs a) {
       acc_to_lds(acc, sA);
       if (t == 0) pl.flag = 0;
       __syncthreads();
-      potrf_tile(a.status, c, a.trace, a.nt * 8);
+      potrf_tile(a.status, c, a.trace, a.exp);
       __syncthreads();
       CH_TRACE(c, 5);
       // publish L(c, c) (zero above the diagonal) and its inverse, coalesced
@@ -441,6 +597,11 @@ int launch_cholesky(const double* A, int64_t lda, int64_t n, double* L, double* 
   a.ctl = ctl;
   a.status = status;
   a.trace = trace;
+  static const int probe = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_K9D_PROBE");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.exp = probe;
   int tasks = 0;
   for (int c = 0; c < nt; ++c) tasks += 1 + (nt - c - 2 > 0 ? nt - c - 2 : 0);
   a.ntasks = tasks;

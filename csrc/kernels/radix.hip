@@ -381,7 +381,6 @@ __device__ unsigned long long* g_radix_trace;
 #endif
 constexpr int kOSMaxTiles = 1024;
 constexpr uint32_t kReady = 0x80000000u;
-constexpr int kSpinLimit = 1 << 22;
 constexpr int kHistKeys = 16;  // keys per thread per round of the histogram kernel
 constexpr int kGCopies = 8;    // copies of the digit totals (histogram block % 8): 8x fewer
                                // same-address device atomics (256 blocks on one address: ~5 us)
@@ -409,6 +408,8 @@ __device__ __forceinline__ void os_add64(unsigned long long* p, unsigned long lo
 __global__ __launch_bounds__(kRT) void onesweep_hist_kernel(RadixArgs a, int64_t per_block) {
   constexpr int kC = 8;
   __shared__ uint32_t h[4][kC][kBins + 1];
+  // this sort's look-back timeout word starts clear (the passes run after this launch)
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.os_hdr[8] = 0u;
   for (int q = threadIdx.x; q < 4 * kC * (kBins + 1); q += kRT) (&h[0][0][0])[q] = 0u;
   __syncthreads();
   const int64_t row = blockIdx.y;
@@ -648,7 +649,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         if (g0 + q < g) {
-          while ((gv[q] >> 32) < static_cast<unsigned long long>(kGroup) && spins < kSpinLimit) {
+          while ((gv[q] >> 32) < static_cast<unsigned long long>(kGroup) && spins < a.spin_limit) {
             ++spins;
             gv[q] = os_get64(ga + static_cast<int64_t>(g0 + q) * kBins + t);
           }
@@ -663,7 +664,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         if (j0 + q < tile) {
-          while (!(sv2[q] & kReady) && spins < kSpinLimit) {
+          while (!(sv2[q] & kReady) && spins < a.spin_limit) {
             ++spins;
             sv2[q] = os_get(st + static_cast<int64_t>(j0 + q) * kBins + t);
           }
@@ -671,7 +672,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
         }
       }
     }
-    if (spins >= kSpinLimit) a.os_hdr[8] = 1u;
+    if (spins >= a.spin_limit) a.os_hdr[8] = 1u;  // surfaced: K3 scans return NaN, the next sort warns
     base[t] = gb + pre;
     // the last tile of the row: every tile of the row has consumed the digit totals
     if (last && tile == a.tiles - 1) {

@@ -196,6 +196,15 @@ __device__ void finalize_row(const AucScanArgs& a, int r, int ntiles, bool fused
       a.out_raw[4 * r + 2] = pn.x;
       a.out_raw[4 * r + 3] = pn.y;
     }
+    if (a.sort_fault != nullptr && *a.sort_fault != 0u) {  // the sort timed out: no wrong numbers
+      const double nan = __builtin_nan("");
+      tot = D2{nan, nan};
+      pn = D2{nan, nan};
+      if (a.out_raw) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a.out_raw[4 * r + k] = nan;
+      }
+    }
     const double factor = pn.x * pn.y;
     if (a.out_auroc) a.out_auroc[r] = factor == 0.0 ? 0.5 : tot.x / factor;
     if (a.out_auprc) a.out_auprc[r] = pn.x == 0.0 ? 0.0 : tot.y / pn.x;
