@@ -272,6 +272,16 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
             m.update_activations(torch.randn(4 * D, D, device=dev, generator=g) * (1.0 if real else 1.1), real)
         return m.compute
 
+    def fid_compute_singular():
+        # 1000 real + 1000 fake activations at D = 2048: both covariances singular (rank <= 999),
+        # so no Cholesky exists - K9p pivoted Cholesky + K9b on the r x r W S2 W^T
+        from torcheval_amd.metrics.image.fid import FrechetInceptionDistance
+
+        m = FrechetInceptionDistance(model=torch.nn.Identity(), feature_dim=D, device=dev)
+        for real in (True, False):
+            m.update_activations(torch.randn(n(1000), D, device=dev, generator=g) * (1.0 if real else 1.1), real)
+        return m.compute
+
     def small_functional():
         x, y = torch.randn(8, 6, device=dev, generator=g), randint(6, 8)
         return lambda: F.multiclass_accuracy(x, y)
@@ -331,6 +341,7 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         "FID update 1000x2048 activations": fid_update,
         "FID 50k x 2048 activations (50 updates of 1000)": fid_50k,
         "FID compute D=2048": fid_compute,
+        "FID compute D=2048, 1000+1000 activations (rank-deficient, K9p)": fid_compute_singular,
     }
 
 

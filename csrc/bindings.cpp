@@ -1214,6 +1214,50 @@ void cholesky_factor(const Tensor& a, const Tensor& l, const Tensor& linv, const
                "cholesky_factor");
 }
 
+// K9p: pivoted (rank-revealing) FP64 Cholesky of a symmetric PSD matrix in one cooperative
+// launch (csrc/kernels/pivchol.hip).  slots: int64 [pivchol_slot_words(n)] scratch, w: contiguous
+// float64 [N, N], N = pivchol_padded(n) (row j = factor column j in the original feature order),
+// piv: int32 [n], info: int32 [2] -> [rank, status (1 NaN in the matrix, 2 aborted)], ctl: int32
+// [>= 1] scratch.  Returns 0 launched, 3 the grid could not be co-scheduled, 4 n unsupported.
+int64_t pivchol_impl(const Tensor& a, const Tensor& slots, const Tensor& w, const Tensor& piv, const Tensor& info,
+                     const Tensor& ctl, unsigned long long* trace) {
+  check_gpu(a, "matrix");
+  TORCH_CHECK(a.dim() == 2 && a.size(0) == a.size(1) && a.scalar_type() == at::kDouble && a.stride(1) == 1,
+              "pivchol: matrix must be a row-contiguous float64 [n, n]");
+  const int64_t n = a.size(0);
+  const int64_t N = tea::pivchol_padded(n);
+  TORCH_CHECK(slots.scalar_type() == at::kLong && slots.is_contiguous() && slots.numel() >= tea::pivchol_slot_words(n) &&
+                  slots.device() == a.device(),
+              "pivchol: slots must be int64 [pivchol_slot_words(n)]");
+  TORCH_CHECK(w.scalar_type() == at::kDouble && w.is_contiguous() && w.numel() == N * N && w.device() == a.device(),
+              "pivchol: w must be a contiguous float64 [", N, ", ", N, "]");
+  TORCH_CHECK(piv.scalar_type() == at::kInt && piv.is_contiguous() && piv.numel() >= n && piv.device() == a.device(),
+              "pivchol: piv must be int32 [n]");
+  TORCH_CHECK(info.scalar_type() == at::kInt && info.is_contiguous() && info.numel() >= 2 && info.device() == a.device(),
+              "pivchol: info must be int32 [2]");
+  TORCH_CHECK(ctl.scalar_type() == at::kInt && ctl.is_contiguous() && ctl.numel() >= 1 && ctl.device() == a.device(),
+              "pivchol: ctl must be int32 [1]");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(a.device());
+  const int rc = tea::launch_pivchol(a.data_ptr<double>(), a.stride(0), n,
+                                     reinterpret_cast<unsigned long long*>(slots.data_ptr<int64_t>()), w.data_ptr<double>(),
+                                     piv.data_ptr<int>(), info.data_ptr<int>(),
+                                     reinterpret_cast<unsigned*>(ctl.data_ptr<int>()), stream_for(a), trace);
+  TORCH_CHECK(rc != 2, "pivchol: launch setup failed");
+  return rc;
+}
+int64_t pivchol(const Tensor& a, const Tensor& slots, const Tensor& w, const Tensor& piv, const Tensor& info,
+                const Tensor& ctl) {
+  return pivchol_impl(a, slots, w, piv, info, ctl, nullptr);
+}
+// profiling hook: pivchol with the launcher's phase stamps in trace (int64 >= 80)
+int64_t pivchol_traced(const Tensor& a, const Tensor& slots, const Tensor& w, const Tensor& piv, const Tensor& info,
+                       const Tensor& ctl, const Tensor& trace) {
+  TORCH_CHECK(trace.scalar_type() == at::kLong && trace.is_contiguous() && trace.numel() >= 80 &&
+                  trace.device() == a.device(),
+              "pivchol_traced: trace must be int64 [80]");
+  return pivchol_impl(a, slots, w, piv, info, ctl, reinterpret_cast<unsigned long long*>(trace.data_ptr<int64_t>()));
+}
+
 // test / profiling hook: cholesky_factor with per-tile-column phase stamps (s_memrealtime,
 // 100 MHz) of the pair-owner tasks in trace (int64 [nt * 8]), then the shader-clock stamps of every
 // column of tile column 1's factorisation (wave 0: [nt * 8, + 65), wave 1: [nt * 8 + 65, + 65))
@@ -1764,6 +1808,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cholesky_factor", &cholesky_factor, "K9d one-launch blocked FP64 Cholesky (padded factor, info, abort)",
         py::arg("a"), py::arg("l"), py::arg("linv"), py::arg("ctl"), py::arg("status"));
   m.def("cholesky_tiles", &tea::cholesky_tiles, "K9d 64 x 64 tiles per side");
+  m.def("pivchol", &pivchol, "K9p pivoted FP64 Cholesky (rank-revealing, W rows in feature order)",
+        py::arg("a"), py::arg("slots"), py::arg("w"), py::arg("piv"), py::arg("info"), py::arg("ctl"));
+  m.def("pivchol_padded", &tea::pivchol_padded, "K9p factor row stride");
+  m.def("pivchol_slot_words", &tea::pivchol_slot_words, "K9p hand-off slot words");
+  m.def("pivchol_traced", &pivchol_traced, "K9p with per-panel phase stamps (profiling hook)");
   m.def("cholesky_factor_traced", &cholesky_factor_traced, "K9d with per-column phase stamps (profiling hook)");
   m.def("trapz_sorted", &trapz_sorted, "K3t trapezoid area per row of x-sorted (x, y)", py::arg("x"),
         py::arg("y_bits"), py::arg("out"));
@@ -1917,6 +1966,7 @@ TORCH_LIBRARY(torcheval_amd, m) {
   m.def("sym_eigvals(Tensor m, Tensor(a!) lam, Tensor(b!) status) -> int");
   m.def("potrf_block(Tensor(a!) a, int k0, int b, Tensor(b!) linv, Tensor(c!) info) -> ()");
   m.def("cholesky_factor(Tensor a, Tensor(a!) l, Tensor(b!) linv, Tensor(c!) ctl, Tensor(d!) status) -> ()");
+  m.def("pivchol(Tensor a, Tensor(a!) slots, Tensor(b!) w, Tensor(c!) piv, Tensor(d!) info, Tensor(e!) ctl) -> int");
   m.def("cov_finalize(Tensor cov_sum, Tensor colsum, float n, Tensor(a!) out) -> ()");
   m.def("sym_fill_upper(Tensor(a!) m) -> ()");
   m.def("trapz_sorted(Tensor x, Tensor y_bits, Tensor(a!) out) -> ()");
@@ -1954,6 +2004,7 @@ TORCH_LIBRARY_IMPL(torcheval_amd, CUDA, m) {
   m.impl("potrf_block", &op_potrf_block);
   m.impl("cholesky_factor", &op_cholesky_factor);
   m.impl("cov_finalize", &cov_finalize);
+  m.impl("pivchol", &pivchol);
   m.impl("sym_fill_upper", &sym_fill_upper);
   m.impl("trapz_sorted", &trapz_sorted);
   m.impl("seg_reduce_rows", &op_seg_reduce_rows);
@@ -1996,6 +2047,9 @@ TORCH_LIBRARY_IMPL(torcheval_amd, Meta, m) {
   m.impl("potrf_block", [](const Tensor&, int64_t, int64_t, const Tensor&, const Tensor&) {});
   m.impl("cholesky_factor", [](const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&) {});
   m.impl("cov_finalize", [](const Tensor&, const Tensor&, double, const Tensor&) {});
+  m.impl("pivchol", [](const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&, const Tensor&) {
+    return int64_t{0};
+  });
   m.impl("sym_fill_upper", [](const Tensor&) {});
   m.impl("trapz_sorted", [](const Tensor&, const Tensor&, const Tensor&) {});
   m.impl("seg_reduce_rows", [](const Tensor&, const Tensor&, int64_t, at::IntArrayRef, at::IntArrayRef,

@@ -559,6 +559,13 @@ int launch_sym_fill_upper(double* M, int64_t ld, int64_t n, hipStream_t stream);
 int launch_cholesky(const double* A, int64_t lda, int64_t n, double* L, double* Linv, int* ctl, int* status,
                     hipStream_t stream, unsigned long long* trace = nullptr);
 int launch_potrf_block(double* A, int64_t lda, int k0, int b, double* Linv, int* info, hipStream_t stream);
+// K9p (pivchol.hip): pivoted FP64 Cholesky, one cooperative launch.  slots: pivchol_slot_words(n)
+// 64-bit words, w: [N, N] doubles, N = pivchol_padded(n); info {rank, status}; ctl 1 word.
+// 0 launched, 3 not co-schedulable, 4 n unsupported
+int pivchol_padded(int64_t n);
+int64_t pivchol_slot_words(int64_t n);
+int launch_pivchol(const double* A, int64_t lda, int64_t n, unsigned long long* slots, double* w, int* piv, int* info,
+                   unsigned* ctl, hipStream_t stream, unsigned long long* trace = nullptr);
 }  // namespace tea
 
 namespace tea {

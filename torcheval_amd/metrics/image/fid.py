@@ -10,9 +10,10 @@ MI355X path:
   state_dict, copies), so the states always reflect every update;
 * compute: tr sqrt(S1 S2) in FP64 from the symmetric L^T S2 L (S1 = L L^T, Cholesky) with an
   eigenvalues-only ``eigvalsh``, instead of the reference's non-symmetric ``linalg.eigvals``
-  (better conditioned, identical in exact arithmetic; singular S1 falls back to eigh).  On
-  ROCm: one covariance pass per side (fid_prep.hip), the one-launch K9d Cholesky, the
-  triangle-aware sandwich and the on-chip K9b eigenvalues;
+  (better conditioned, identical in exact arithmetic).  On ROCm: one covariance pass per side
+  (fid_prep.hip), the one-launch K9d Cholesky, the triangle-aware sandwich and the on-chip K9b
+  eigenvalues; when both sides have fewer samples than features (singular covariances), the
+  one-launch K9p pivoted Cholesky gives S1 = W^T W and K9b takes the r x r W S2 W^T;
 * sync: every state is ``merge="sum"``, so syncing is one RCCL all-reduce of 2 x D^2 + 2 x D
   floats; the model itself is never pickled or transferred (the reference all-gathers the
   whole pickled metric, Inception-v3 included).
@@ -58,37 +59,85 @@ def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
     cov_sum += torch.matmul(act.T, act)
 
 
-def _tr_sqrt_product(s1: Tensor, s2: Tensor) -> Tensor:
+def _tr_sqrt_product(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optional[int] = None) -> Tensor:
     """tr sqrt(S1 S2) for symmetric PSD S1, S2 (FP64, both exactly symmetric).
 
     The eigenvalues of S1 S2 equal those of the symmetric L^T S2 L when S1 = L L^T, so the
     fast path is one Cholesky (K9d), the triangle-aware sandwich and ONE eigenvalues-only
     ``eigvalsh`` (K9b; no eigenvectors, no back-transformation).  A singular S1 (fewer samples
     than features) has no Cholesky factor; the same holds with the roles swapped when S2 has
-    one.  When both are singular, a full ``eigh`` gives S1 = W W^T with W = V_r sqrt(lam_r) over
-    the numerically non-zero eigenvalues (rank r, the ``matrix_rank`` tolerance of the FP64
-    matrix), and the eigvalsh runs on the r x r matrix W^T S2 W: the same non-zero spectrum as
-    S1 S2.  The tolerance is deliberately the FP64 one: covariances assembled from FP32 state
-    sums carry rounding "noise" eigenvalues well above it, and the reference's
-    ``eigvals(S1 S2)`` includes their square roots too, so they are kept (r is then the FP64
-    numerical rank, usually above the sample rank - the r x r saving shrinks accordingly)."""
-    L, info = _chol(s1)
-    if info == 0:
-        m = _lt_s_l(L, s2)
-    elif (L2 := _chol(s2))[1] == 0:
+    one.  When both are singular, S1 = W^T W with W [r, D] of rank r, and the eigvalsh runs on
+    the r x r matrix W S2 W^T: the same non-zero spectrum as S1 S2.  On ROCm W comes from K9p
+    (csrc/kernels/pivchol.hip), a pivoted (rank-revealing) Cholesky stopping at the LAPACK
+    dpstrf tolerance D eps max diag; elsewhere (and as K9p's fallback) from ``eigh`` over the
+    eigenvalues above the ``matrix_rank`` tolerance of the FP64 matrix.  Both tolerances are
+    the FP64 ones: covariances assembled from FP32 state sums carry rounding "noise" spectrum
+    well above them, and the reference's ``eigvals(S1 S2)`` includes its square roots too, so it
+    is kept (r is then the FP64 numerical rank, usually above the sample rank).
+
+    ``n1`` / ``n2`` (optional sample counts) mark a side with n <= D as singular up front, so
+    its Cholesky is not attempted; the pivoted factor then takes the side with fewer samples."""
+    d = s1.shape[0]
+    sing1 = n1 is not None and n1 <= d
+    sing2 = n2 is not None and n2 <= d
+    if not sing1:
+        L, info = _chol(s1)
+        if info == 0:
+            return _sqrt_eig_sum(_lt_s_l(L, s2))
+    if not sing2:
         # S1 singular, S2 not: S1 S2 and S2 S1 share their spectrum, so factor S2 instead
-        # (one more Cholesky rather than a full eigh with eigenvectors)
-        m = _lt_s_l(L2[0], s1)
-    else:
-        lam, vec = torch.linalg.eigh(s1)
-        keep = lam > lam.max().clamp(min=0) * lam.numel() * torch.finfo(lam.dtype).eps
-        w = vec[:, keep] * lam[keep].sqrt()
-        if w.shape[1] == 0:
-            return torch.zeros((), dtype=s1.dtype, device=s1.device)
-        m = w.T @ s2 @ w
-        m = (m + m.T) / 2
-    ev = sym_eigvalsh(m)
-    return ev.clamp(min=0).sqrt().sum()
+        # (one more Cholesky rather than a rank-revealing factorisation)
+        L2, info2 = _chol(s2)
+        if info2 == 0:
+            return _sqrt_eig_sum(_lt_s_l(L2, s1))
+    a, b = (s2, s1) if (n1 is not None and n2 is not None and n2 < n1) else (s1, s2)
+    w = _pivoted_factor(a)
+    if w is None:
+        w = _eigh_factor(a)
+    if w.shape[0] == 0:
+        return torch.zeros((), dtype=s1.dtype, device=s1.device)
+    m = w @ (b @ w.T)
+    return _sqrt_eig_sum((m + m.T) / 2)
+
+
+def _sqrt_eig_sum(m: Tensor) -> Tensor:
+    return sym_eigvalsh(m).clamp(min=0).sqrt().sum()
+
+
+def _eigh_factor(s: Tensor) -> Tensor:
+    """W [r, D] with S = W^T W from ``eigh``: the eigenvectors of the eigenvalues above the FP64
+    ``matrix_rank`` tolerance, scaled by their square roots (the CPU path and K9p's fallback)."""
+    lam, vec = torch.linalg.eigh(s)
+    keep = lam > lam.max().clamp(min=0) * lam.numel() * torch.finfo(lam.dtype).eps
+    return (vec[:, keep] * lam[keep].sqrt()).T
+
+
+def _pivoted_factor(s: Tensor) -> Optional[Tensor]:
+    """W [r, D] with S = W^T W + O(tol) from K9p's pivoted Cholesky (rows in the original
+    feature order), or None when the native path does not apply / its grid aborted."""
+    n = s.shape[0]
+    if not (use_native(s) and s.dtype == torch.float64 and s.dim() == 2 and 1 <= n <= 2048):
+        return None
+    from torcheval_amd.ops import native
+    from torcheval_amd.ops.hostread import read_ints
+
+    nat = native()
+    N = nat.pivchol_padded(n)
+    a = s if s.stride(1) == 1 else s.contiguous()
+    slots = torch.empty(nat.pivchol_slot_words(n), dtype=torch.int64, device=s.device)
+    w = torch.empty(N, N, dtype=torch.float64, device=s.device)
+    piv = torch.empty(n, dtype=torch.int32, device=s.device)
+    info = torch.empty(2, dtype=torch.int32, device=s.device)
+    ctl = torch.empty(1, dtype=torch.int32, device=s.device)
+    if nat.pivchol(a, slots, w, piv, info, ctl) != 0:
+        return None  # (the grid could not be co-scheduled)
+    rank, status = read_ints(info)
+    if status & 2:
+        warnings.warn("K9p pivoted Cholesky grid aborted (a hand-off timed out); using eigh", RuntimeWarning)
+        return None
+    if status & 1:  # a NaN in the matrix: the result is NaN, as the eigh path's would be
+        return torch.full((1, n), float("nan"), dtype=torch.float64, device=s.device)
+    return w[:rank, :n]
 
 
 def _sandwich_blocks(n: int) -> int:
@@ -194,10 +243,12 @@ def frechet_distance(mu1: Tensor, sigma1: Tensor, mu2: Tensor, sigma2: Tensor) -
     return _frechet_symmetric(mu1, (s1 + s1.T) / 2, mu2, (s2 + s2.T) / 2)
 
 
-def _frechet_symmetric(mu1: Tensor, s1: Tensor, mu2: Tensor, s2: Tensor) -> Tensor:
-    """``frechet_distance`` of exactly symmetric FP64 covariances."""
+def _frechet_symmetric(mu1: Tensor, s1: Tensor, mu2: Tensor, s2: Tensor, n1: Optional[int] = None,
+                       n2: Optional[int] = None) -> Tensor:
+    """``frechet_distance`` of exactly symmetric FP64 covariances (``n1`` / ``n2``: sample
+    counts, see ``_tr_sqrt_product``)."""
     mu1, mu2 = mu1.double(), mu2.double()
-    tr_sqrt = _tr_sqrt_product(s1, s2)
+    tr_sqrt = _tr_sqrt_product(s1, s2, n1, n2)
     return (mu1 - mu2).square().sum() + s1.trace() + s2.trace() - 2 * tr_sqrt
 
 
@@ -376,7 +427,7 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
         fake_mean = self.fake_sum.double() / nf
         real_cov = _covariance(self.real_cov_sum, self.real_sum, nr)
         fake_cov = _covariance(self.fake_cov_sum, self.fake_sum, nf)
-        return _frechet_symmetric(real_mean, real_cov, fake_mean, fake_cov).to(torch.float32)
+        return _frechet_symmetric(real_mean, real_cov, fake_mean, fake_cov, nr, nf).to(torch.float32)
 
     real_sum = _staged_state("real_sum", 0)
     real_cov_sum = _staged_state("real_cov_sum", 0)
