@@ -933,7 +933,18 @@ static tea::MomentsArgs moments_args(const optional<Tensor>& x, const optional<T
   return a;
 }
 
+// deferred-mode pend buffer size for d columns and statistic set `need` (the one place the
+// slot layout is computed; Python sizes its buffers from here)
+int64_t column_moments_pend_numel(int64_t d, int64_t need) {
+  const int ns = tea::moments_ns_of(static_cast<int>(need));
+  TORCH_CHECK(ns > 0, "column_moments_pend: the slot layout covers the statistic sets {sse}, {sse, st, stt} and "
+              "{sse, st, stt, sx} only (need = ", need, ")");
+  return tea::kMomentsPendSlots * (ns * d + 1);
+}
+
 static void bind_pend(tea::MomentsArgs& a, const Tensor& pend, const Tensor& ref) {
+  TORCH_CHECK(tea::moments_ns(a) > 0, "column_moments: deferred mode needs the statistic set {sse}, {sse, st, stt} "
+              "or {sse, st, stt, sx} (need = ", tea::moments_need(a), ")");
   TORCH_CHECK(pend.scalar_type() == at::kDouble && pend.is_contiguous() && pend.device() == ref.device() &&
                   pend.numel() >= tea::kMomentsPendSlots * (tea::moments_ns(a) * a.d + 1),
               "column_moments: pend must be a contiguous float64 buffer of slots * (ns * d + 1)");
@@ -1773,6 +1784,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("rows"), py::arg("pend"));
   m.def("row_sums_fold", &row_sums_fold, "K5b pending slots -> outputs (ADD), slots zeroed", py::arg("pend"),
         py::arg("used"), py::arg("outs"), py::arg("codes"), py::arg("rows"));
+  m.def("column_moments_pend_numel", &column_moments_pend_numel, "deferred-mode pend buffer numel for (d, need)");
   m.def("column_moments_pend", &column_moments_pend,
         "K5 deferred-mode class update: FP64 column partials added to pending slots; returns the slots used",
         py::arg("x"), py::arg("t"), py::arg("w"), py::arg("sse"), py::arg("st"), py::arg("stt"), py::arg("sx"),

@@ -251,10 +251,14 @@ int column_moments_blocks(int64_t n, int64_t d);
 // v2 plan: whether it applies, and its geometry / workspace size (doubles and tickets)
 bool column_moments_v2_plan(MomentsArgs& a, int64_t* ws_doubles, int64_t* tickets);
 constexpr int kMomentsPendSlots = 64;
-inline int moments_ns(const MomentsArgs& a) {
-  const int need = (a.sse ? 1 : 0) | (a.st ? 2 : 0) | (a.stt ? 4 : 0) | (a.sx ? 8 : 0);
-  return need == 1 ? 1 : need == 7 ? 3 : 4;
+// the deferred-mode slot layout: statistic k of the set sits in slot row k, which holds for the
+// sets {sse} (need 1), {sse, st, stt} (7) and {sse, st, stt, sx} (15) only: 0 for any other set
+// (constexpr: callable from the fold kernel too)
+constexpr int moments_ns_of(int need) { return need == 1 ? 1 : need == 7 ? 3 : need == 15 ? 4 : 0; }
+constexpr int moments_need(const MomentsArgs& a) {
+  return (a.sse ? 1 : 0) | (a.st ? 2 : 0) | (a.stt ? 4 : 0) | (a.sx ? 8 : 0);
 }
+constexpr int moments_ns(const MomentsArgs& a) { return moments_ns_of(moments_need(a)); }
 // pending slots r < rows_used of a deferred-mode pend buffer -> outputs (+= in float32; sse /
 // st / stt / sx at out_stride, sw scalar), slots zeroed
 int launch_moments_fold(const MomentsArgs& a, int rows_used, hipStream_t stream);

@@ -724,8 +724,7 @@ __global__ __launch_bounds__(kB) void moments_v2_kernel(MomentsArgs a) {
 // deferred-mode fold: thread per column, every slot's loads in flight 8 at a time, slots zeroed
 __global__ __launch_bounds__(kB) void moments_pend_fold_kernel(MomentsArgs a, int R) {
   const int64_t d = a.d;
-  const int need = (a.sse ? 1 : 0) | (a.st ? 2 : 0) | (a.stt ? 4 : 0) | (a.sx ? 8 : 0);
-  const int ns = need == 1 ? 1 : need == 7 ? 3 : 4;  // tea_kernels.h moments_ns
+  const int ns = moments_ns(a);  // the binding admits only the sets whose layout this reads
   const int64_t col = static_cast<int64_t>(blockIdx.x) * kB + threadIdx.x;
   float* outs[4] = {a.sse, a.st, a.stt, a.sx};
   if (col < d) {

@@ -26,7 +26,11 @@ Engine policies (read once per process; not flags):
                                                every group; ``0``: always torch.distributed
 ``TORCHEVAL_AMD_RCCL_ASYNC_ERROR_HANDLING``    1 (default): a failed direct communicator ends
                                                the process (c10d's default); 0: the next sync
-                                               votes group-wide and rebuilds
+                                               votes group-wide and rebuilds - the vote is a
+                                               blocking torch.distributed MIN all-reduce + a
+                                               host read before EVERY direct sync at ws > 1
+                                               (async side-stream syncs included, which then
+                                               synchronise the host once per call)
 ``TORCHEVAL_AMD_ASYNC_DIRECT_RCCL``            1: async syncs ride the direct path on a side
                                                stream (default: torch.distributed async)
 ``TORCHEVAL_AMD_RCCL_WATCHDOG``                0: no completion watchdog (A/B only)

@@ -105,10 +105,9 @@ def fused_regression_update(metric, input: torch.Tensor, target: torch.Tensor, w
             # metric's pending slots; the states fold them in when read
             d = input.shape[1]
             need = sum(b for k, b in (("sse", 1), ("st", 2), ("stt", 4)) if kw[k] is not None)
-            ns = 1 if need == 1 else 3 if need == 7 else 4  # tea_kernels.h moments_ns
-            from torcheval_amd.metrics._pending import PEND_SLOTS
-
-            pend = metric._pend_buffer(PEND_SLOTS * (ns * d + 1), input.device, spec)
+            # the slot layout comes from C++ (tea_kernels.h moments_ns_of; it rejects a statistic
+            # set the fold kernel cannot read)
+            pend = metric._pend_buffer(native().column_moments_pend_numel(d, need), input.device, spec)
             slots = native().column_moments_pend(input, target, w, kw["sse"], kw["st"], kw["stt"], None, kw["sw"], pend)
             if slots:
                 metric._pend_mark(slots, spec)

@@ -1,4 +1,5 @@
-"""HIP-graph capture of metric ``update`` calls.
+"""HIP-graph capture of metric ``update`` calls (EXPERIMENTAL: no measured case is faster than
+direct calls yet - replay 11.2-17.8 us vs 5.5-12.6 us direct on every metric the GPU tests graph).
 
 ``GraphedUpdate`` records ``metric.update(*static_inputs)`` once into a HIP graph
 (``torch.cuda.CUDAGraph`` on ROCm) and then replays it: per call, the new inputs are copied into
