@@ -65,6 +65,8 @@ if HIST:  # histogram blocks of 4096 x h keys (TORCHEVAL_AMD_K3_HIST_ROUNDS), de
     MODES = [("1", "", "0h" + h) for h in HIST]
 if os.environ.get("K3_AB_ROUNDS") == "1":
     MODES += [("1", "16", "1"), ("0", "16", "1")]
+if os.environ.get("K3_AB_BUCKET") == "1":  # splitter-bucket mode (default) vs the four onesweep passes
+    MODES = [("1", "", "0b1"), ("1", "", "0b0"), ("1", "", "0b1"), ("1", "", "0b0")]
 for mode, rounds, fold in MODES:
     env = dict(os.environ, TORCHEVAL_AMD_K3_ONESWEEP=mode, TORCHEVAL_AMD_K3_ROUNDS=rounds,
                TORCHEVAL_AMD_K3_FOLD=fold[0], REPO=repo)
@@ -72,6 +74,8 @@ for mode, rounds, fold in MODES:
         env["TORCHEVAL_AMD_K3_FOLD_PROBE"] = fold[2:]
     if fold[1:2] == "h":
         env["TORCHEVAL_AMD_K3_HIST_ROUNDS"] = fold[2:]
+    if fold[1:2] == "b":
+        env["TORCHEVAL_AMD_K3_BUCKET"] = fold[2:]
     out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     if out.returncode != 0:
         print(out.stdout[-2000:], out.stderr[-4000:])
@@ -82,5 +86,6 @@ for mode, rounds, fold in MODES:
     line["tile_sums_fold"] = fold[0] == "1" and mode == "1"
     line["fold_probe"] = fold[2:] if fold[1:2] == "p" else None
     line["hist_rounds"] = fold[2:] if fold[1:2] == "h" else "1"
+    line["bucket"] = fold[2:] != "0" if fold[1:2] == "b" else None
     line["n"] = int(os.environ.get("AUROC_N", "1000000"))
     print(json.dumps(line), flush=True)

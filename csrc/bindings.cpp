@@ -1482,13 +1482,14 @@ bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
   if (a.rows == 0 || a.n == 0) return false;
   a.tiles = tea::radix_sort_tiles(a.rows, a.n);
   const int64_t m = a.rows * a.n;
-  Tensor ws = at::empty({4 * m + a.rows * 256 * a.tiles}, x.options().dtype(at::kInt));
+  Tensor ws = at::empty({4 * m + a.rows * 256 * a.tiles + a.rows * 512}, x.options().dtype(at::kInt));
   uint32_t* base = reinterpret_cast<uint32_t*>(ws.data_ptr<int32_t>());
   a.keys0 = base;
   a.vals0 = base + m;
   a.keys1 = base + 2 * m;
   a.vals1 = base + 3 * m;
   a.hist = base + 4 * m;
+  uint32_t* bkt = a.hist + a.rows * 256 * a.tiles;  // splitter-bucket mode: splitters, bucket sizes
   a.ngroups = tea::radix_sort_groups(a.tiles);
   // self-cleaning: [header: cells left dirty in region 3 | pad | 4 regions of `region` cells]
   int64_t cap = 0;
@@ -1541,6 +1542,8 @@ bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
     a.os_splane = scap / 8;  // two u32 planes
     a.os_gacc = gws;
     a.os_gplane = gcap / 16;  // two u64 planes
+    a.bkt_spl = bkt;
+    a.bkt_cnt = bkt + a.rows * 256;
   }
   Tensor pl;
   if (payload.has_value() && payload_kind != 0) {

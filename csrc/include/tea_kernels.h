@@ -488,7 +488,13 @@ struct RadixArgs {
   // 0: descending (NaN first); ~0u: ascending (NaN last, as torch.sort ascending), both stable -
   // XORed into every key at load and out of it at the final store
   uint32_t key_xor = 0;
+  // splitter-bucket mode (radix_bucket_ok; onesweep workspaces required): 255 equal-frequency
+  // splitters per row from a sorted sample, ONE stable onesweep pass scatters the keys into the
+  // 256 buckets they delimit, and one workgroup per bucket finishes it in LDS
+  uint32_t* bkt_spl = nullptr;  // [rows, 256] splitters (sample kernel)
+  uint32_t* bkt_cnt = nullptr;  // [rows, 256] bucket sizes (the pass's first tile)
 };
+bool radix_bucket_ok(int64_t rows, int64_t n);    // the rows / lengths the bucket mode takes
 bool radix_onesweep_ok(int64_t rows, int64_t n);  // the tiling the onesweep passes take
 int64_t radix_onesweep_status_words(int64_t rows, int64_t n);
 int64_t radix_onesweep_group_words(int64_t rows, int64_t n);

@@ -374,10 +374,23 @@ __device__ unsigned long long* g_radix_trace;
     if (threadIdx.x == 0) g_radix_trace[(static_cast<size_t>(pass) * 4096 + blockIdx.x) * 8 + (i)] = \
         __builtin_amdgcn_s_memrealtime();                                                        \
   } while (0)
+#define BKT_TRACE(region, i)                                                                     \
+  do {                                                                                           \
+    if (threadIdx.x == 0) g_radix_trace[(static_cast<size_t>(region) * 4096 + blockIdx.x) * 8 + (i)] = \
+        __builtin_amdgcn_s_memrealtime();                                                        \
+  } while (0)
 #else
 #define RDX_TRACE(i) \
   do {               \
   } while (0)
+#define BKT_TRACE(region, i) \
+  do {                       \
+  } while (0)
+#endif
+#ifdef TEA_RADIX_TRACE
+#define BKT_NBITS(v) g_radix_trace[(static_cast<size_t>(7) * 4096 + blockIdx.x) * 8] = (v)
+#else
+#define BKT_NBITS(v) (void)(v)
 #endif
 constexpr int kOSMaxTiles = 1024;
 constexpr uint32_t kReady = 0x80000000u;
@@ -518,7 +531,16 @@ __device__ __forceinline__ void fold_tile_sums(const RadixArgs& a, int64_t row, 
 }
 
 // one pass: load + rank as radix_downsweep_kernel, then publish / look back, then scatter
-template <int kRounds, int VMODE, typename PT = uint32_t, int KIND = 0, bool FOLD = false>
+// bucket of a key in splitter-bucket mode: the number of the 255 ascending splitters below it
+// (spl[255] = ~0u is never below a key): 8 LDS probes, monotone in the key
+__device__ __forceinline__ uint32_t bkt_of(uint32_t key, const uint32_t* spl) {
+  uint32_t lo = 0;
+#pragma unroll
+  for (uint32_t step = 128; step > 0; step >>= 1) lo += spl[lo + step - 1] < key ? step : 0u;
+  return lo;
+}
+
+template <int kRounds, int VMODE, typename PT = uint32_t, int KIND = 0, bool FOLD = false, bool BKT = false>
 __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const uint32_t* keys_in,
                                                             const uint32_t* vals_in, uint32_t* keys_out,
                                                             uint32_t* vals_out, int pass) {
@@ -531,6 +553,8 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   __shared__ uint32_t sk[kRTile], sv[kRTile];
   __shared__ double fa[FOLD ? kRTile + 1 : 1], fb[FOLD ? kRTile + 1 : 1];
   __shared__ double fw[2][kRWaves];
+  __shared__ uint32_t sspl[BKT ? kBins : 1];
+  __shared__ uint8_t sdg[BKT ? kRTile : 1];  // bucket mode: the staged keys' buckets (one search per key)
   uint32_t my_cnt = 0;  // this tile's count of digit threadIdx.x
   // tile id = blockIdx: workgroups are dispatched in order per XCD, so the lowest unfinished
   // tile only ever waits on finished ones.  (Ids from a counter ticket, the textbook guard,
@@ -541,6 +565,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   const int tile = static_cast<int>(id - row * a.tiles);
   const int shift = 8 * pass;
   const bool last = pass == 3;
+  if constexpr (BKT) sspl[threadIdx.x] = threadIdx.x < kBins - 1 ? a.bkt_spl[row * kBins + threadIdx.x] : ~0u;
   const int lane = lane_id();
   const int w = threadIdx.x >> 6;
   const int64_t tbase = static_cast<int64_t>(tile) * kRTile;
@@ -560,6 +585,9 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   uint32_t gtot = 0;
 #pragma unroll
   for (int c = 0; c < kGCopies; ++c) gtot += a.os_g[((row * kGCopies + c) * 4 + pass) * kBins + threadIdx.x];
+  if constexpr (BKT) {
+    if (tile == 0) a.bkt_cnt[row * kBins + threadIdx.x] = gtot;  // the bucket sizes, for the LDS stage
+  }
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
     const bool ok = wbase + j * 64 + lane < a.n;
@@ -586,11 +614,18 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   }
   // wave-local stable ranks (as radix_downsweep_kernel)
   const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  uint32_t dj[BKT ? kRounds : 1];
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
     const bool valid = wbase + j * 64 + lane < a.n;
     const uint64_t active = __ballot(valid);
-    const uint32_t d = (k[j] >> shift) & 0xffu;
+    uint32_t d;
+    if constexpr (BKT) {
+      d = bkt_of(k[j], sspl);
+      dj[j] = d;
+    } else {
+      d = (k[j] >> shift) & 0xffu;
+    }
     const uint64_t peers = match_digit(d, active);
     const uint64_t pb = peers & below;
     r[j] = wc[w][d] + static_cast<uint32_t>(__popcll(pb));
@@ -675,7 +710,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     if (spins >= a.spin_limit) a.os_hdr[8] = 1u;  // surfaced: K3 scans return NaN, the next sort warns
     base[t] = gb + pre;
     // the last tile of the row: every tile of the row has consumed the digit totals
-    if (last && tile == a.tiles - 1) {
+    if ((last || BKT) && tile == a.tiles - 1) {
 #pragma unroll
       for (int q = 0; q < kGCopies * 4; ++q) a.os_g[(row * kGCopies * 4 + q) * kBins + t] = 0u;
     }
@@ -696,10 +731,13 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
 #pragma unroll
   for (int j = 0; j < kRounds; ++j) {
     if (wbase + j * 64 + lane < a.n) {
-      const uint32_t d = (k[j] >> shift) & 0xffu;
+      uint32_t d;
+      if constexpr (BKT) d = dj[j];
+      else d = (k[j] >> shift) & 0xffu;
       const uint32_t p = tstart[d] + wc[w][d] + r[j];
       sk[p] = k[j];
       sv[p] = v[j];
+      if constexpr (BKT) sdg[p] = static_cast<uint8_t>(d);
     }
   }
   __syncthreads();
@@ -719,7 +757,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
     }
 #pragma unroll
     for (int j = 0; j < kRounds; ++j) {
-      const uint32_t d = (kk[j] >> shift) & 0xffu;
+      const uint32_t d = BKT ? static_cast<uint32_t>(sdg[threadIdx.x + j * kRT]) : (kk[j] >> shift) & 0xffu;
       pb[j] = static_cast<int32_t>(base[d]) - static_cast<int32_t>(tstart[d]);
     }
 #pragma unroll
@@ -738,7 +776,7 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
   }
   for (int p = threadIdx.x; p < tn; p += kRT) {
     const uint32_t key = sk[p];
-    const uint32_t d = (key >> shift) & 0xffu;
+    const uint32_t d = BKT ? static_cast<uint32_t>(sdg[p]) : (key >> shift) & 0xffu;
     const int64_t pos = row * a.n + base[d] + (p - tstart[d]);
     if (last) {
       a.out_sorted[pos] = key2f_desc(key ^ a.key_xor);
@@ -747,6 +785,365 @@ __global__ __launch_bounds__(kRT) void onesweep_pass_kernel(RadixArgs a, const u
       keys_out[pos] = key;
       vals_out[pos] = sv[p];
     }
+  }
+}
+
+// ---------------------------------------------------------------- splitter-bucket mode (opt-in)
+// binary_auroc at 1M spent ~52 of its ~82 us in the four onesweep passes (each a ~13 us latency
+// chain: load + rank, look-back, staging, stores; profiles/k3_pass_trace_r5.txt).  Bucket mode
+// keeps ONE such pass: 255 splitters cut the row into 256 near-equal buckets (equal-frequency
+// quantiles of an 8192-key sorted sample, so the bucket sizes follow the data, not the key bits:
+// probabilities, whose top key bits are nearly constant, bucket as evenly as logits), the pass
+// scatters the keys stably into their buckets, and one workgroup per bucket sorts it in LDS
+// (packed (key, position) bitonic sort: stable) and writes the final floats and payload.
+constexpr int kBktSample = 8192;
+constexpr int kBktT = 1024;      // threads of the sample / bucket kernels
+constexpr int kBktFast = 8192;   // keys a bucket workgroup radix-sorts in LDS (2 x 64 KB of packed pairs)
+constexpr int kBktCap = 16384;   // ... or bitonic-sorts in place (the two halves as one array)
+constexpr int kBktW = kBktT / 64;
+
+// block-wide exclusive scan of one value per thread (kBktT threads); returns the block total
+__device__ __forceinline__ uint32_t bkt_block_scan(uint32_t v, uint32_t& excl, uint32_t* ws) {
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  uint32_t inc = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t u = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += u;
+  }
+  if (lane == 63) ws[w] = inc;
+  __syncthreads();
+  uint32_t off = 0, tot = 0;
+#pragma unroll
+  for (int q = 0; q < kBktW; ++q) {
+    const uint32_t x = ws[q];
+    off += q < w ? x : 0u;
+    tot += x;
+  }
+  excl = off + inc - v;
+  __syncthreads();
+  return tot;
+}
+
+// XOR of the block's min and max key over e[0, N) (the high words): the key bits that differ
+__device__ __forceinline__ uint32_t bkt_key_spread(const unsigned long long* e, int N, uint32_t* ws) {
+  uint32_t mn = ~0u, mx = 0u;
+  for (int i = threadIdx.x; i < N; i += kBktT) {
+    const uint32_t k = static_cast<uint32_t>(e[i] >> 32);
+    mn = k < mn ? k : mn;
+    mx = k > mx ? k : mx;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    ws[w] = mn;
+    ws[kBktW + w] = mx;
+  }
+  __syncthreads();
+  mn = ~0u;
+  mx = 0u;
+#pragma unroll
+  for (int q = 0; q < kBktW; ++q) {
+    mn = ws[q] < mn ? ws[q] : mn;
+    mx = ws[kBktW + q] > mx ? ws[kBktW + q] : mx;
+  }
+  __syncthreads();
+  return mn ^ mx;
+}
+
+// stable LSD radix sort of N <= kBktFast packed (key << 32 | value) words by their key bits
+// [0, nbits), 8 bits per pass, ping-pong A <-> B; returns the buffer holding the result.  Wave w
+// ranks the contiguous chunk [w C, (w + 1) C) in 64-key rounds (onesweep's match-mask ranks),
+// the digit bases combine the waves in order: stable.
+__device__ __forceinline__ unsigned long long* lds_radix_u64(unsigned long long* A, unsigned long long* B, int N, int nbits,
+                                             uint32_t (*wcnt)[kBins], uint32_t* dbase, uint32_t* ws) {
+  constexpr int kMaxR = kBktFast / kBktT;  // rounds per wave
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  const int C = ((N + kBktW - 1) / kBktW + 63) / 64 * 64;
+  const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int sh = 0; sh < nbits; sh += 8) {
+    for (int q = lane; q < kBins; q += 64) wcnt[w][q] = 0u;
+    __syncthreads();
+    unsigned long long el[kMaxR];
+    uint32_t rk[kMaxR];
+#pragma unroll
+    for (int r = 0; r < kMaxR; ++r) {
+      const int i = w * C + r * 64 + lane;
+      const bool valid = r * 64 < C && i < N;
+      el[r] = valid ? A[i] : 0ull;
+      const uint32_t d = static_cast<uint32_t>(el[r] >> (32 + sh)) & 0xffu;
+      const uint64_t active = __ballot(valid);
+      const uint64_t peers = match_digit(d, active);
+      const uint64_t pb = peers & below;
+      rk[r] = wcnt[w][d] + static_cast<uint32_t>(__popcll(pb));
+      if (valid && pb == 0ull) wcnt[w][d] += static_cast<uint32_t>(__popcll(peers));
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (threadIdx.x < kBins) {
+#pragma unroll
+      for (int q = 0; q < kBktW; ++q) {
+        const uint32_t c = wcnt[q][threadIdx.x];
+        wcnt[q][threadIdx.x] = tot;
+        tot += c;
+      }
+    }
+    uint32_t ex = 0;
+    bkt_block_scan(tot, ex, ws);
+    if (threadIdx.x < kBins) dbase[threadIdx.x] = ex;
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < kMaxR; ++r) {
+      const int i = w * C + r * 64 + lane;
+      const uint32_t d = static_cast<uint32_t>(el[r] >> (32 + sh)) & 0xffu;
+      if (r * 64 < C && i < N) B[dbase[d] + wcnt[w][d] + rk[r]] = el[r];
+    }
+    __syncthreads();
+    unsigned long long* t = A;
+    A = B;
+    B = t;
+  }
+  return A;
+}
+
+// ascending bitonic sort of e[0, P) in place (P a power of two <= kBktCap): the tier for buckets
+// between kBktFast and kBktCap keys
+__device__ void lds_bitonic(unsigned long long* e, int P) {
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P / 2; i += kBktT) {
+        const int lo = ((i & ~(j - 1)) << 1) | (i & (j - 1));  // i-th pair (lo, lo + j)
+        const int hi = lo + j;
+        const unsigned long long x = e[lo], y = e[hi];
+        const bool up = (lo & k) == 0;
+        if ((x > y) == up) {
+          e[lo] = y;
+          e[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// one block per row: sorted 8192-key sample (LDS radix) -> 255 splitters (its ranks 32, 64, ...)
+__global__ __launch_bounds__(kBktT) void bkt_split_kernel(RadixArgs a) {
+  __shared__ unsigned long long e[2][kBktSample];
+  __shared__ uint32_t wcnt[kBktW][kBins];
+  __shared__ uint32_t dbase[kBins];
+  __shared__ uint32_t ws[2 * kBktW];
+  const int64_t row = blockIdx.x;
+  const float* in = a.in + row * a.in_row_stride;
+  BKT_TRACE(6, 0);
+  for (int i = threadIdx.x; i < kBktSample; i += kBktT)
+    e[0][i] = static_cast<unsigned long long>(f2key_desc(in[static_cast<int64_t>(i) * a.n / kBktSample]) ^ a.key_xor) << 32;
+  __syncthreads();
+  BKT_TRACE(6, 1);
+  const uint32_t spread = bkt_key_spread(e[0], kBktSample, ws);
+  const int nbits = spread ? 32 - __clz(static_cast<int>(spread)) : 0;
+  const unsigned long long* s = lds_radix_u64(e[0], e[1], kBktSample, nbits, wcnt, dbase, ws);
+  BKT_TRACE(6, 2);
+  if (threadIdx.x < kBins - 1)
+    a.bkt_spl[row * kBins + threadIdx.x] = static_cast<uint32_t>(s[(threadIdx.x + 1) * (kBktSample / kBins) - 1] >> 32);
+}
+
+// the bucket histogram into digit-total slot 0 (as onesweep_hist_kernel's pass-0 digit)
+__global__ __launch_bounds__(kRT) void bkt_hist_kernel(RadixArgs a, int64_t per_block) {
+  constexpr int kC = 8;
+  __shared__ uint32_t h[kC][kBins + 1];
+  __shared__ uint32_t spl[kBins];
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.os_hdr[8] = 0u;
+  const int64_t row = blockIdx.y;
+  for (int q = threadIdx.x; q < kC * (kBins + 1); q += kRT) (&h[0][0])[q] = 0u;
+  spl[threadIdx.x] = threadIdx.x < kBins - 1 ? a.bkt_spl[row * kBins + threadIdx.x] : ~0u;
+  __syncthreads();
+  const int64_t lo = static_cast<int64_t>(blockIdx.x) * per_block;
+  const int64_t hi = lo + per_block < a.n ? lo + per_block : a.n;
+  const int c = threadIdx.x % kC;
+  const float* in = a.in + row * a.in_row_stride;
+  for (int64_t i0 = lo; i0 < hi; i0 += kRT * kHistKeys) {
+    uint32_t k[kHistKeys];
+#pragma unroll
+    for (int j = 0; j < kHistKeys; ++j) {
+      const int64_t i = i0 + j * kRT + threadIdx.x;
+      k[j] = f2key_desc(in[i < hi ? i : hi - 1]) ^ a.key_xor;
+    }
+#pragma unroll
+    for (int j = 0; j < kHistKeys; ++j)
+      if (i0 + j * kRT + threadIdx.x < hi) atomicAdd(&h[c][bkt_of(k[j], spl)], 1u);
+  }
+  __syncthreads();
+  uint32_t v = 0;
+#pragma unroll
+  for (int q = 0; q < kC; ++q) v += h[q][threadIdx.x];
+  if (v) atomicAdd(&a.os_g[((row * kGCopies + blockIdx.x % kGCopies) * 4 + 0) * kBins + threadIdx.x], v);
+}
+
+
+// one block per (bucket, row): the bucket's keys (stably scattered by the pass into keys0 /
+// vals0 at the bucket's offset) sorted in LDS as packed (key << 32 | position) pairs - equal
+// keys keep their input order - then written out as the sorted floats and their payload.  A
+// bucket over kBktCap keys (a tie group larger than ~n / 256 lands in one bucket at its upper
+// splitter) puts the keys equal to that splitter after the LDS-sorted rest, in input order; a
+// rest still over kBktCap (never for near-continuous scores) takes a slow single-workgroup LSD
+// sort through keys1 / vals1.  The blocks also clear the status / group plane the pass used.
+__global__ __launch_bounds__(kBktT) void bkt_sort_kernel(RadixArgs a) {
+  __shared__ unsigned long long e[kBktCap];  // two kBktFast halves for the radix tier
+  __shared__ uint32_t ws[2 * kBktW];
+  __shared__ uint32_t hist[kBins];
+  __shared__ uint32_t wcnt[kBktW][kBins];
+  __shared__ uint32_t dbase[kBins];
+  const int b = blockIdx.x;
+  const int64_t row = blockIdx.y;
+  BKT_TRACE(5, 0);
+  {  // the pass's status / group plane (0), grid-stride over every block
+    const int64_t nthr = static_cast<int64_t>(gridDim.x) * gridDim.y * kBktT;
+    const int64_t me = (static_cast<int64_t>(blockIdx.y) * gridDim.x + blockIdx.x) * kBktT + threadIdx.x;
+    const int64_t se = a.os_hdr[4], ge = a.os_hdr[6];
+    for (int64_t q = me; q < se; q += nthr) a.os_status[q] = 0u;
+    for (int64_t q = me; q < ge; q += nthr) a.os_gacc[q] = 0ull;
+  }
+  // this bucket's offset (exclusive scan of the bucket sizes) and size
+  __shared__ uint32_t s_off;
+  {
+    const uint32_t cv = threadIdx.x < kBins ? a.bkt_cnt[row * kBins + threadIdx.x] : 0u;
+    uint32_t ex = 0;
+    bkt_block_scan(cv, ex, ws);
+    if (threadIdx.x == static_cast<unsigned>(b)) s_off = ex;
+    __syncthreads();
+  }
+  const uint32_t off = s_off;
+  const uint32_t cnt = a.bkt_cnt[row * kBins + b];
+  BKT_TRACE(5, 1);
+  if (cnt == 0) return;
+  const int64_t base = row * a.n + off;
+  const uint32_t* kin = a.keys0 + base;
+  const uint32_t* vin = a.vals0 + base;
+  float* os = a.out_sorted + base;
+  int32_t* oo = a.out_order + base;
+  const uint32_t split = b < kBins - 1 ? a.bkt_spl[row * kBins + b] : ~0u;
+  // keys other than the upper splitter (all of them when the bucket fits)
+  const bool fits = cnt <= static_cast<uint32_t>(kBktCap);
+  uint32_t m = cnt;
+  if (!fits) {
+    uint32_t mine = 0;
+    for (uint32_t i = threadIdx.x; i < cnt; i += kBktT) mine += kin[i] != split ? 1u : 0u;
+    uint32_t ex = 0;
+    m = bkt_block_scan(mine, ex, ws);
+  }
+  if (m <= static_cast<uint32_t>(kBktCap)) {
+    const bool radix = m <= static_cast<uint32_t>(kBktFast);
+    int P = 64;
+    while (P < static_cast<int>(m)) P <<= 1;
+    const int fill = radix ? static_cast<int>(m) : P;
+    if (fits) {
+      for (int i = threadIdx.x; i < fill; i += kBktT)
+        e[i] = i < static_cast<int>(cnt) ? (static_cast<unsigned long long>(kin[i]) << 32) | static_cast<uint32_t>(i) : ~0ull;
+    } else {
+      // stable compaction of the non-splitter keys, then the splitter's tie run in input order
+      uint32_t done_ne = 0, done_eq = 0;
+      for (uint32_t i0 = 0; i0 < cnt; i0 += kBktT) {
+        const uint32_t i = i0 + threadIdx.x;
+        const bool valid = i < cnt;
+        const uint32_t key = valid ? kin[i] : split;
+        const bool ne = valid && key != split;
+        uint32_t ex_ne = 0, ex_eq = 0;
+        const uint32_t t_ne = bkt_block_scan(ne ? 1u : 0u, ex_ne, ws);
+        const uint32_t t_eq = bkt_block_scan(valid && !ne ? 1u : 0u, ex_eq, ws);
+        if (ne) e[done_ne + ex_ne] = (static_cast<unsigned long long>(key) << 32) | i;
+        if (valid && !ne) {
+          os[m + done_eq + ex_eq] = key2f_desc(split ^ a.key_xor);
+          oo[m + done_eq + ex_eq] = static_cast<int32_t>(vin[i]);
+        }
+        done_ne += t_ne;
+        done_eq += t_eq;
+      }
+      for (int i = static_cast<int>(m) + threadIdx.x; i < fill; i += kBktT) e[i] = ~0ull;
+    }
+    __syncthreads();
+    BKT_TRACE(5, 2);
+    const unsigned long long* r = e;
+    if (radix) {  // LSD over the key bits that differ inside the bucket (2-3 passes for scores)
+      const uint32_t spread = bkt_key_spread(e, static_cast<int>(m), ws);
+      const int nbits = spread ? 32 - __clz(static_cast<int>(spread)) : 0;
+      BKT_TRACE(5, 3);
+      if (threadIdx.x == 0) BKT_NBITS(nbits);
+      r = lds_radix_u64(e, e + kBktFast, static_cast<int>(m), nbits, wcnt, dbase, ws);
+    } else {
+      lds_bitonic(e, P);
+    }
+    BKT_TRACE(5, 4);
+    for (int i = threadIdx.x; i < static_cast<int>(m); i += kBktT) {
+      const unsigned long long x = r[i];
+      os[i] = key2f_desc(static_cast<uint32_t>(x >> 32) ^ a.key_xor);
+      oo[i] = static_cast<int32_t>(vin[static_cast<uint32_t>(x)]);
+    }
+    BKT_TRACE(5, 5);
+    return;
+  }
+  // slow path: stable LSD radix sort of the whole bucket by this workgroup alone, 8 bits per
+  // pass, ping-pong keys0 / vals0 <-> keys1 / vals1 at the bucket's offset (chunks of kBktT keys
+  // in order; per-wave stable ranks as the onesweep passes; running digit bases)
+  uint32_t* k2 = a.keys1 + base;
+  uint32_t* v2 = a.vals1 + base;
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  for (int pass = 0; pass < 4; ++pass) {
+    const uint32_t* ks = pass & 1 ? k2 : kin;
+    const uint32_t* vs = pass & 1 ? v2 : vin;
+    uint32_t* kd = pass & 1 ? const_cast<uint32_t*>(kin) : k2;
+    uint32_t* vd = pass & 1 ? const_cast<uint32_t*>(vin) : v2;
+    const int sh = 8 * pass;
+    if (threadIdx.x < kBins) hist[threadIdx.x] = 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < cnt; i += kBktT) atomicAdd(&hist[(ks[i] >> sh) & 0xffu], 1u);
+    __syncthreads();
+    {
+      uint32_t ex = 0;
+      const uint32_t hv = threadIdx.x < kBins ? hist[threadIdx.x] : 0u;
+      bkt_block_scan(hv, ex, ws);
+      if (threadIdx.x < kBins) dbase[threadIdx.x] = ex;
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < cnt; i0 += kBktT) {
+      const uint32_t i = i0 + threadIdx.x;
+      const bool valid = i < cnt;
+      const uint32_t key = valid ? ks[i] : 0u;
+      const uint32_t val = valid ? vs[i] : 0u;
+      for (int q = lane; q < kBins; q += 64) wcnt[w][q] = 0u;
+      __syncthreads();
+      const uint64_t active = __ballot(valid);
+      const uint32_t d = (key >> sh) & 0xffu;
+      const uint64_t peers = match_digit(d, active);
+      const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+      const uint32_t rk = static_cast<uint32_t>(__popcll(peers & below));
+      if (valid && (peers & below) == 0ull) wcnt[w][d] = static_cast<uint32_t>(__popcll(peers));
+      __syncthreads();
+      uint32_t pre = 0;
+      for (int q = 0; q < w; ++q) pre += wcnt[q][d];
+      if (valid) {
+        const uint32_t pos = dbase[d] + pre + rk;
+        kd[pos] = key;
+        vd[pos] = val;
+      }
+      __syncthreads();
+      if (threadIdx.x < kBins) {
+        uint32_t add = 0;
+        for (int q = 0; q < kBktW; ++q) add += wcnt[q][threadIdx.x];
+        dbase[threadIdx.x] += add;
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+  // 4 passes: the result is back in keys0 / vals0
+  for (uint32_t i = threadIdx.x; i < cnt; i += kBktT) {
+    os[i] = key2f_desc(kin[i] ^ a.key_xor);
+    oo[i] = static_cast<int32_t>(vin[i]);
   }
 }
 
@@ -916,7 +1313,49 @@ int radix_onesweep(const RadixArgs& a, hipStream_t stream) {
   return static_cast<int>(hipGetLastError());
 }
 
+template <int R>
+int radix_bucket(const RadixArgs& a, hipStream_t stream) {
+  hipLaunchKernelGGL(bkt_split_kernel, dim3(static_cast<unsigned>(a.rows)), dim3(kBktT), 0, stream, a);
+  const int64_t per = static_cast<int64_t>(kRT) * kHistKeys;
+  const dim3 hgrid(static_cast<unsigned>((a.n + per - 1) / per), static_cast<unsigned>(a.rows));
+  hipLaunchKernelGGL(bkt_hist_kernel, hgrid, dim3(kRT), 0, stream, a, per);
+  const dim3 grid(static_cast<unsigned>(a.rows * a.tiles));
+#define TEA_BPASS(...) \
+  hipLaunchKernelGGL((onesweep_pass_kernel<R, __VA_ARGS__>), grid, dim3(kRT), 0, stream, a, nullptr, nullptr, a.keys0, a.vals0, 0)
+  if (a.payload_kind == 0) {
+    TEA_BPASS(1, uint32_t, 0, false, true);
+  } else if (a.payload_kind == 1) {
+    switch (a.payload_dt) {
+      case DType::f32: TEA_BPASS(2, float, 1, false, true); break;
+      case DType::i64: TEA_BPASS(2, int64_t, 1, false, true); break;
+      case DType::i32: TEA_BPASS(2, int32_t, 1, false, true); break;
+      case DType::u8: case DType::b8: TEA_BPASS(2, uint8_t, 1, false, true); break;
+      default: return -2;
+    }
+  } else {
+    switch (a.payload_dt) {
+      case DType::i64: TEA_BPASS(2, int64_t, 2, false, true); break;
+      case DType::i32: TEA_BPASS(2, int32_t, 2, false, true); break;
+      default: return -2;
+    }
+  }
+#undef TEA_BPASS
+  hipLaunchKernelGGL(bkt_sort_kernel, dim3(kBins, static_cast<unsigned>(a.rows)), dim3(kBktT), 0, stream, a);
+  return static_cast<int>(hipGetLastError());
+}
+
 }  // namespace
+
+bool radix_bucket_ok(int64_t rows, int64_t n) {
+  // opt-in (TORCHEVAL_AMD_K3_BUCKET=1, read per sort): measured slower than the four onesweep
+  // passes at 1M (115 vs 85 us per binary_auroc, profiles/k3_bucket_attempt_r6.json) - its LDS
+  // stages (the 8192-key sample sort on one CU, the per-bucket LSD) cost 5-6 us per 8-bit pass
+  const char* e = std::getenv("TORCHEVAL_AMD_K3_BUCKET");
+  const bool on = e != nullptr && e[0] == '1';
+  // from 64k keys (below, the sample is most of the row) to 2M per row (~8k keys per bucket; the
+  // LDS stage holds 16k)
+  return on && radix_onesweep_ok(rows, n) && n >= (int64_t{1} << 16) && n <= (int64_t{2} << 20);
+}
 
 bool radix_onesweep_ok(int64_t rows, int64_t n) {
   // few long rows only: at 100 rows x 100k the legacy sort stays ahead (361 vs 370 us for
@@ -941,6 +1380,8 @@ int launch_radix_sort_desc(const RadixArgs& a, hipStream_t stream) {
     if (a.fold_ab != nullptr && ((a.payload_kind != 1 && a.payload_kind != 2) ||
                                  a.fold_otiles != ((a.n + (1 << kFoldShift) - 1) >> kFoldShift)))
       return -2;
+    if (a.bkt_spl != nullptr && a.bkt_cnt != nullptr && a.fold_ab == nullptr && radix_bucket_ok(a.rows, a.n))
+      return radix_sort_rounds(a.rows, a.n) == 16 ? radix_bucket<16>(a, stream) : radix_bucket<8>(a, stream);
     return radix_sort_rounds(a.rows, a.n) == 16 ? radix_onesweep<16>(a, stream) : radix_onesweep<8>(a, stream);
   }
   return radix_sort_rounds(a.rows, a.n) == 16 ? radix_passes<16>(a, stream) : radix_passes<8>(a, stream);
