@@ -55,7 +55,7 @@ int main() {
   CK(hipMalloc(&hdr, (16 + rows * 8 * 4 * 256) * 4));
   CK(hipMalloc(&status, 2 * sw * 4));
   CK(hipMalloc(&gacc, 2 * gw * 8));
-  CK(hipMalloc(&trace, 8 * 4096 * 8 * 8));
+  CK(hipMalloc(&trace, 16 * 4096 * 8 * 8));
   CK(hipMemset(groups, 0, (4 + 4 * region) * 4));
   CK(hipMemset(hdr, 0, (16 + rows * 8 * 4 * 256) * 4));
   CK(hipMemset(status, 0, 2 * sw * 4));
@@ -88,7 +88,7 @@ int main() {
   a.bkt_spl = ws + 4 * n + rows * 256 * a.tiles;
   a.bkt_cnt = a.bkt_spl + rows * 256;
   for (int it = 0; it < 6; ++it) {
-    if (it == 5) CK(hipMemset(trace, 0, 8 * 4096 * 8 * 8));
+    if (it == 5) CK(hipMemset(trace, 0, 16 * 4096 * 8 * 8));
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -107,7 +107,7 @@ int main() {
   bool desc = true;
   for (int64_t i = 1; i < n; ++i) desc = desc && !(hs[i] > hs[i - 1]);
   std::printf("descending %s, look-back timeout flag %u\n", desc ? "yes" : "NO", timeout_flag);
-  std::vector<unsigned long long> tr(8 * 4096 * 8);
+  std::vector<unsigned long long> tr(16 * 4096 * 8);
   CK(hipMemcpy(tr.data(), trace, tr.size() * 8, hipMemcpyDeviceToHost));
   const unsigned long long* sp = &tr[(6 * 4096) * 8];
   std::printf("sample kernel: load %.2f us, spread + LDS radix %.2f us\n", (sp[1] - sp[0]) * 0.01, (sp[2] - sp[1]) * 0.01);
@@ -130,5 +130,16 @@ int main() {
   }
   std::sort(nbits.begin(), nbits.end());
   std::printf("key bits sorted per bucket: median %d max %d\n", nbits[128], nbits.back());
+  std::vector<double> q[3];
+  for (int b = 0; b < 4096; ++b) {  // first LSD pass of the blocks (bucket blocks < 256, the sample block 0 too)
+    const unsigned long long* t = &tr[(8 * 4096 + b) * 8];
+    for (int i = 0; i < 3; ++i)
+      if (t[i] && t[i + 1]) q[i].push_back((t[i + 1] - t[i]) * 0.01);
+  }
+  const char* qn[] = {"zero->ranked", "ranked->bases", "bases->scattered"};
+  for (int i = 0; i < 3; ++i) {
+    std::sort(q[i].begin(), q[i].end());
+    if (!q[i].empty()) std::printf("  first LSD pass %-18s median %.2f max %.2f us\n", qn[i], q[i][q[i].size() / 2], q[i].back());
+  }
   return desc && timeout_flag == 0 ? 0 : 1;
 }

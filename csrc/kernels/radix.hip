@@ -867,6 +867,7 @@ __device__ __forceinline__ unsigned long long* lds_radix_u64(unsigned long long*
   const int C = ((N + kBktW - 1) / kBktW + 63) / 64 * 64;
   const uint64_t below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   for (int sh = 0; sh < nbits; sh += 8) {
+    if (sh == 0) BKT_TRACE(8, 0);
     for (int q = lane; q < kBins; q += 64) wcnt[w][q] = 0u;
     __syncthreads();
     unsigned long long el[kMaxR];
@@ -884,6 +885,7 @@ __device__ __forceinline__ unsigned long long* lds_radix_u64(unsigned long long*
       if (valid && pb == 0ull) wcnt[w][d] += static_cast<uint32_t>(__popcll(peers));
     }
     __syncthreads();
+    if (sh == 0) BKT_TRACE(8, 1);
     uint32_t tot = 0;
     if (threadIdx.x < kBins) {
 #pragma unroll
@@ -897,6 +899,7 @@ __device__ __forceinline__ unsigned long long* lds_radix_u64(unsigned long long*
     bkt_block_scan(tot, ex, ws);
     if (threadIdx.x < kBins) dbase[threadIdx.x] = ex;
     __syncthreads();
+    if (sh == 0) BKT_TRACE(8, 2);
 #pragma unroll
     for (int r = 0; r < kMaxR; ++r) {
       const int i = w * C + r * 64 + lane;
@@ -904,6 +907,7 @@ __device__ __forceinline__ unsigned long long* lds_radix_u64(unsigned long long*
       if (r * 64 < C && i < N) B[dbase[d] + wcnt[w][d] + rk[r]] = el[r];
     }
     __syncthreads();
+    if (sh == 0) BKT_TRACE(8, 3);
     unsigned long long* t = A;
     A = B;
     B = t;
