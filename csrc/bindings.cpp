@@ -1325,6 +1325,31 @@ void cov_finalize(const Tensor& cov_sum, const Tensor& colsum, double n, const T
                "cov_finalize");
 }
 
+// FID's closing combination: |sum1 / n1 - sum2 / n2|^2 + tr S1 + tr S2 - 2 sum sqrt(max(lam, 0))
+// -> out (float32 scalar), one launch
+void fid_finish(const Tensor& sum1, double n1, const Tensor& sum2, double n2, const Tensor& s1, const Tensor& s2,
+                const Tensor& lam, const Tensor& out) {
+  check_gpu(sum1, "sum1");
+  const int64_t d = sum1.numel();
+  TORCH_CHECK(sum1.scalar_type() == at::kFloat && sum1.is_contiguous() && sum2.scalar_type() == at::kFloat &&
+                  sum2.is_contiguous() && sum2.numel() == d,
+              "fid_finish: sums must be contiguous float32 [d]");
+  for (const Tensor* s : {&s1, &s2})
+    TORCH_CHECK(s->scalar_type() == at::kDouble && s->dim() == 2 && s->size(0) == d && s->size(1) == d &&
+                    s->stride(1) == 1 && s->device() == sum1.device(),
+                "fid_finish: covariances must be row-contiguous float64 [d, d]");
+  TORCH_CHECK(lam.scalar_type() == at::kDouble && lam.is_contiguous() && lam.device() == sum1.device(),
+              "fid_finish: eigenvalues must be contiguous float64");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.numel() == 1 && out.device() == sum1.device(),
+              "fid_finish: out must be a float32 scalar");
+  TORCH_CHECK(n1 > 0 && n2 > 0, "fid_finish: needs samples on both sides");
+  c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(sum1.device());
+  check_launch(tea::launch_fid_finish(sum1.data_ptr<float>(), n1, sum2.data_ptr<float>(), n2, d, s1.data_ptr<double>(),
+                                      s1.stride(0), s2.data_ptr<double>(), s2.stride(0), lam.data_ptr<double>(),
+                                      lam.numel(), out.data_ptr<float>(), stream_for(sum1)),
+               "fid_finish");
+}
+
 void sym_fill_upper(const Tensor& m) {
   check_gpu(m, "matrix");
   TORCH_CHECK(m.dim() == 2 && m.size(0) == m.size(1) && m.scalar_type() == at::kDouble && m.stride(1) == 1 &&
@@ -1826,6 +1851,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("pivchol", &pivchol, "K9p pivoted FP64 Cholesky (rank-revealing, W rows in feature order)",
         py::arg("a"), py::arg("slots"), py::arg("w"), py::arg("piv"), py::arg("info"), py::arg("ctl"));
   m.def("pivchol_padded", &tea::pivchol_padded, "K9p factor row stride");
+  m.def("fid_finish", &fid_finish, "FID's closing combination in one launch");
   m.def("pivchol_slot_words", &tea::pivchol_slot_words, "K9p hand-off slot words");
   m.def("pivchol_traced", &pivchol_traced, "K9p with per-panel phase stamps (profiling hook)");
   m.def("cholesky_factor_traced", &cholesky_factor_traced, "K9d with per-column phase stamps (profiling hook)");
@@ -1984,6 +2010,7 @@ TORCH_LIBRARY(torcheval_amd, m) {
   m.def("pivchol(Tensor a, Tensor(a!) slots, Tensor(b!) w, Tensor(c!) piv, Tensor(d!) info, Tensor(e!) ctl) -> int");
   m.def("cov_finalize(Tensor cov_sum, Tensor colsum, float n, Tensor(a!) out) -> ()");
   m.def("sym_fill_upper(Tensor(a!) m) -> ()");
+  m.def("fid_finish(Tensor sum1, float n1, Tensor sum2, float n2, Tensor s1, Tensor s2, Tensor lam, Tensor(a!) out) -> ()");
   m.def("trapz_sorted(Tensor x, Tensor y_bits, Tensor(a!) out) -> ()");
   m.def("seg_reduce_rows(Tensor rows, Tensor(a!) out, int ws, int[] offs, int[] counts, int[] dtypes, "
         "int[] ops) -> ()");
@@ -2021,6 +2048,7 @@ TORCH_LIBRARY_IMPL(torcheval_amd, CUDA, m) {
   m.impl("cov_finalize", &cov_finalize);
   m.impl("pivchol", &pivchol);
   m.impl("sym_fill_upper", &sym_fill_upper);
+  m.impl("fid_finish", &fid_finish);
   m.impl("trapz_sorted", &trapz_sorted);
   m.impl("seg_reduce_rows", &op_seg_reduce_rows);
   m.impl("row_sums", &op_row_sums);
@@ -2066,6 +2094,8 @@ TORCH_LIBRARY_IMPL(torcheval_amd, Meta, m) {
     return int64_t{0};
   });
   m.impl("sym_fill_upper", [](const Tensor&) {});
+  m.impl("fid_finish", [](const Tensor&, double, const Tensor&, double, const Tensor&, const Tensor&, const Tensor&,
+                          const Tensor&) {});
   m.impl("trapz_sorted", [](const Tensor&, const Tensor&, const Tensor&) {});
   m.impl("seg_reduce_rows", [](const Tensor&, const Tensor&, int64_t, at::IntArrayRef, at::IntArrayRef,
                                at::IntArrayRef, at::IntArrayRef) {});

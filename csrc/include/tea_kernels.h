@@ -566,6 +566,9 @@ int launch_trapz_sorted(const float* x, const float* y, int64_t rows, int64_t n,
                         hipStream_t stream);
 int launch_cov_finalize(const float* C, const float* colsum, double n, int64_t d, double* S, hipStream_t stream);
 int launch_sym_fill_upper(double* M, int64_t ld, int64_t n, hipStream_t stream);
+int launch_fid_finish(const float* sum1, double n1, const float* sum2, double n2, int64_t d, const double* s1,
+                      int64_t ld1, const double* s2, int64_t ld2, const double* lam, int64_t r, float* out,
+                      hipStream_t stream);
 int launch_cholesky(const double* A, int64_t lda, int64_t n, double* L, double* Linv, int* ctl, int* status,
                     hipStream_t stream, unsigned long long* trace = nullptr);
 int launch_potrf_block(double* A, int64_t lda, int k0, int b, double* Linv, int* info, hipStream_t stream);

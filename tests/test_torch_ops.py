@@ -36,7 +36,7 @@ def test_schemas_declare_mutation():
 HOT_OPS = ("micro_accuracy", "cls_counts", "binary_counts", "rank_scores", "multilabel_counts", "binned_counts",
            "binned_finalize", "auc_scan", "sort_desc", "rafp", "curve_count", "curve_emit", "merge_sorted_runs",
            "retrieval_topk_update", "row_sums", "column_moments", "ne_sums", "perplexity_sums", "fid_cov_update",
-           "sym_eigvals", "potrf_block", "cholesky_factor", "pivchol", "cov_finalize", "sym_fill_upper", "trapz_sorted", "transpose_f32", "seg_reduce_rows")
+           "sym_eigvals", "potrf_block", "cholesky_factor", "pivchol", "cov_finalize", "sym_fill_upper", "fid_finish", "trapz_sorted", "transpose_f32", "seg_reduce_rows")
 
 
 @pytest.mark.parametrize("name", HOT_OPS)

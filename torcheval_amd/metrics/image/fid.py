@@ -60,20 +60,29 @@ def _cov_update(act: Tensor, cov_sum: Tensor, col_sum: Tensor) -> None:
 
 
 def _tr_sqrt_product(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optional[int] = None) -> Tensor:
-    """tr sqrt(S1 S2) for symmetric PSD S1, S2 (FP64, both exactly symmetric).
+    """tr sqrt(S1 S2) for symmetric PSD S1, S2 (FP64, both exactly symmetric): the sum of the
+    square roots of ``_spectrum(s1, s2, n1, n2)``."""
+    lam = _spectrum(s1, s2, n1, n2)
+    return lam.clamp(min=0).sqrt().sum()
+
+
+def _spectrum(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optional[int] = None) -> Tensor:
+    """Eigenvalues (FP64) whose square roots sum to tr sqrt(S1 S2).
 
     The eigenvalues of S1 S2 equal those of the symmetric L^T S2 L when S1 = L L^T, so the
     fast path is one Cholesky (K9d), the triangle-aware sandwich and ONE eigenvalues-only
-    ``eigvalsh`` (K9b; no eigenvectors, no back-transformation).  A singular S1 (fewer samples
-    than features) has no Cholesky factor; the same holds with the roles swapped when S2 has
-    one.  When both are singular, S1 = W^T W with W [r, D] of rank r, and the eigvalsh runs on
-    the r x r matrix W S2 W^T: the same non-zero spectrum as S1 S2.  On ROCm W comes from K9p
-    (csrc/kernels/pivchol.hip), a pivoted (rank-revealing) Cholesky stopping at the LAPACK
-    dpstrf tolerance D eps max diag; elsewhere (and as K9p's fallback) from ``eigh`` over the
-    eigenvalues above the ``matrix_rank`` tolerance of the FP64 matrix.  Both tolerances are
-    the FP64 ones: covariances assembled from FP32 state sums carry rounding "noise" spectrum
-    well above them, and the reference's ``eigvals(S1 S2)`` includes its square roots too, so it
-    is kept (r is then the FP64 numerical rank, usually above the sample rank).
+    ``eigvalsh`` (K9b; no eigenvectors, no back-transformation); on ROCm the three launch
+    back to back and ONE host read checks both kernels' status words (``_spectrum_fast``).  A
+    singular S1 (fewer samples than features) has no Cholesky factor; the same holds with the
+    roles swapped when S2 has one.  When both are singular, S1 = W^T W with W [r, D] of rank r,
+    and the eigvalsh runs on the r x r matrix W S2 W^T: the same non-zero spectrum as S1 S2.  On
+    ROCm W comes from K9p (csrc/kernels/pivchol.hip), a pivoted (rank-revealing) Cholesky
+    stopping at the LAPACK dpstrf tolerance D eps max diag; elsewhere (and as K9p's fallback)
+    from ``eigh`` over the eigenvalues above the ``matrix_rank`` tolerance of the FP64 matrix.
+    Both tolerances are the FP64 ones: covariances assembled from FP32 state sums carry
+    rounding "noise" spectrum well above them, and the reference's ``eigvals(S1 S2)`` includes
+    its square roots too, so it is kept (r is then the FP64 numerical rank, usually above the
+    sample rank).
 
     ``n1`` / ``n2`` (optional sample counts) mark a side with n <= D as singular up front, so
     its Cholesky is not attempted; the pivoted factor then takes the side with fewer samples."""
@@ -81,23 +90,60 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optio
     sing1 = n1 is not None and n1 <= d
     sing2 = n2 is not None and n2 <= d
     if not sing1:
-        L, info = _chol(s1)
-        if info == 0:
-            return _sqrt_eig_sum(_lt_s_l(L, s2))
+        lam, info = _spectrum_fast(s1, s2)
+        if lam is not None:
+            return lam
+        if info is None:  # not applicable / a grid aborted: the checked sequence
+            L, info = _chol(s1)
+            if info == 0:
+                return sym_eigvalsh(_lt_s_l(L, s2))
     if not sing2:
         # S1 singular, S2 not: S1 S2 and S2 S1 share their spectrum, so factor S2 instead
         # (one more Cholesky rather than a rank-revealing factorisation)
         L2, info2 = _chol(s2)
         if info2 == 0:
-            return _sqrt_eig_sum(_lt_s_l(L2, s1))
+            return sym_eigvalsh(_lt_s_l(L2, s1))
     a, b = (s2, s1) if (n1 is not None and n2 is not None and n2 < n1) else (s1, s2)
     w = _pivoted_factor(a)
     if w is None:
         w = _eigh_factor(a)
     if w.shape[0] == 0:
-        return torch.zeros((), dtype=s1.dtype, device=s1.device)
+        return torch.zeros(0, dtype=s1.dtype, device=s1.device)
     m = w @ (b @ w.T)
-    return _sqrt_eig_sum((m + m.T) / 2)
+    return sym_eigvalsh((m + m.T) / 2)
+
+
+def _spectrum_fast(s1: Tensor, s2: Tensor) -> "tuple[Optional[Tensor], Optional[int]]":
+    """K9d Cholesky -> triangle-aware sandwich -> K9b eigenvalues launched back to back with ONE
+    host read of both kernels' status words (a host read after the Cholesky cost ~70 us of idle
+    GPU, profiles/README.md round 6): (eigenvalues, 0), or (None, info != 0) when S1 is not
+    positive definite, or (None, None) when the path does not apply or a grid aborted (the
+    caller then takes the checked sequence)."""
+    n = s1.shape[0]
+    if not (use_native(s1) and s1.dtype == torch.float64 and s1.dim() == 2 and 3 <= n <= 2560):
+        return None, None
+    from torcheval_amd.ops import native
+    from torcheval_amd.ops.hostread import read_ints
+
+    nat = native()
+    nt = nat.cholesky_tiles(n)
+    N = 64 * nt
+    a = s1 if s1.stride(1) == 1 else s1.contiguous()
+    L = torch.empty(N, N, dtype=torch.float64, device=s1.device)
+    linv = torch.empty(nt * 4096, dtype=torch.float64, device=s1.device)
+    ctl = torch.empty(1, dtype=torch.int32, device=s1.device)
+    status = torch.zeros(3, dtype=torch.int32, device=s1.device)  # K9d info, abort; K9b status
+    nat.cholesky_factor(a, L, linv, ctl, status[:2])
+    m = _lt_s_l(L[:n, :n], s2).contiguous()
+    lam = torch.empty(n, dtype=torch.float64, device=s1.device)
+    if nat.sym_eigvals(m, lam, status[2:]) != 0:
+        return None, None
+    info, abort, eig = read_ints(status)
+    if abort != 0:
+        return None, None
+    if info != 0:
+        return None, info
+    return (lam, 0) if eig == 0 else (None, None)
 
 
 def _sqrt_eig_sum(m: Tensor) -> Tensor:
@@ -414,7 +460,10 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> Tensor:
-        nr, nf = int(self.num_real_images), int(self.num_fake_images)
+        counts = torch.stack([self.num_real_images.reshape(()).long(), self.num_fake_images.reshape(()).long()])
+        from torcheval_amd.ops.hostread import read_ints
+
+        nr, nf = read_ints(counts)  # one host read for both counts
         if nr == 0 or nf == 0:
             warnings.warn(
                 "Computing FID requires at least 1 real image and 1 fake image,"
@@ -423,10 +472,20 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
                 RuntimeWarning,
             )
             return torch.tensor(0.0)
-        real_mean = self.real_sum.double() / nr
-        fake_mean = self.fake_sum.double() / nf
         real_cov = _covariance(self.real_cov_sum, self.real_sum, nr)
         fake_cov = _covariance(self.fake_cov_sum, self.fake_sum, nf)
+        if (use_native(real_cov) and self.real_sum.dtype == torch.float32 and self.fake_sum.dtype == torch.float32
+                and real_cov.dtype == torch.float64 and fake_cov.dtype == torch.float64):
+            # the spectrum, then ONE launch for |mu1 - mu2|^2 + tr S1 + tr S2 - 2 sum sqrt(lam)
+            from torcheval_amd.ops import native
+
+            lam = _spectrum(real_cov, fake_cov, nr, nf)
+            out = torch.empty((), dtype=torch.float32, device=real_cov.device)
+            native().fid_finish(self.real_sum.contiguous(), float(nr), self.fake_sum.contiguous(), float(nf),
+                                real_cov, fake_cov, lam.contiguous(), out)
+            return out
+        real_mean = self.real_sum.double() / nr
+        fake_mean = self.fake_sum.double() / nf
         return _frechet_symmetric(real_mean, real_cov, fake_mean, fake_cov, nr, nf).to(torch.float32)
 
     real_sum = _staged_state("real_sum", 0)
