@@ -31,8 +31,8 @@ for _ in range(3):
     wall = (time.perf_counter() - t0) * 1e3
 t = tr.cpu().tolist()
 us = lambda a, b: round((b - a) / 100.0, 2)  # noqa: E731
-steps = {f"P{P}k{k}": {"pivot_known_to_stored": us(t[2 * (8 * P + k)], t[2 * (8 * P + k) + 1]),
-                       "stored_to_next_pivot": us(t[2 * (8 * P + k) + 1], t[2 * (8 * P + k + 1)]) if k < 7 else None}
+steps = {f"P{P}k{k}": {"round_start_to_stored": us(t[2 * (8 * P + k)], t[2 * (8 * P + k) + 1]),
+                       "stored_to_next_round": us(t[2 * (8 * P + k) + 1], t[2 * (8 * P + k + 1)]) if k < 7 else None}
          for P in range(3) for k in range(8)}
 upd = {f"P{P}": us(t[64 + 2 * P], t[64 + 2 * P + 1]) for P in range(3)}
 print(json.dumps({"info": info.cpu().tolist(), "wall_ms": round(wall, 3), "update_us": upd, "steps_us": steps}))

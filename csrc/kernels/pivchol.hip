@@ -42,7 +42,6 @@ constexpr int kPT = 256;  // threads per workgroup
 constexpr int kNB = 16;   // panel width
 constexpr int kRMax = 8;  // rows per workgroup
 constexpr int kNMax = 2048;
-constexpr int kSlotW = 2 + kNB;  // candidate slot: Schur diagonal, feature, its panel values
 constexpr unsigned kSpin = 1u << 20;
 constexpr unsigned long long kSent = ~0ull;
 
@@ -135,8 +134,31 @@ __device__ __forceinline__ void wave_argmax(double& v, int& i) {
   swap_cand<true>(v, i);
 }
 
-__device__ __forceinline__ unsigned long long* slot(const PcArgs& a, int j, int g) {
-  return a.slots + gridDim.x + (static_cast<int64_t>(j) * gridDim.x + g) * kSlotW;
+constexpr int kBP = 4;         // pivots chosen per round (block)
+constexpr int kAW = kBP;       // A-slot words per workgroup and round: 4 packed (Schur diagonal, feature)
+constexpr int kBW = kBP + kNB + 1;  // B-slot words per chosen pivot: its block row, panel values, exact diagonal
+// a round's later pivot is taken while its Schur diagonal (after the earlier ones of the round) is
+// at least kEta x the round's first: within that factor of the greedy choice (relaxed pivoting)
+constexpr double kEta = 0.25;
+
+__device__ __forceinline__ unsigned long long* slot_a(const PcArgs& a, int s, int g) {
+  return a.slots + gridDim.x + (static_cast<int64_t>(s) * gridDim.x + g) * kAW;
+}
+__device__ __forceinline__ unsigned long long* slot_b(const PcArgs& a, int s, int w) {
+  return a.slots + gridDim.x + static_cast<int64_t>(a.n) * gridDim.x * kAW + (static_cast<int64_t>(s) * kBP + w) * kBW;
+}
+
+// a candidate as ONE word: the Schur diagonal's bits with its low 11 mantissa bits replaced by
+// 2047 - feature (n <= 2048), so the words order by value and then by lower feature - for ranking
+// only (the exact diagonal of a chosen pivot comes with its block row); "none" = -inf, field 0
+__device__ __forceinline__ unsigned long long pack_cand(double v, int i) {
+  if (i == INT_MAX) return bits_of(-HUGE_VAL) & ~0x7ffull;
+  // (a zero diagonal packs as a negative subnormal, so it never passes the tolerance test)
+  return (bits_of(v > 0.0 ? v : (v == 0.0 ? -0.0 : v)) & ~0x7ffull) | static_cast<unsigned long long>(2047 - i);
+}
+__device__ __forceinline__ void unpack_cand(unsigned long long b, double& v, int& i) {
+  v = dbl(b);
+  i = (b & ~0x7ffull) == (bits_of(-HUGE_VAL) & ~0x7ffull) ? INT_MAX : 2047 - static_cast<int>(b & 0x7ffull);
 }
 
 #define PC_STAMP(idx)                                                                         \
@@ -144,65 +166,113 @@ __device__ __forceinline__ unsigned long long* slot(const PcArgs& a, int j, int 
     if (a.trace != nullptr && blockIdx.x == 0 && lane == 0) a.trace[(idx)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 
-// wave 0: publish this workgroup's candidate for step j (k = its column within the panel: the
-// candidate's first k panel values ride along)
-__device__ __forceinline__ void publish(const PcArgs& a, int j, int k, double d, bool live, int fi, const double (&Lr)[kNB]) {
+// wave 0: publish this workgroup's 4 best (Schur diagonal, feature) candidates of round s.  With
+// `drain`, the wave's write-through W stores drain first: a workgroup that has seen these
+// candidates may read the finished panel's W rows with plain loads after one acquire.
+__device__ __forceinline__ void publish_top(const PcArgs& a, int s, double d, bool live, int fi, bool drain) {
   const int lane = threadIdx.x & 63;
-  double v = live ? d : -HUGE_VAL;
-  int i = live ? fi : INT_MAX;
-  if (v != v) {  // a NaN diagonal never wins (the NaN is reported through info)
-    v = -HUGE_VAL;
-    i = INT_MAX;
-  }
-  wave_argmax(v, i);
-  unsigned long long* s = slot(a, j, blockIdx.x);
-  if (i != INT_MAX && fi == i) {
+  bool taken = false;
+  double cv[kBP];
+  int ci[kBP];
 #pragma unroll
-    for (int q = 0; q < kNB; ++q)
-      if (q < k) put(s + 2 + q, bits_of(Lr[q]));
+  for (int t = 0; t < kBP; ++t) {
+    double v = (live && !taken && d == d) ? d : -HUGE_VAL;  // (a NaN diagonal never wins: info reports it)
+    int i = (live && !taken && d == d) ? fi : INT_MAX;
+    wave_argmax(v, i);
+    cv[t] = v;
+    ci[t] = i;
+    taken = taken || (i != INT_MAX && i == fi);
   }
-  // at a panel's first step, the wave's write-through W stores of the panel drain before its
-  // candidate is visible: a workgroup that has seen these candidates may read the panel's W rows
-  // with plain loads after one acquire (the panel update).  (A drain on every step cost ~1 us.)
-  if (k == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if (lane == 0) {
-    put(s, bits_of(v));
-    put(s + 1, static_cast<unsigned long long>(static_cast<unsigned>(i)));
+  if (drain) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane < kBP) {
+    double v = cv[0];
+    int i = ci[0];
+#pragma unroll
+    for (int t = 1; t < kBP; ++t) {
+      v = lane == t ? cv[t] : v;
+      i = lane == t ? ci[t] : i;
+    }
+    put(slot_a(a, s, blockIdx.x) + lane, pack_cand(v, i));
   }
 }
 
-// wave 0: the G candidates of step j (4 slots per lane, loads issued together) -> the pivot
-__device__ __forceinline__ bool poll_candidates(const PcArgs& a, int j, double& dp, int& p, unsigned* abort_w) {
+// wave 0: every workgroup's 4 candidates of round s (16 per lane, loads issued together) -> the
+// round's 4 best, in order, in every lane
+__device__ __forceinline__ bool poll_top(const PcArgs& a, int s, double (&cv)[kBP], int (&cp)[kBP], unsigned* abort_w) {
   const int lane = threadIdx.x & 63, G = gridDim.x;
-  unsigned long long vb[4], ib[4];
+  unsigned long long cb[4][kBP];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int gg = lane + 64 * u;
-    vb[u] = gg < G ? get(slot(a, j, gg)) : bits_of(-HUGE_VAL);
-    ib[u] = gg < G ? get(slot(a, j, gg) + 1) : static_cast<unsigned long long>(INT_MAX);
+#pragma unroll
+    for (int t = 0; t < kBP; ++t) cb[u][t] = gg < G ? get(slot_a(a, s, gg) + t) : pack_cand(0.0, INT_MAX);
   }
+  // re-read every still-sentinel word together, one round trip per pass (a word-at-a-time wait
+  // paid a round trip per late word)
   bool ok = true;
-  dp = -HUGE_VAL;
-  p = INT_MAX;
+  for (unsigned it = 0;; ++it) {
+    bool pend = false;
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const int gg = lane + 64 * u;
-    if (gg < G) {
-      ok = ok && wait_word(slot(a, j, gg), vb[u], abort_w);
-      ok = ok && wait_word(slot(a, j, gg) + 1, ib[u], abort_w);
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < kBP; ++t) pend = pend || cb[u][t] == kSent;
+    if (!__any(pend)) break;
+    if ((it & 31) == 31 &&
+        __hip_atomic_load((pg_u32*)abort_w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      ok = false;
+      break;
     }
-    if (better(dbl(vb[u]), static_cast<int>(ib[u]), dp, p)) {
-      dp = dbl(vb[u]);
-      p = static_cast<int>(ib[u]);
+    if (it > kSpin) {
+      __hip_atomic_store((pg_u32*)abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ok = false;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int gg = lane + 64 * u;
+#pragma unroll
+      for (int t = 0; t < kBP; ++t)
+        if (gg < G && cb[u][t] == kSent) cb[u][t] = get(slot_a(a, s, gg) + t);
     }
   }
-  wave_argmax(dp, p);
+  unsigned taken = 0;
+#pragma unroll
+  for (int t = 0; t < kBP; ++t) {
+    double v = -HUGE_VAL;
+    int i = INT_MAX;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < kBP; ++q) {
+        double x;
+        int xi;
+        unpack_cand(cb[u][q], x, xi);
+        if (!((taken >> (u * kBP + q)) & 1u) && better(x, xi, v, i)) {
+          v = x;
+          i = xi;
+        }
+      }
+    wave_argmax(v, i);
+    cv[t] = v;
+    cp[t] = i;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < kBP; ++q) {
+        double x;
+        int xi;
+        unpack_cand(cb[u][q], x, xi);
+        if (i != INT_MAX && xi == i) taken |= 1u << (u * kBP + q);
+      }
+  }
   return !__any(!ok);
 }
 
 __global__ __launch_bounds__(kPT) void pivchol_kernel(PcArgs a) {
   __shared__ double rows[kRMax * kNMax];
   __shared__ double sL[kRMax][kNB];
+  __shared__ double sBv[kBP * kBW];  // wave 0: the round's block rows and panel values (B slots)
   __shared__ int s_state;  // 0 go on, 1 done, 2 aborted
   const int tid = threadIdx.x, lane = tid & 63;
   const int n = a.n, N = a.N, R = a.R, G = gridDim.x, g = blockIdx.x;
@@ -230,8 +300,9 @@ __global__ __launch_bounds__(kPT) void pivchol_kernel(PcArgs a) {
   for (int q = 0; q < kNB; ++q) Lr[q] = 0.0;
   double tol = 0.0;
   int rank = 0;
-  double dp = -HUGE_VAL;  // wave 0: the current step's pivot (value, feature)
-  int p = INT_MAX;
+  int j = 0, s = 0;  // next factor column, round
+  double cv[kBP];    // wave 0: the current round's candidates (Schur diagonal, feature), best first
+  int cp[kBP];
   if (tid < 64) {
     if (lane < R && fi < n) {
       d = rows[lane * N + fi];
@@ -253,8 +324,8 @@ __global__ __launch_bounds__(kPT) void pivchol_kernel(PcArgs a) {
     wave_argmax(mx, dummy);
     tol = static_cast<double>(n) * DBL_EPSILON * mx;
     if (__any(!ok) && lane == 0) s_state = 2;
-    publish(a, 0, 0, d, live, fi, Lr);
-    if (!poll_candidates(a, 0, dp, p, abort_w) && lane == 0) s_state = 2;
+    publish_top(a, 0, d, live, fi, false);
+    if (!poll_top(a, 0, cv, cp, abort_w) && lane == 0) s_state = 2;
   }
   __syncthreads();
 
@@ -262,55 +333,150 @@ __global__ __launch_bounds__(kPT) void pivchol_kernel(PcArgs a) {
     const int j0 = P * kNB;
     if (tid < 64) {
       int state = 0;
-      for (int k = 0; k < kNB; ++k) {  // (k uniform: Lr[k] is register-indexed)
-        const int j = j0 + k;
+      int k = 0;  // columns of this panel done (uniform: Lr[k] is register-indexed)
+      while (k < kNB) {
         if (j >= n) {
           state = 1;
           break;
         }
-        if (k < 8 && P < 4) PC_STAMP(2 * (P * 8 + k));
-        if (!(dp > tol)) {  // every remaining Schur diagonal <= tol (or none left): rank j
-          rank = j;
+        if (!(cv[0] > tol)) {  // every remaining Schur diagonal <= tol (or none left): rank j
           state = 1;
           break;
         }
-        // the winner's panel values (published with its candidate)
-        double x = 0.0;
-        if (k > 0) {
+        if (s < 8 && P < 4) PC_STAMP(2 * (P * 8 + (s & 7)));
+        // candidates this round may take: leading ones above tol, within the panel and n
+        int mmax = 1;
+        while (mmax < kBP && mmax < kNB - k && j + mmax < n && cv[mmax] > tol && cp[mmax] != INT_MAX) ++mmax;
+        // B: each chosen candidate's owner publishes its row of the block (A'(p_a, p_b)) and its
+        // panel values; a single candidate at a panel's first column needs neither
+        {  // (always: the chosen pivots' exact diagonals come with their block rows)
+#pragma unroll
+          for (int t = 0; t < kBP; ++t) {
+            if (t < mmax && lane < R && fi == cp[t]) {  // this lane holds candidate t's row
+              unsigned long long* sb = slot_b(a, s, t);
+              put(sb + kBP + kNB, bits_of(d));
+#pragma unroll
+              for (int b = 0; b < kBP; ++b)
+                if (b < mmax) put(sb + b, bits_of(rows[lane * N + cp[b]]));
+#pragma unroll
+              for (int q = 0; q < kNB; ++q)
+                if (q < k) put(sb + kBP + q, bits_of(Lr[q]));
+            }
+          }
+          // poll: word w = t * kBW + e over the needed ones, two per lane, into sBv
           bool ok = true;
-          const unsigned long long* ws = slot(a, j, p / R) + 2;
-          unsigned long long b = kSent;
-          if (lane < k) {
-            b = get(ws + lane);
-            ok = wait_word(ws + lane, b, abort_w);
-            x = dbl(b);
+          unsigned long long bw[2];
+          bool need[2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int wd = lane + 64 * h;
+            const int t = wd / kBW, e = wd - t * kBW;
+            need[h] = t < mmax && ((e < kBP && e < mmax) || (e >= kBP && e - kBP < k) || e == kBP + kNB);
+            bw[h] = need[h] ? get(slot_b(a, s, t) + e) : 0ull;
+          }
+          for (unsigned it = 0;; ++it) {  // one round trip per pass over the late words
+            const bool pend = (need[0] && bw[0] == kSent) || (need[1] && bw[1] == kSent);
+            if (!__any(pend)) break;
+            if (it > kSpin || ((it & 31) == 31 && __hip_atomic_load((pg_u32*)abort_w, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT) != 0u)) {
+              if (it > kSpin) __hip_atomic_store((pg_u32*)abort_w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              ok = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int wd = lane + 64 * h;
+              const int t = wd / kBW, e = wd - t * kBW;
+              if (need[h] && bw[h] == kSent) bw[h] = get(slot_b(a, s, t) + e);
+            }
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int wd = lane + 64 * h;
+            if (wd < kBP * kBW) sBv[wd] = need[h] ? dbl(bw[h]) : 0.0;
           }
           if (__any(!ok)) {
             state = 2;
             break;
           }
         }
-        double t = (lane < R) ? rows[lane * N + p] : 0.0;
-        for (int q = 0; q < k; ++q) t = fma(-Lr[q], __shfl(x, q), t);
-        const double sq = sqrt(dp);
-        double l = 0.0;
-        if (live) {
-          if (fi == p) {
-            l = sq;
-            live = false;
-          } else {
-            l = t / sq;
-            d = fma(-l, l, d);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // (one wave: its LDS stores land before its reads)
+        // the block's factor with relaxed acceptance (uniform: every lane the same values)
+        double lb[kBP][kBP];
+#pragma unroll
+        for (int t = 0; t < kBP; ++t)
+#pragma unroll
+          for (int b = 0; b < kBP; ++b) lb[t][b] = 0.0;
+        double cx[kBP];  // the chosen pivots' exact Schur diagonals
+#pragma unroll
+        for (int t = 0; t < kBP; ++t) cx[t] = sBv[t * kBW + kBP + kNB];
+        if (!(cx[0] > tol)) {  // (the exact diagonal: the ranking word dropped its low bits)
+          state = 1;
+          break;
+        }
+        lb[0][0] = sqrt(cx[0]);
+        int m = 1;
+#pragma unroll
+        for (int t = 1; t < kBP; ++t) {
+          if (t < mmax && m == t) {
+            double dd = cx[t];
+#pragma unroll
+            for (int b = 0; b < kBP; ++b) {
+              if (b < t) {
+                double x = sBv[t * kBW + b];
+                // all 16 panel terms, unconditionally: the words past k are zero (a runtime-bounded
+                // loop waited an LDS round trip per term)
+#pragma unroll
+                for (int q = 0; q < kNB; ++q) x = fma(-sBv[t * kBW + kBP + q], sBv[b * kBW + kBP + q], x);
+#pragma unroll
+                for (int c = 0; c < kBP; ++c)
+                  if (c < b) x = fma(-lb[t][c], lb[b][c], x);
+                lb[t][b] = x / lb[b][b];
+                dd = fma(-lb[t][b], lb[t][b], dd);
+              }
+            }
+            if (dd > tol && dd >= kEta * cx[0]) {
+              lb[t][t] = sqrt(dd);
+              m = t + 1;
+            }
           }
         }
-        Lr[k] = l;
-        if (lane < R && fi < n) put(a.w + static_cast<int64_t>(j) * N + fi, bits_of(l));
-        if (g == 0 && lane == 0) a.piv[j] = p;
-        rank = j + 1;
-        if (k < 8 && P < 4) PC_STAMP(2 * (P * 8 + k) + 1);
-        if (j + 1 < n) {
-          publish(a, j + 1, k + 1 < kNB ? k + 1 : 0, d, live, fi, Lr);
-          if (!poll_candidates(a, j + 1, dp, p, abort_w)) {
+        // this lane's row: its m new column values
+        double lr[kBP];
+#pragma unroll
+        for (int t = 0; t < kBP; ++t) {
+          double l = 0.0;
+          if (t < m && live) {
+            if (fi == cp[t]) {
+              l = lb[t][t];
+              live = false;
+            } else {
+              double x = rows[lane * N + cp[t]];
+#pragma unroll
+              for (int q = 0; q < kNB; ++q) x = fma(-Lr[q], sBv[t * kBW + kBP + q], x);  // (Lr past k: 0)
+#pragma unroll
+              for (int b = 0; b < kBP; ++b)
+                if (b < t) x = fma(-lr[b], lb[t][b], x);
+              l = x / lb[t][t];
+              d = fma(-l, l, d);
+            }
+          }
+          lr[t] = l;
+          if (t < m) {
+            Lr[k + t] = l;
+            if (lane < R && fi < n) put(a.w + static_cast<int64_t>(j + t) * N + fi, bits_of(l));
+            if (g == 0 && lane == 0) a.piv[j + t] = cp[t];
+          }
+        }
+        if (s < 8 && P < 4) PC_STAMP(2 * (P * 8 + (s & 7)) + 1);
+        j += m;
+        k += m;
+        rank = j;
+        ++s;
+        if (j < n) {
+          publish_top(a, s, d, live, fi, k == kNB);
+          if (!poll_top(a, s, cv, cp, abort_w)) {
             state = 2;
             break;
           }
@@ -322,14 +488,14 @@ __global__ __launch_bounds__(kPT) void pivchol_kernel(PcArgs a) {
       }
 #pragma unroll
       for (int q = 0; q < kNB; ++q) Lr[q] = 0.0;
-      if (state == 0 && j0 + kNB >= n) state = 1;
+      if (state == 0 && j >= n) state = 1;
       if (lane == 0) {
         s_state = state;
         if (state != 0 && g == 0) {
           a.info[0] = rank;
           if (state == 2) atomicOr(&a.info[1], 2);
         }
-        // every workgroup's step j0 + 15 W stores drained before its step j0 + 16 candidate,
+        // every workgroup's W stores of the panel drained before its next-round candidates,
         // which this wave has seen: one acquire, then the update reads the panel plainly
         if (state == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       }
@@ -366,11 +532,7 @@ __global__ __launch_bounds__(kPT) void pivchol_kernel(PcArgs a) {
           if (m0 + u * kPT < n) rows[r * N + m0 + u * kPT] = acc[u];
       }
     }
-    bool ok = true;
-    if (__syncthreads_or(!ok) != 0) {
-      if (tid == 0 && g == 0) atomicOr(&a.info[1], 2);
-      break;
-    }
+    __syncthreads();
     if (P < 4) PC_STAMP(64 + 2 * P + 1);
   }
 }
@@ -394,12 +556,12 @@ int pivchol_padded(int64_t n) { return static_cast<int>((n + 63) / 64 * 64); }
 
 int64_t pivchol_slot_words(int64_t n) {
   const int64_t G = n < 1 ? 1 : pc_grid(n);
-  return G + n * G * kSlotW;
+  return G + n * G * kAW + n * kBP * kBW;  // tolerance words, A slots per round, B slots per round
 }
 
-// trace (optional, >= 80 words, s_memrealtime 100 MHz, workgroup 0): [2 (8 P + k)] step start
-// (pivot known) / [+1] its W row stored, for steps k < 8 of panels P < 4; [64 + 2 P] / [+1] panel
-// P's update start / end
+// trace (optional, >= 80 words, s_memrealtime 100 MHz, workgroup 0): [2 (8 P + s % 8)] round start
+// (candidates known) / [+1] its W rows stored, for panels P < 4; [64 + 2 P] / [+1] panel P's
+// update start / end
 int launch_pivchol(const double* A, int64_t lda, int64_t n, unsigned long long* slots, double* w, int* piv, int* info,
                    unsigned* ctl, hipStream_t stream, unsigned long long* trace) {
   if (n < 1 || n > kNMax) return 4;
