@@ -12,21 +12,25 @@
 // MI355X design: the trailing matrix never leaves the chip.  One cooperative launch, one
 // 256-thread workgroup per CU; workgroup g keeps R = ceil(D / G) <= 8 whole rows of the matrix in
 // LDS (8 x 2048 x 8 B = 128 KB at D = 2048 on 256 CUs) and wave 0 of each workgroup runs the
-// column steps for its rows:
-//  * every workgroup publishes its best (Schur diagonal, feature) candidate, together with that
-//    feature's values in the current 16-column panel, to its own slot of the step;
-//  * each wave 0 reads all G candidates (lanes poll 4 slots each), reduces them to the pivot p
-//    with DPP row reductions and gfx950's permlane16 / permlane32 swaps (every workgroup gets
-//    the same p: a total order, ties to the lower feature), reads the winner's panel values,
-//    and forms its rows' column values l_i = (A'[i][p] - L[i][panel] . L[p][panel]) / sqrt(d_p)
-//    locally (A'[i][p] = A'[p][i] is its own LDS row), publishing them as row j of W;
+// pivot rounds for its rows.  A round takes up to 4 columns with TWO cross-CU exchanges:
+//  * A: every workgroup publishes its 4 best (Schur diagonal, feature) candidates, one packed
+//    word each (the diagonal's bits with the feature in its low mantissa bits: ranking only);
+//    each wave 0 reads all 4 G words (16 per lane, re-polled together) and picks the round's 4
+//    best with DPP row reductions and gfx950's permlane16 / permlane32 swaps - every workgroup
+//    the same, ties to the lower feature;
+//  * B: each chosen candidate's owner publishes its row of the 4 x 4 block A'(p_a, p_b) (its own
+//    LDS row), its panel values and its exact diagonal; every workgroup factors the block with
+//    relaxed pivoting (candidate a is taken while its Schur diagonal after the earlier ones is
+//    >= 1/4 of the round's first, i.e. within a factor 4 of the greedy choice; the first is the
+//    exact greedy pivot) and forms its rows' values l_i,a from its LDS rows (A'(i, p_a) =
+//    A'(p_a, i)), publishing them as rows of W;
 //  * after 16 columns all 4 waves apply the panel's rank-16 update to the LDS rows, reading the
-//    panel's W rows (256 KB, the same for every workgroup).
-// One cross-CU exchange per column (the candidates; the winner's panel values ride along), no
-// trailing-matrix traffic to HBM.  Hand-offs are sentinel words (round 3's K9b form: the slots and
-// W are filled with all-one bytes, a NaN pattern no stored value carries, and every value is
-// written once with an agent-scope store; consumers poll until none is the sentinel).  Every spin
-// is bounded and raises an abort word; the host then falls back to eigh.
+//    panel's W rows with plain loads behind one acquire (L2-served, 256 KB per XCD).
+// (One pivot per exchange took 6.3 ms at D = 2048, rank 999; the 4-pivot rounds 4.4 ms,
+// profiles/fid_singular_k9p_r6.json.)  Hand-offs are sentinel words (round 3's K9b form: the
+// slots and W are filled with all-one bytes, a NaN pattern no stored value carries, and every
+// value is written once with an agent-scope store; consumers poll until none is the sentinel).
+// Every spin is bounded and raises an abort word; the host then falls back to eigh.
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
