@@ -48,7 +48,17 @@ int main() {
   CK(hipMemset(trace, 0, 2 * 16 * 8 * 8));
   CK(hipMemcpy(dA, h.data(), (size_t)n * n * 8, hipMemcpyHostToDevice));
   CK(hipMemcpyToSymbol(HIP_SYMBOL(tea::g_symeig_trace), &trace, sizeof(trace)));
-  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.slots = gran; a.ctl = ctl; a.grid = grid;
+  unsigned long long* col = nullptr;
+  CK(hipMalloc(&col, n * 8));
+  CK(hipMemset(col, 0, n * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(tea::g_symeig_col), &col, sizeof(col)));
+  unsigned long long* ttr = nullptr;
+  CK(hipMalloc(&ttr, 16 * 8 * 8));
+  CK(hipMemset(ttr, 0, 16 * 8 * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(tea::g_symeig_tailtr), &ttr, sizeof(ttr)));
+  double* tailbuf = nullptr;  // the one-workgroup tail's trailing block (TORCHEVAL_AMD_SYMEIG_TAIL)
+  CK(hipMalloc(&tailbuf, tea::symeig_tail_bytes()));
+  a.a = dA; a.d = dd; a.e = de; a.lam = dl; a.slots = gran; a.ctl = ctl; a.grid = grid; a.tail = tailbuf;
   for (int it = 0; it < 3; ++it) {
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -78,5 +88,22 @@ int main() {
     }
   }
   (void)names;
+  // workgroup 0's column starts (100 MHz wall clock): mean us per column in blocks of 128
+  std::vector<unsigned long long> cs(n);
+  CK(hipMemcpy(cs.data(), col, n * 8, hipMemcpyDeviceToHost));
+  std::printf("us per column, workgroup 0, blocks of 128 columns:\n");
+  for (int b = 0; b + 128 <= n - 3; b += 128)
+    std::printf("  columns %4d-%4d: %.2f\n", b, b + 127, (double)(cs[b + 128] - cs[b]) / 100.0 / 128.0);
+  std::printf("  columns %4d-%4d: %.2f (total to last column %.3f ms)\n", (n - 3) / 128 * 128, n - 3,
+              (double)(cs[n - 3] - cs[(n - 3) / 128 * 128]) / 100.0 / ((n - 3) % 128 ? (n - 3) % 128 : 1),
+              (double)(cs[n - 3] - cs[0]) / 1e5);
+  std::vector<unsigned long long> tt(16 * 8);
+  CK(hipMemcpy(tt.data(), ttr, tt.size() * 8, hipMemcpyDeviceToHost));
+  std::printf("tail kernel (cycles), columns 1-14: top->sigma, ->reflector, ->matvec+reduce, barrier, ->update | column\n");
+  for (int j = 1; j < 15; ++j) {
+    const unsigned long long* q = &tt[j * 8];
+    std::printf("  j=%d: %llu %llu %llu %llu %llu | %llu\n", j, q[1] - q[0], q[2] - q[1], q[3] - q[2], q[4] - q[3],
+                q[5] - q[4], tt[(j + 1) * 8] - q[0]);
+  }
   return 0;
 }

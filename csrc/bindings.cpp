@@ -1165,14 +1165,17 @@ int64_t sym_eigvals(const Tensor& m, const Tensor& lam, const Tensor& status) {
   a.n = n;
   a.ld = tea::symeig_slot_stride(n);
   // layout: ctl (2 KB), d [ld], e [ld], the 2 hand-off slot planes (sentinel-filled by the
-  // launcher on every call, so no state carries over between launches), the Sturm-count grid
-  const int64_t bytes = 2048 + 2 * a.ld * (int64_t)sizeof(double) + tea::symeig_slot_bytes(n) + tea::symeig_grid_bytes();
+  // launcher on every call, so no state carries over between launches), the Sturm-count grid,
+  // the tail kernel's trailing block
+  const int64_t bytes = 2048 + 2 * a.ld * (int64_t)sizeof(double) + tea::symeig_slot_bytes(n) + tea::symeig_grid_bytes() +
+                        tea::symeig_tail_bytes();
   char* ws = static_cast<char*>(scratch_workspace(m, stream, bytes, 3));
   a.ctl = reinterpret_cast<unsigned*>(ws);
   a.d = reinterpret_cast<double*>(ws + 2048);
   a.e = a.d + a.ld;
   a.slots = reinterpret_cast<unsigned long long*>(a.e + a.ld);
   a.grid = reinterpret_cast<int*>(reinterpret_cast<char*>(a.slots) + tea::symeig_slot_bytes(n));
+  a.tail = reinterpret_cast<double*>(reinterpret_cast<char*>(a.grid) + tea::symeig_grid_bytes());
   a.lam = lam.data_ptr<double>();
   const int rc = tea::launch_symeig(a, stream);
   if (rc == 1 || rc == 3) return rc;

@@ -538,12 +538,14 @@ struct SymEigArgs {
                                         // symeig_slot_bytes(n) (sentinel-filled by the launcher)
   unsigned* ctl = nullptr;    // 128 B: ctl[1] abort word (zeroed by the launcher)
   int* grid = nullptr;        // symeig_grid_bytes(): Sturm counts of the eigenvalue search grid
+  double* tail = nullptr;     // symeig_tail_bytes(): the trailing block the one-workgroup tail finishes
 };
 // 0 when the on-chip one-launch reduction fits this device (grid / rows per block out)
 int symeig_plan(int64_t n, int* grid, int* rows_per_block);
 int64_t symeig_slot_stride(int64_t n);
 int64_t symeig_slot_bytes(int64_t n);
 int64_t symeig_grid_bytes();
+int64_t symeig_tail_bytes();
 // 0 launched, 1 unsupported size, 2 HIP error, 3 cooperative launch refused
 int launch_symeig(const SymEigArgs& a, hipStream_t stream);
 

@@ -51,9 +51,24 @@ constexpr int kMaxCols = 10;   // columns per thread: n <= 2560
 constexpr int kMaxRows = 10;   // rows per workgroup (registers: R x C doubles per thread)
 constexpr unsigned kSpinLimit = 1u << 18;
 constexpr size_t kCtlBytes = 128;  // ctl[1] = abort word
+// The last kTail columns of the reduction run in ONE workgroup with the trailing block in
+// registers (symeig_tail_kernel): ~1.7 us a column there (a latency-bound chain of LDS round
+// trips, DPP sums, sqrt / divisions and two barriers) against ~3.7 us a column for the grid's
+// cross-CU hand-off (the grid's column cost is nearly flat in j: 4.4 us at j = 0, 3.7 at the end)
+constexpr int kTail = 128;
 
 #ifdef TEA_SYMEIG_TRACE  // csrc/bench/k9b_trace.hip: per-phase timestamps of two workgroups
 __device__ unsigned long long* g_symeig_trace;
+__device__ unsigned long long* g_symeig_col;  // workgroup 0's s_memrealtime (100 MHz) at every column
+__device__ unsigned long long* g_symeig_tailtr;  // symeig_tail_kernel phase stamps, columns 0..15
+#define SYM_TT(j, i)                                                                   \
+  do {                                                                                 \
+    if (threadIdx.x == 0 && (j) < 16) g_symeig_tailtr[(j) * 8 + (i)] = clock64();      \
+  } while (0)
+#define SYM_COL(j)                                                        \
+  do {                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_symeig_col[j] = wall_clock64(); \
+  } while (0)
 #define SYM_TRACE(j, i)                                                                       \
   do {                                                                                       \
     if (threadIdx.x == 0 && (blockIdx.x == 0 || blockIdx.x == 100) && (j) >= 1000 &&         \
@@ -63,6 +78,12 @@ __device__ unsigned long long* g_symeig_trace;
 #else
 #define SYM_TRACE(j, i) \
   do {                  \
+  } while (0)
+#define SYM_COL(j) \
+  do {             \
+  } while (0)
+#define SYM_TT(j, i) \
+  do {               \
   } while (0)
 #endif
 
@@ -309,7 +330,7 @@ template <int C, int RM, int NT = kThreads>
 __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ A, int n,
                                                      int R, int64_t ld, double* d_out,
                                                      double* e_out, unsigned long long* slots,
-                                                     unsigned* ctl) {
+                                                     unsigned* ctl, double* tail, int jt) {
   __shared__ double red[3][(NT / 16) * RM];
   __shared__ double bc[2][4];  // single-element broadcasts riding on the reductions' barriers
   __shared__ double vw[2][RM];
@@ -373,6 +394,8 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
   // (Skipping whole dead column slots with wave-uniform branches in the loads and the LDS
   // pass measured slower - 19.4 vs 17.9 ms at D = 2048: the branches split the batched loads.)
   for (int j = 0; j <= n - 3; ++j) {
+    if (j == jt) break;  // the trailing block goes to symeig_tail_kernel (below the loop)
+    SYM_COL(j);
     // ---- w_j from the gathered p_j; row j+1 updated through step j.  Each thread polls the
     // slots of ITS columns until none holds the sentinel (bounded; any abort ends the
     // block at the reduction barrier below)
@@ -512,6 +535,21 @@ __global__ __launch_bounds__(NT) void tridiag_kernel(const double* __restrict__ 
     for (int s = 0; s < C; ++s) v[s] = vn[s];
     h = hn;
     SYM_TRACE(j, 5);
+  }
+  if (jt < n) {
+    // stopped at column jt: the owned rows' columns >= jt (updated through step jt - 1) are the
+    // tail kernel's trailing block
+#pragma unroll
+    for (int r = 0; r < RM; ++r) {
+      const int row = row0 + r;
+      if (r < nrows && row >= jt) {
+#pragma unroll
+        for (int s = 0; s < C; ++s) {
+          const int k = t + s * NT;
+          if (k >= jt && k < n) tail[(int64_t)(row - jt) * kTail + (k - jt)] = rw[r][s];
+        }
+      }
+    }
   }
 }
 
@@ -764,6 +802,141 @@ __global__ __launch_bounds__(kThreads, 1) void tridiag_wave_kernel(const double*
   }
 }
 
+// The reduction's last kTail columns on one workgroup (LAPACK dsytd2 on the trailing block),
+// the block held in registers: TR x 8 tiles, 16 tile columns, kTail / TR tile rows, one thread a
+// tile (thread t: tile row t / 16, tile column t % 16; a 16-lane DPP row = one tile row).  Per
+// column: the owners of column j publish it (barrier), every wave forms the reflector
+// redundantly from it (DPP sums), the tile products p = M v reduce over the 16 lanes of a tile
+// row (DPP), tau p goes through LDS (barrier), p . v reduces over a tile row's column tiles,
+// then the rank-2 update M -= v w^T + w v^T in registers.
+// a lane's double in every lane (two readlanes)
+__device__ __forceinline__ double lane_f64(double x, int l) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <int TR>
+__global__ __launch_bounds__(16 * kTail / TR) void symeig_tail_kernel(const double* __restrict__ tail, int n,
+                                                                      double* d_out, double* e_out) {
+  constexpr int NT = 16 * kTail / TR;
+  __shared__ double col[kTail];
+  __shared__ double tp[kTail];
+  const int t = threadIdx.x, rb = t >> 4, cb = t & 15, jt = n - kTail;
+  double m[TR][8];
+#pragma unroll
+  for (int a = 0; a < TR; ++a)
+#pragma unroll
+    for (int b = 0; b < 8; ++b) m[a][b] = tail[(rb * TR + a) * kTail + cb * 8 + b];
+  if (cb == 0) {
+#pragma unroll
+    for (int a = 0; a < TR; ++a) col[rb * TR + a] = m[a][0];
+  }
+  __syncthreads();
+  for (int jb = 0; jb < kTail / 8; ++jb) {
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int j = jb * 8 + jj;
+      if (j > kTail - 3) break;
+      SYM_TT(j, 0);
+      // reflector of column j (rows > j), redundantly in every wave
+      const int l = t & 63;
+      const double x0 = col[l], x1 = col[l + 64];
+      // every column value this thread needs, loaded unconditionally up front (loads under the
+      // v selects below compiled to one branch and one LDS round trip each)
+      double cr[TR], cc[8];
+#pragma unroll
+      for (int a = 0; a < TR; ++a) cr[a] = col[rb * TR + a];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) cc[b] = col[cb * 8 + b];
+      const double cj = col[j];
+      double sg = row16_sum((l >= j + 2 ? x0 * x0 : 0.0) + (l + 64 >= j + 2 ? x1 * x1 : 0.0));
+      sg = (lane_f64(sg, 0) + lane_f64(sg, 16)) + (lane_f64(sg, 32) + lane_f64(sg, 48));
+      const double alpha = col[j + 1];
+      SYM_TT(j, 1);
+      double tau, beta, scale;
+      if (sg == 0.0) {
+        tau = 0.0;
+        beta = alpha;
+        scale = 0.0;
+      } else {
+        const double mu = sqrt(alpha * alpha + sg);
+        beta = alpha >= 0.0 ? -mu : mu;
+        tau = (beta - alpha) / beta;
+        scale = 1.0 / (alpha - beta);
+      }
+      if (t == 0) {
+        d_out[jt + j] = cj;
+        e_out[jt + j] = beta;
+      }
+      SYM_TT(j, 2);
+      double vr[TR], vc[8];
+#pragma unroll
+      for (int a = 0; a < TR; ++a) {
+        const int i = rb * TR + a;
+        vr[a] = i == j + 1 ? 1.0 : (i > j + 1 ? cr[a] * scale : 0.0);
+      }
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        const int k = cb * 8 + b;
+        vc[b] = k == j + 1 ? 1.0 : (k > j + 1 ? cc[b] * scale : 0.0);
+      }
+      // p = tau M v: tile products, reduced over the tile row's 16 lanes
+      double p[TR];
+#pragma unroll
+      for (int a = 0; a < TR; ++a) {
+        double acc = 0.0;
+#pragma unroll
+        for (int b = 0; b < 8; ++b) acc = fma(m[a][b], vc[b], acc);
+        p[a] = acc;
+      }
+#pragma unroll
+      for (int a = 0; a < TR; ++a) p[a] = tau * row16_sum(p[a]);
+      SYM_TT(j, 3);
+      if (cb == 0) {
+#pragma unroll
+        for (int a = 0; a < TR; ++a) tp[rb * TR + a] = p[a];
+      }
+      __syncthreads();
+      SYM_TT(j, 4);
+      // p . v over the tile row's 16 column tiles (every index once)
+      double tc[8], pv = 0.0;
+#pragma unroll
+      for (int b = 0; b < 8; ++b) {
+        tc[b] = tp[cb * 8 + b];
+        pv = fma(tc[b], vc[b], pv);
+      }
+      const double K = 0.5 * tau * row16_sum(pv);
+      double wr[TR], wc[8];
+#pragma unroll
+      for (int a = 0; a < TR; ++a) wr[a] = p[a] - K * vr[a];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) wc[b] = tc[b] - K * vc[b];
+#pragma unroll
+      for (int a = 0; a < TR; ++a)
+#pragma unroll
+        for (int b = 0; b < 8; ++b) m[a][b] = fma(-vr[a], wc[b], fma(-wr[a], vc[b], m[a][b]));
+      SYM_TT(j, 5);
+      // the next column, as updated through this step
+      const int jn = j + 1;
+      if (cb == (jn >> 3)) {
+#pragma unroll
+        for (int a = 0; a < TR; ++a) {
+          double x = 0.0;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) x = b == (jn & 7) ? m[a][b] : x;
+          col[rb * TR + a] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  if (t == NT - 1) {  // the last tile: rows kTail - TR .., columns kTail - 8 ..
+    d_out[n - 2] = m[TR - 2][6];
+    e_out[n - 2] = m[TR - 1][6];
+    d_out[n - 1] = m[TR - 1][7];
+  }
+}
+
 // # eigenvalues of the tridiagonal (d, e2 = e^2) below x (LAPACK dstebz's Sturm count).
 // (Round 3: the bare v_rcp_f64 was faster but cost 6e-9 of accuracy, and rcp + Newton with two
 // interleaved chains per lane measured 13% slower; round 5: one chain, rcp + one Newton step,
@@ -931,6 +1104,8 @@ int64_t symeig_slot_stride(int64_t n) { return (n + 15) / 16 * 16; }
 
 int64_t symeig_grid_bytes() { return (int64_t)kGrid * sizeof(int); }
 
+int64_t symeig_tail_bytes() { return (int64_t)kTail * kTail * sizeof(double); }
+
 int64_t symeig_slot_bytes(int64_t n) { return 2 * (n - 2) * symeig_slot_stride(n) * (int64_t)sizeof(unsigned long long); }
 
 int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
@@ -1008,7 +1183,14 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   double *d = a.d, *e = a.e;
   unsigned long long* slots = a.slots;
   unsigned* ctl = a.ctl;
-  void* args[] = {&A, &n, &R, &ld, &d, &e, &slots, &ctl};
+  // the last kTail columns in one workgroup (TORCHEVAL_AMD_SYMEIG_TAIL=0: the grid does all, A/B)
+  static const bool tail_on = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_TAIL");
+    return !(e && e[0] == '0');
+  }();
+  double* tail = a.tail;
+  int jt = (tail_on && tail != nullptr && !wkern && n >= 2 * kTail) ? n - kTail : n;
+  void* args[] = {&A, &n, &R, &ld, &d, &e, &slots, &ctl, &tail, &jt};
   void* wargs[] = {&A, &n, &ld, &d, &e, &slots, &ctl};
   // TORCHEVAL_AMD_SYMEIG_COOP=0: a plain launch of the same grid (A/B of the cooperative
   // launch's process-exit behaviour under rocprofv3; G <= #CUs workgroups are co-resident in
@@ -1024,6 +1206,21 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
   const hipError_t lrc = coop ? hipLaunchCooperativeKernel(lk, dim3(lg), dim3(lt), la, 0, stream)
                               : hipLaunchKernel(lk, dim3(lg), dim3(lt), la, 0, stream);
   if (lrc != hipSuccess) return 3;
+  // tile height: TORCHEVAL_AMD_SYMEIG_TAIL_TR=8 (256 threads, the default) / 4 (512) / 2 (1024):
+  // 210 / 217 / 280 us at D = 2048 (profiles/k9b_tail_r6.json)
+  static const int tail_tr = [] {
+    const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_TAIL_TR");
+    const int v = e ? std::atoi(e) : 8;
+    return (v == 2 || v == 4) ? v : 8;
+  }();
+  if (jt < n) {
+    if (tail_tr == 8)
+      symeig_tail_kernel<8><<<1, 16 * kTail / 8, 0, stream>>>(tail, n, d, e);
+    else if (tail_tr == 2)
+      symeig_tail_kernel<2><<<1, 16 * kTail / 2, 0, stream>>>(tail, n, d, e);
+    else
+      symeig_tail_kernel<4><<<1, 16 * kTail / 4, 0, stream>>>(tail, n, d, e);
+  }
   sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
   // lanes per eigenvalue: 32 from D = 1536 (with the rcp + Newton Sturm steps 32 lanes edge out
   // 16: 9.34-9.36 vs 9.40-9.42 ms at D = 2048, profiles/symeig_L_ab_r5.json), else 64;
