@@ -1,7 +1,6 @@
 """K9b tail A/B: FID compute at D = 2048 (full rank) and sym_eigvalsh accuracy against torch's
 eigvalsh, one process per arm (TORCHEVAL_AMD_SYMEIG_TAIL is read once per process).
-The tail arm was measured slower and removed (profiles/k9b_tail_attempt_r6.json); the variable
-is now ignored and both arms run the grid-only reduction."""
+TORCHEVAL_AMD_SYMEIG_TAIL=0 runs the grid-only reduction (profiles/k9b_tail_r6.json)."""
 import json
 import os
 import sys
