@@ -10,5 +10,7 @@ tail -15 gpurun_out/r6_pytest_gpu.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python -u benchmarks/bench_suite.py --out gpurun_out/r6_bench_suite.json > gpurun_out/r6_bench_suite.log 2>&1 || { tail -20 gpurun_out/r6_bench_suite.log; exit 1; }
 tail -45 gpurun_out/r6_bench_suite.log
+timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r6_smoke.log 2>&1 || { tail -20 gpurun_out/r6_smoke.log; exit 1; }
+echo smoke ok
 timeout -k 10 300 python -u bench.py > gpurun_out/r6_bench.log 2>&1 || { tail -20 gpurun_out/r6_bench.log; exit 1; }
 tail -1 gpurun_out/r6_bench.log

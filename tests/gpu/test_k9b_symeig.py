@@ -47,9 +47,9 @@ def test_indefinite_and_clustered(n):
     torch.testing.assert_close(got, ref, rtol=0, atol=1e-12 * n * 5)
 
 
+@pytest.mark.parametrize("n", [129, 384])  # 384: the grid hands its last 128 columns to the one-workgroup tail
 @pytest.mark.parametrize("kind", ["zeros", "identity", "diagonal", "rank3", "tridiagonal"])
-def test_structured(kind):
-    n = 129
+def test_structured(kind, n):
     if kind == "zeros":
         m = torch.zeros(n, n, dtype=torch.float64)
     elif kind == "identity":
@@ -66,6 +66,22 @@ def test_structured(kind):
     got = _native_eig(m.to(DEV))
     scale = max(float(ref.abs().max()), 1.0)
     torch.testing.assert_close(got, ref, rtol=0, atol=1e-12 * n * scale)
+
+
+@pytest.mark.parametrize("n", [256, 257, 383, 640])
+def test_tail_block_boundaries(n):
+    # the grid reduction stops at column n - 128 and the tail kernel finishes the trailing block:
+    # spectra whose trailing block is already diagonal (zero reflectors in the tail), or couples
+    # to the leading block only through one entry
+    m = _spd(n, n)
+    m[n - 128 :, n - 128 :] = torch.diag(torch.linspace(-3, 3, 128, dtype=torch.float64))
+    m[n - 128 :, : n - 128] = 0.0
+    m[: n - 128, n - 128 :] = 0.0
+    m[n - 1, 0] = m[0, n - 1] = 0.5
+    for mat in (m, _spd(n, n + 1)):
+        ref = torch.linalg.eigvalsh(mat)
+        got = _native_eig(mat.to(DEV))
+        torch.testing.assert_close(got, ref, rtol=0, atol=1e-12 * n * max(float(ref.abs().max()), 1.0))
 
 
 def test_repeated_calls_reuse_workspace():
