@@ -301,7 +301,45 @@ def cases(dev: torch.device, s: float) -> Dict[str, Callable[[], Callable[[], ob
         step = GraphedUpdate(m, x, y)
         return lambda: step(x, y)
 
+    def five(bs, c):
+        # a training step's classification metrics, all fed the same batch
+        return [
+            M.MulticlassAccuracy(num_classes=c, device=dev),
+            M.MulticlassPrecision(num_classes=c, device=dev),
+            M.MulticlassRecall(num_classes=c, device=dev),
+            M.MulticlassF1Score(num_classes=c, device=dev),
+            M.MulticlassConfusionMatrix(c, device=dev),
+        ]
+
+    def five_direct(bs, c):
+        def make():
+            x, y = torch.randn(bs, c, device=dev, generator=g), randint(c, bs)
+            ms = five(bs, c)
+
+            def step():
+                for m in ms:
+                    m.update(x, y)
+
+            return step
+        return make
+
+    def five_graphed(bs, c):
+        def make():
+            x, y = torch.randn(bs, c, device=dev, generator=g), randint(c, bs)
+            ms = five(bs, c)
+            if dev.type != "cuda":
+                return lambda: [m.update(x, y) for m in ms]
+            from torcheval_amd.utils.graphs import GraphedUpdate
+
+            step = GraphedUpdate(ms, x, y, check_speed=False)
+            return lambda: step(x, y)
+        return make
+
     return {
+        "5 multiclass metrics (acc/prec/rec/F1/CM) .update bs=8 C=6": five_direct(n(8), 6),
+        "5 multiclass metrics .update bs=8 C=6, one HIP graph": five_graphed(n(8), 6),
+        "5 multiclass metrics .update bs8192 C1000": five_direct(B, C),
+        "5 multiclass metrics .update bs8192 C1000, one HIP graph": five_graphed(B, C),
         "multiclass_accuracy functional bs=8 C=6": small_functional,
         "MulticlassAccuracy.update bs=8 C=6": small_class,
         "MulticlassAccuracy.update bs=8 C=6 HIP-graph replay": small_graphed,
