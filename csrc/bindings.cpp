@@ -1467,23 +1467,22 @@ bool onesweep_faulted(const Tensor& x, hipStream_t st) {
   return true;
 }
 
-void onesweep_watch(const Tensor& x, hipStream_t st, const uint32_t* hdr) {
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return;
+// the pinned host word of this (device, stream) that each onesweep sort's histogram launch fills
+// with the PREVIOUS sort's timeout word (RadixArgs::os_watch): a timed-out sort is reported one
+// sort later (its own K3 scan already returned NaN from the device word), and no sort pays a
+// device-to-host copy on its stream (the hipMemcpyAsync of round 5 was a ~5 us blit kernel in
+// every binary_auroc's timeline)
+uint32_t* onesweep_watch_word(const Tensor& x, hipStream_t st) {
   auto& h = onesweep_health();
-  uint32_t* word = nullptr;
-  {
-    std::lock_guard<std::mutex> lock(h.mu);
-    auto it = h.host_word.find(stream_key(x, st));
-    if (it == h.host_word.end()) {
-      void* p = nullptr;
-      if (hipHostMalloc(&p, 64, hipHostMallocDefault) != hipSuccess) return;
-      std::memset(p, 0, 64);
-      it = h.host_word.emplace(stream_key(x, st), static_cast<uint32_t*>(p)).first;
-    }
-    word = it->second;
+  std::lock_guard<std::mutex> lock(h.mu);
+  auto it = h.host_word.find(stream_key(x, st));
+  if (it == h.host_word.end()) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocCoherent) != hipSuccess) return nullptr;
+    std::memset(p, 0, 64);
+    it = h.host_word.emplace(stream_key(x, st), static_cast<uint32_t*>(p)).first;
   }
-  (void)hipMemcpyAsync(word, hdr + 8, 4, hipMemcpyDeviceToHost, st);
+  return it->second;
 }
 
 // `fold` (optional, float64 [rows, ceil(n / 1024), 2]): with a target / label payload on the
@@ -1572,6 +1571,7 @@ bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
     a.os_gplane = gcap / 16;  // two u64 planes
     a.bkt_spl = bkt;
     a.bkt_cnt = bkt + a.rows * 256;
+    a.os_watch = onesweep_watch_word(x, st);
   }
   Tensor pl;
   if (payload.has_value() && payload_kind != 0) {
@@ -1613,7 +1613,6 @@ bool sort_desc(const Tensor& x, const Tensor& out_sorted, const Tensor& out_orde
     }
   }
   check_launch(tea::launch_radix_sort_desc(a, stream_for(x)), "sort_desc");
-  if (a.os_hdr != nullptr) onesweep_watch(x, stream_for(x), a.os_hdr);
   return a.fold_ab != nullptr;
 }
 

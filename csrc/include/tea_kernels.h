@@ -473,6 +473,9 @@ struct RadixArgs {
   uint32_t* os_hdr = nullptr;     // [16]: [4..7] dirty extents of the status / group planes,
                                   // [8] look-back timeout flag (cleared by each sort's histogram
                                   // launch, so it describes the latest onesweep sort of the stream)
+  uint32_t* os_watch = nullptr;   // host (pinned) word: the histogram launch copies [8] there before
+                                  // clearing it, so the host learns of a timed-out sort one sort
+                                  // later without a device-to-host copy on the stream
   int spin_limit = 1 << 22;       // look-back polls before a tile gives up (TORCHEVAL_AMD_K3_SPIN_LIMIT)
   uint32_t* os_g = nullptr;       // [rows, 8 copies, 4, 256] digit totals (hist kernel; cleared by pass 3)
   uint32_t* os_status = nullptr;  // 2 planes of [rows * tiles, 256] ready-flagged tile counts

@@ -421,8 +421,12 @@ __device__ __forceinline__ void os_add64(unsigned long long* p, unsigned long lo
 __global__ __launch_bounds__(kRT) void onesweep_hist_kernel(RadixArgs a, int64_t per_block) {
   constexpr int kC = 8;
   __shared__ uint32_t h[4][kC][kBins + 1];
-  // this sort's look-back timeout word starts clear (the passes run after this launch)
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.os_hdr[8] = 0u;
+  // this sort's look-back timeout word starts clear (the passes run after this launch); the
+  // previous sort's word goes to the host first (RadixArgs::os_watch)
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    if (a.os_watch != nullptr) a.os_watch[0] = a.os_hdr[8];
+    a.os_hdr[8] = 0u;
+  }
   for (int q = threadIdx.x; q < 4 * kC * (kBins + 1); q += kRT) (&h[0][0][0])[q] = 0u;
   __syncthreads();
   const int64_t row = blockIdx.y;
@@ -961,7 +965,10 @@ __global__ __launch_bounds__(kRT) void bkt_hist_kernel(RadixArgs a, int64_t per_
   constexpr int kC = 8;
   __shared__ uint32_t h[kC][kBins + 1];
   __shared__ uint32_t spl[kBins];
-  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) a.os_hdr[8] = 0u;
+  if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    if (a.os_watch != nullptr) a.os_watch[0] = a.os_hdr[8];
+    a.os_hdr[8] = 0u;
+  }
   const int64_t row = blockIdx.y;
   for (int q = threadIdx.x; q < kC * (kBins + 1); q += kRT) (&h[0][0])[q] = 0u;
   spl[threadIdx.x] = threadIdx.x < kBins - 1 ? a.bkt_spl[row * kBins + threadIdx.x] : ~0u;
