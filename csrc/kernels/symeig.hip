@@ -960,6 +960,61 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e2, in
   return cnt;
 }
 
+// The same count from the three-term recurrence of the leading minors,
+// p_k = (d_k - x) p_{k-1} - e_{k-1}^2 p_{k-2} (count = sign changes of p_0 = 1, p_1, .., p_n): ONE
+// FMA on the recurrence's critical path (e^2 p_{k-2} is ready a step early; the sign change is
+// integer work on the sign words, off the path), against the ratio form's reciprocal, three FMAs
+// and the pivot guard (~94 cycles a step at one wave per SIMD).  Needs the tridiagonal scaled to
+// O(1) with every e^2 at least 2^-600 (tridiag_setup: zeros and tinier values are raised to it, a
+// perturbation of 2^-300 in e), so |p| grows at most 8x a step and two consecutive minors are
+// never both zero; the pair (p_{k-1}, p_{k-2}) is renormalised by a power of two every 4 steps.
+// An exact zero minor comes out +0 and counts as positive: with e^2 > 0 the next minor,
+// -e^2 p_{k-2}, has the sign opposite to p_{k-2}, so the pair contributes the one sign change the
+// ratio form's -pivmin convention gives.  Each step is exact for d_k, e_k^2 perturbed by an ulp
+// or two (backward stable, as the ratio form).
+__device__ __forceinline__ int sign_flip(double p, double q) {
+  return static_cast<int>((static_cast<unsigned>(__double2hiint(p)) ^ static_cast<unsigned>(__double2hiint(q))) >> 31);
+}
+__device__ __forceinline__ int sturm_count_prod(const double* d, const double* e2, int n, double x) {
+  double p2 = 1.0;
+  double p1 = d[0] - x;
+  int cnt = sign_flip(p1, p2);
+  int k = 1;
+  for (; k + 4 <= n; k += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double p = fma(d[k + u] - x, p1, -(e2[k + u - 1] * p2));
+      cnt += sign_flip(p, p1);
+      p2 = p1;
+      p1 = p;
+    }
+    const int ex = static_cast<int>((__double_as_longlong(fmax(fabs(p1), fabs(p2))) >> 52) & 0x7ff) - 1023;
+    p1 = ldexp(p1, -ex);
+    p2 = ldexp(p2, -ex);
+  }
+  for (; k < n; ++k) {
+    const double p = fma(d[k] - x, p1, -(e2[k - 1] * p2));
+    cnt += sign_flip(p, p1);
+    p2 = p1;
+    p1 = p;
+  }
+  return cnt;
+}
+
+// TORCHEVAL_AMD_SYMEIG_STURM: the count both eigenvalue kernels use (they must agree: the
+// multisection starts from the grid's cells).  1 = product form (default), 0 = ratio form.
+#ifndef TEA_STURM_PROD
+#define TEA_STURM_PROD 1
+#endif
+__device__ __forceinline__ int sturm_count_any(const double* d, const double* e2, int n, double x, double pivmin) {
+#if TEA_STURM_PROD
+  (void)pivmin;
+  return sturm_count_prod(d, e2, n, x);
+#else
+  return sturm_count(d, e2, n, x, pivmin);
+#endif
+}
+
 constexpr int kEigMaxN = 2560;
 
 // Sturm-count grid: kGrid points evenly spaced inside the Gershgorin interval, one count per
@@ -970,6 +1025,7 @@ constexpr int kGrid = 65536;
 
 struct Bounds {
   double a, b, pivmin, span;
+  double inv_scale;  // the arrays (and a, b, pivmin, span) are in units of 1 / inv_scale
 };
 
 // d, e^2 into LDS and the widened Gershgorin interval (block-cooperative; every kernel that
@@ -1015,6 +1071,31 @@ __device__ Bounds tridiag_setup(const double* __restrict__ d_in, const double* _
     emax = fmax(emax, red[2][w]);
   }
   Bounds r;
+  r.inv_scale = 1.0;
+#if TEA_STURM_PROD
+  {
+    // scale by a power of two (exact) so the Gershgorin span is in [1, 2): the product-form
+    // count's growth bound; every e^2 raised to at least 2^-600 (zeros included: the count is
+    // then exact for a matrix within 2^-300 of this one, far below rounding)
+    const double sp = fmax(fabs(lo), fabs(hi));
+    if (sp > 0.0 && sp <= DBL_MAX) {
+      const int ex = static_cast<int>((__double_as_longlong(sp) >> 52) & 0x7ff) - 1023;
+      if (ex > -1000) {
+        const double sc = ldexp(1.0, -ex), sc2 = sc * sc;
+        for (int k = t; k < n; k += kThreads) {
+          d[k] *= sc;
+          const double x = e2[k] * sc2;
+          e2[k] = x < 0x1p-600 ? 0x1p-600 : x;
+        }
+        lo *= sc;
+        hi *= sc;
+        emax *= sc2;
+        r.inv_scale = ldexp(1.0, ex);
+      }
+    }
+    __syncthreads();
+  }
+#endif
   r.pivmin = DBL_MIN * fmax(1.0, emax);
   r.span = fmax(fabs(lo), fabs(hi));
   // widen so count(a) = 0 and count(b) = n hold despite rounding
@@ -1034,7 +1115,7 @@ __global__ __launch_bounds__(kThreads) void sturm_grid_kernel(const double* __re
   __shared__ double red[3][kWaves];
   const Bounds q = tridiag_setup(d_in, e_in, n, d, e2, red);
   const int g = blockIdx.x * kThreads + threadIdx.x;
-  if (g < kGrid) counts[g] = sturm_count(d, e2, n, grid_x(q, g), q.pivmin);
+  if (g < kGrid) counts[g] = sturm_count_any(d, e2, n, grid_x(q, g), q.pivmin);
 }
 
 // L lanes per eigenvalue index i (ascending): L-point multisection of the eigenvalue's grid cell
@@ -1072,7 +1153,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double*
     done = done || width <= DBL_EPSILON * span + 2.0 * DBL_EPSILON * fmax(fabs(a), fabs(b)) + pivmin;
     if (__all(done)) break;
     const double x = a + width * (double)(sub + 1) / (double)(L + 1);
-    const int c = sturm_count(d, e2, n, x, pivmin);
+    const int c = sturm_count_any(d, e2, n, x, pivmin);
     const unsigned long long above = __ballot(c > idx);
     const unsigned long long gm = L == 64 ? above : (above >> (L * grp)) & ((1ull << (L % 64)) - 1ull);
     const int first = gm ? __ffsll((long long)gm) - 1 : L;
@@ -1083,7 +1164,7 @@ __global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double*
       if (first < L) b = xb;
     }
   }
-  if (sub == 0 && idx < n) lam[idx] = 0.5 * (a + b);
+  if (sub == 0 && idx < n) lam[idx] = 0.5 * (a + b) * q.inv_scale;
 }
 
 }  // namespace
