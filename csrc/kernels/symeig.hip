@@ -1130,9 +1130,8 @@ __global__ __launch_bounds__(kThreads) void tridiag_eigvals_kernel(const double*
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const Bounds q = tridiag_setup(d_in, e_in, n, d, e2, red);
   const double pivmin = q.pivmin, span = q.span;
-  // L lanes per eigenvalue, 64 / L eigenvalues per wave.  L = 16 (D >= 1536): 16-point
-  // sections need ~13 rounds instead of ~9 for 64 points, but 2.8x less Sturm work in all
-  // (1.63 vs 1.86 ms at D = 2048); smaller D keeps L = 64 for occupancy (0.29 vs 0.39 ms at 512).
+  // L lanes per eigenvalue, 64 / L eigenvalues per wave (fewer lanes: more rounds but less
+  // Sturm work in all; the launcher picks L, see launch_symeig).
   constexpr int kPer = 64 / L;
   const int grp = lane / L, sub = lane % L;
   const int idx = (blockIdx.x * kWaves + wave) * kPer + grp;
@@ -1303,14 +1302,14 @@ int launch_symeig(const SymEigArgs& a, hipStream_t stream) {
       symeig_tail_kernel<4><<<1, 16 * kTail / 4, 0, stream>>>(tail, n, d, e);
   }
   sturm_grid_kernel<<<kGrid / kThreads, kThreads, 0, stream>>>(d, e, n, a.grid);
-  // lanes per eigenvalue: 32 from D = 1536 (with the rcp + Newton Sturm steps 32 lanes edge out
-  // 16: 9.34-9.36 vs 9.40-9.42 ms at D = 2048, profiles/symeig_L_ab_r5.json), else 64;
-  // TORCHEVAL_AMD_SYMEIG_L=16 / 32 / 64 forces (A/B)
+  // lanes per eigenvalue: 64 (with the product-form Sturm count 64 / 32 / 16 lanes take 394-397 /
+  // 402-405 / 423-426 us at D = 2048, profiles/k9b_sturm_r6.json; the ratio form's 32 lanes had
+  // edged out 16 and 64 there); TORCHEVAL_AMD_SYMEIG_L=16 / 32 / 64 forces (A/B)
   static const int l_env = [] {
     const char* e = std::getenv("TORCHEVAL_AMD_SYMEIG_L");
     return e ? std::atoi(e) : 0;
   }();
-  const int L = (l_env == 16 || l_env == 32 || l_env == 64) ? l_env : (n >= 1536 ? 32 : 64);
+  const int L = (l_env == 16 || l_env == 32 || l_env == 64) ? l_env : 64;
   if (L == 16)
     tridiag_eigvals_kernel<16><<<(n + kWaves * 4 - 1) / (kWaves * 4), kThreads, 0, stream>>>(d, e, n, a.grid, a.lam);
   else if (L == 32)

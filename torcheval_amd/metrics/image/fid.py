@@ -66,7 +66,7 @@ def _tr_sqrt_product(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optio
     return lam.clamp(min=0).sqrt().sum()
 
 
-def _spectrum(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optional[int] = None) -> Tensor:
+def _spectrum(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optional[int] = None, finish=None) -> Tensor:
     """Eigenvalues (FP64) whose square roots sum to tr sqrt(S1 S2).
 
     The eigenvalues of S1 S2 equal those of the symmetric L^T S2 L when S1 = L L^T, so the
@@ -85,40 +85,56 @@ def _spectrum(s1: Tensor, s2: Tensor, n1: Optional[int] = None, n2: Optional[int
     sample rank).
 
     ``n1`` / ``n2`` (optional sample counts) mark a side with n <= D as singular up front, so
-    its Cholesky is not attempted; the pivoted factor then takes the side with fewer samples."""
+    its Cholesky is not attempted; the pivoted factor then takes the side with fewer samples.
+
+    ``finish`` (optional callable): applied to the returned eigenvalues, once they are final (the
+    fast path applies it before its status read, see ``_spectrum_fast``)."""
+    return _spectrum_checked(s1, s2, n1, n2, finish)
+
+
+def _spectrum_checked(s1: Tensor, s2: Tensor, n1: Optional[int], n2: Optional[int], finish) -> Tensor:
     d = s1.shape[0]
     sing1 = n1 is not None and n1 <= d
     sing2 = n2 is not None and n2 <= d
+
+    def done(lam: Tensor) -> Tensor:
+        if finish is not None:
+            finish(lam)
+        return lam
+
     if not sing1:
-        lam, info = _spectrum_fast(s1, s2)
+        lam, info = _spectrum_fast(s1, s2, finish)
         if lam is not None:
-            return lam
+            return lam  # finish already applied (speculatively, before the clean status read)
         if info is None:  # not applicable / a grid aborted: the checked sequence
             L, info = _chol(s1)
             if info == 0:
-                return sym_eigvalsh(_lt_s_l(L, s2))
+                return done(sym_eigvalsh(_lt_s_l(L, s2)))
     if not sing2:
         # S1 singular, S2 not: S1 S2 and S2 S1 share their spectrum, so factor S2 instead
         # (one more Cholesky rather than a rank-revealing factorisation)
         L2, info2 = _chol(s2)
         if info2 == 0:
-            return sym_eigvalsh(_lt_s_l(L2, s1))
+            return done(sym_eigvalsh(_lt_s_l(L2, s1)))
     a, b = (s2, s1) if (n1 is not None and n2 is not None and n2 < n1) else (s1, s2)
     w = _pivoted_factor(a)
     if w is None:
         w = _eigh_factor(a)
     if w.shape[0] == 0:
-        return torch.zeros(0, dtype=s1.dtype, device=s1.device)
+        return done(torch.zeros(0, dtype=s1.dtype, device=s1.device))
     m = w @ (b @ w.T)
-    return sym_eigvalsh((m + m.T) / 2)
+    return done(sym_eigvalsh((m + m.T) / 2))
 
 
-def _spectrum_fast(s1: Tensor, s2: Tensor) -> "tuple[Optional[Tensor], Optional[int]]":
+def _spectrum_fast(s1: Tensor, s2: Tensor, finish=None) -> "tuple[Optional[Tensor], Optional[int]]":
     """K9d Cholesky -> triangle-aware sandwich -> K9b eigenvalues launched back to back with ONE
     host read of both kernels' status words (a host read after the Cholesky cost ~70 us of idle
     GPU, profiles/README.md round 6): (eigenvalues, 0), or (None, info != 0) when S1 is not
     positive definite, or (None, None) when the path does not apply or a grid aborted (the
-    caller then takes the checked sequence)."""
+    caller then takes the checked sequence).  ``finish`` (optional) is called on the eigenvalues
+    BEFORE the status read, so the caller's closing launch is queued behind the eigensolver
+    instead of after a host round trip (~45 us of idle GPU); when the status is bad the caller's
+    later ``finish`` of the checked result overwrites it (stream order)."""
     n = s1.shape[0]
     if not (use_native(s1) and s1.dtype == torch.float64 and s1.dim() == 2 and 3 <= n <= 2560):
         return None, None
@@ -138,6 +154,8 @@ def _spectrum_fast(s1: Tensor, s2: Tensor) -> "tuple[Optional[Tensor], Optional[
     lam = torch.empty(n, dtype=torch.float64, device=s1.device)
     if nat.sym_eigvals(m, lam, status[2:]) != 0:
         return None, None
+    if finish is not None:
+        finish(lam)  # speculative: valid when the status below is clean
     info, abort, eig = read_ints(status)
     if abort != 0:
         return None, None
@@ -460,10 +478,11 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> Tensor:
-        counts = torch.stack([self.num_real_images.reshape(()).long(), self.num_fake_images.reshape(()).long()])
-        from torcheval_amd.ops.hostread import read_ints
+        from torcheval_amd.ops.hostread import read_int
 
-        nr, nf = read_ints(counts)  # one host read for both counts
+        # two one-word reads (the first waits for the queued work, the second is ~7 us): cheaper
+        # than stacking the counts first (three small launches ahead of one read)
+        nr, nf = read_int(self.num_real_images), read_int(self.num_fake_images)
         if nr == 0 or nf == 0:
             warnings.warn(
                 "Computing FID requires at least 1 real image and 1 fake image,"
@@ -479,10 +498,13 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
             # the spectrum, then ONE launch for |mu1 - mu2|^2 + tr S1 + tr S2 - 2 sum sqrt(lam)
             from torcheval_amd.ops import native
 
-            lam = _spectrum(real_cov, fake_cov, nr, nf)
             out = torch.empty((), dtype=torch.float32, device=real_cov.device)
-            native().fid_finish(self.real_sum.contiguous(), float(nr), self.fake_sum.contiguous(), float(nf),
-                                real_cov, fake_cov, lam.contiguous(), out)
+            rs, fs = self.real_sum.contiguous(), self.fake_sum.contiguous()
+
+            def finish(lam: Tensor) -> None:
+                native().fid_finish(rs, float(nr), fs, float(nf), real_cov, fake_cov, lam.contiguous(), out)
+
+            _spectrum(real_cov, fake_cov, nr, nf, finish)
             return out
         real_mean = self.real_sum.double() / nr
         fake_mean = self.fake_sum.double() / nf
