@@ -612,6 +612,7 @@ int launch_merge_flag_slots(const float* slots, int* out, int words, int ws, hip
 // low-latency host read (hostread.hip): words <= kHostReadWords int32 from src into a pinned,
 // device-mapped host slot [seq, words...], published by a system-scope release store of seq
 constexpr int kHostReadWords = 14;
-int launch_publish_words(const int32_t* src, int words, int32_t* slot_dev, int32_t seq, hipStream_t stream);
+int launch_publish_words(const int32_t* src, int words, int32_t* slot_dev, int32_t seq, hipStream_t stream,
+                         const int32_t* src2 = nullptr, int words2 = 0);
 int launch_spin_on_flag(const int* flag, int64_t max_ms, hipStream_t stream);
 }  // namespace tea

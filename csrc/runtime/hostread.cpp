@@ -55,10 +55,14 @@ std::atomic<uint32_t> g_seq{0};
 
 // the values of a contiguous int32 CUDA tensor of <= kHostReadWords elements, as of the end of
 // the work queued before this call on the device's current stream
-std::vector<int64_t> read_small_ints(const at::Tensor& t, int64_t spin_us) {
+std::vector<int64_t> read_words(const at::Tensor& t, const at::Tensor* t2, int64_t spin_us) {
   TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kInt && t.is_contiguous() && t.numel() >= 1 &&
-                  t.numel() <= tea::kHostReadWords,
-              "read_small_ints: a contiguous int32 device tensor of 1..", tea::kHostReadWords, " elements");
+                  t.numel() + (t2 ? t2->numel() : 0) <= tea::kHostReadWords,
+              "read_small_ints: contiguous int32 device tensors of 1..", tea::kHostReadWords, " elements in all");
+  if (t2 != nullptr)
+    TORCH_CHECK(t2->is_cuda() && t2->device() == t.device() && t2->scalar_type() == at::kInt && t2->is_contiguous() &&
+                    t2->numel() >= 1,
+                "read_small_ints_pair: the second tensor must be a contiguous int32 tensor on the same device");
   c10::hip::OptionalHIPGuardMasqueradingAsCUDA guard(t.device());
   const hipStream_t s = c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
   SlotPool& p = pool();
@@ -71,8 +75,10 @@ std::vector<int64_t> read_small_ints(const at::Tensor& t, int64_t spin_us) {
   const int32_t seq = static_cast<int32_t>(seq32);
   const int slot = static_cast<int>(seq32 % kSlots);
   int32_t* hs = p.host + slot * kSlotInts;
-  const int words = static_cast<int>(t.numel());
-  TORCH_CHECK(tea::launch_publish_words(t.data_ptr<int32_t>(), words, p.dev + slot * kSlotInts, seq, s) == 0,
+  const int words1 = static_cast<int>(t.numel()), words2 = t2 ? static_cast<int>(t2->numel()) : 0;
+  const int words = words1 + words2;
+  TORCH_CHECK(tea::launch_publish_words(t.data_ptr<int32_t>(), words1, p.dev + slot * kSlotInts, seq, s,
+                                        t2 ? t2->data_ptr<int32_t>() : nullptr, words2) == 0,
               "read_small_ints: launch failed");
   const auto t0 = std::chrono::steady_clock::now();
   bool seen = false;
@@ -94,9 +100,20 @@ std::vector<int64_t> read_small_ints(const at::Tensor& t, int64_t spin_us) {
   return out;
 }
 
+std::vector<int64_t> read_small_ints(const at::Tensor& t, int64_t spin_us) { return read_words(t, nullptr, spin_us); }
+
+// two tensors' words in ONE read (one publish launch, one host wait)
+std::vector<int64_t> read_small_ints_pair(const at::Tensor& a, const at::Tensor& b, int64_t spin_us) {
+  return read_words(a, &b, spin_us);
+}
+
 }  // namespace
 
 void tea_register_hostread(pybind11::module_& m) {
+  m.def("read_small_ints_pair", &read_small_ints_pair,
+        "values of two small int32 device tensors (a's words, then b's) through one pinned-memory publish",
+        pybind11::arg("a"), pybind11::arg("b"), pybind11::arg("spin_us") = 1000,
+        pybind11::call_guard<pybind11::gil_scoped_release>());
   m.def("read_small_ints", &read_small_ints,
         "values of a small int32 device tensor through a pinned-memory publish + host spin (low latency)",
         pybind11::arg("t"), pybind11::arg("spin_us") = 1000, pybind11::call_guard<pybind11::gil_scoped_release>());

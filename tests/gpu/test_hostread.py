@@ -28,6 +28,22 @@ def test_int64_values():
     assert not hostread._fast(torch.zeros(8, dtype=torch.int64, device=DEV))  # 16 words
 
 
+def test_pair_read_matches_tolist():
+    g = torch.Generator().manual_seed(1)
+    for _ in range(20):
+        a = torch.randint(-(2**31), 2**31 - 1, (3,), generator=g, dtype=torch.int64).to(torch.int32).to(DEV)
+        b = torch.randint(-(2**31), 2**31 - 1, (2,), generator=g, dtype=torch.int64).to(torch.int32).to(DEV)
+        assert list(native().read_small_ints_pair(a, b)) == a.tolist() + b.tolist()
+        assert hostread.read_int_pair(a, b) == (a[0].item(), b[0].item())
+    # mixed dtypes / 0-d counts take the per-tensor path
+    x, y = torch.tensor(5, device=DEV), torch.tensor(7, dtype=torch.int32, device=DEV)
+    assert hostread.read_int_pair(x, y) == (5, 7)
+    t = torch.zeros(1, dtype=torch.int32, device=DEV)
+    for v in range(1, 50):  # stream order: the read sees the fill queued before it
+        t.fill_(v)
+        assert hostread.read_int_pair(t, y) == (v, 7)
+
+
 def test_sees_work_queued_before_it():
     t = torch.zeros(3, dtype=torch.int32, device=DEV)
     for v in range(1, 200):

@@ -478,11 +478,11 @@ class FrechetInceptionDistance(Metric[torch.Tensor]):
 
     @torch.inference_mode()
     def compute(self) -> Tensor:
-        from torcheval_amd.ops.hostread import read_int
+        from torcheval_amd.ops.hostread import read_int_pair
 
-        # two one-word reads (the first waits for the queued work, the second is ~7 us): cheaper
-        # than stacking the counts first (three small launches ahead of one read)
-        nr, nf = read_int(self.num_real_images), read_int(self.num_fake_images)
+        # both counts in one host read (one publish launch; stacking them first cost three small
+        # launches ahead of the read)
+        nr, nf = read_int_pair(self.num_real_images, self.num_fake_images)
         if nr == 0 or nf == 0:
             warnings.warn(
                 "Computing FID requires at least 1 real image and 1 fake image,"

@@ -51,3 +51,13 @@ def read_int(t: torch.Tensor) -> int:
     if _fast(t):
         return read_ints(t.reshape(-1)[:1])[0]
     return int(t.reshape(-1)[0].item())
+
+
+def read_int_pair(a: torch.Tensor, b: torch.Tensor) -> "tuple[int, int]":
+    """The first elements of ``a`` and ``b`` as Python ints, in ONE host read when both are int32
+    device tensors (one publish launch; two ``read_int`` calls pay two)."""
+    a1, b1 = a.reshape(-1)[:1], b.reshape(-1)[:1]
+    if a1.dtype == torch.int32 and b1.dtype == torch.int32 and a1.device == b1.device and _fast(a1):
+        w = _ops.native().read_small_ints_pair(a1, b1, _SPIN_US)
+        return int(w[0]), int(w[1])
+    return read_int(a), read_int(b)
