@@ -1078,7 +1078,10 @@ __device__ Bounds tridiag_setup(const double* __restrict__ d_in, const double* _
     // count's growth bound; every e^2 raised to at least 2^-600 (zeros included: the count is
     // then exact for a matrix within 2^-300 of this one, far below rounding)
     const double sp = fmax(fabs(lo), fabs(hi));
-    if (sp > 0.0 && sp <= DBL_MAX) {
+    if (sp == 0.0) {  // the zero matrix: only the e^2 floor (every minor would be an exact zero)
+      for (int k = t; k < n; k += kThreads) e2[k] = 0x1p-600;
+      emax = 0x1p-600;
+    } else if (sp <= DBL_MAX) {
       const int ex = static_cast<int>((__double_as_longlong(sp) >> 52) & 0x7ff) - 1023;
       if (ex > -1000) {
         const double sc = ldexp(1.0, -ex), sc2 = sc * sc;
